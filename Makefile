@@ -1,0 +1,28 @@
+# Build libppfit.so (HIP, gfx950) in-tree.  `make -j8`; `make clean`.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := pulseportraiture_amd/csrc
+OUT := pulseportraiture_amd/lib/libppfit.so
+SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_api.cpp
+HDRS := $(CSRC)/ppf_device.hpp $(CSRC)/ppf_internal.hpp include/ppfit.h
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+            -ffp-contract=fast -munsafe-fp-atomics
+
+OBJS := $(CSRC)/ppf_kernels.o $(CSRC)/ppf_api.o
+
+all: $(OUT)
+
+$(CSRC)/ppf_kernels.o: $(CSRC)/ppf_kernels.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/ppf_api.o: $(CSRC)/ppf_api.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OUT): $(OBJS)
+	@mkdir -p $(dir $(OUT))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+
+clean:
+	rm -f $(OBJS) $(OUT)
+
+.PHONY: all clean

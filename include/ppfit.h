@@ -1,0 +1,200 @@
+/*
+ * ppfit.h -- C ABI of libppfit, the MI355X (gfx950) wideband FFTFIT engine.
+ *
+ * Drop-in boundary for the PulsePortraiture hot path.
+ * The reference has no FFI: each entry point below replaces a Python/NumPy
+ * routine of the reference and is bound from Python with ctypes
+ * (pulseportraiture_amd/_lib.py; see INTEGRATION.md for the binding a
+ * PulsePortraiture maintainer would add).
+ *
+ * Conventions
+ *   - Every array pointer is a DEVICE pointer (hipMalloc / torch.cuda memory)
+ *     unless stated otherwise; arrays are C-contiguous.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All
+ *     calls are asynchronous on that stream; they never synchronise the
+ *     device and never allocate device memory except the per-context
+ *     twiddle-table cache (created on first use of an nbin).
+ *   - Return value: PPF_OK (0) or a negative PPF_E* code; ppf_last_error()
+ *     gives the message.  Per-sub-integration numerical outcomes are reported
+ *     in ppf_result.status, never by aborting the batch.
+ *   - nbin must be a power of two in [32, 8192].
+ *   - Contexts are thread-compatible, not thread-safe.
+ */
+#ifndef PPFIT_H
+#define PPFIT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPF_ABI_VERSION 1
+
+enum ppf_error {
+    PPF_OK = 0,
+    PPF_EINVAL = -1,   /* bad argument / shape */
+    PPF_EHIP = -2,     /* HIP runtime error */
+    PPF_ENOMEM = -3,   /* workspace too small */
+    PPF_EUNSUP = -4    /* unsupported configuration (e.g. nbin) */
+};
+
+enum ppf_dtype { PPF_F32 = 0, PPF_F64 = 1 };
+
+/* ppf_result.status values (low byte = scipy trust-region warnflag) */
+enum ppf_status {
+    PPF_ST_SUCCESS = 0,      /* gradient test met (never, gtol = -1)        */
+    PPF_ST_MAXITER = 1,      /* iteration cap reached                        */
+    PPF_ST_CONVERGED = 2,    /* predicted reduction <= 0 (the usual stop)    */
+    PPF_ST_LINALG = 3,       /* subproblem failure                           */
+    PPF_ST_NO_ROOT = 0x100,  /* no positive real zero-covariance root:
+                                the reference raises ValueError here         */
+    PPF_ST_SINGULAR = 0x200, /* singular covariance (LinAlgError)            */
+    PPF_ST_NONFINITE = 0x400,/* non-finite objective encountered             */
+    PPF_ST_NOFIT = 0x800     /* no parameter to fit / no usable channel      */
+};
+
+enum ppf_mode {
+    PPF_MODE_FULL = 0,    /* pptoaslib.fit_portrait_full semantics */
+    PPF_MODE_LEGACY2 = 1  /* pplib.fit_portrait semantics (phase + DM)  */
+};
+
+/* One fixed-size record per sub-integration (all doubles, 32 of them). */
+typedef struct ppf_result {
+    double params[5];      /* phi_out, DM, GM, tau_out, alpha               */
+    double param_errs[5];
+    double nu_out[3];      /* nu_DM, nu_GM, nu_tau of the reported params   */
+    double nu_fit[3];      /* reference frequencies used inside the fit     */
+    double chi2, red_chi2, snr;
+    double fun;            /* objective at the fit (chi2 - Sd)              */
+    double Sd;             /* data power term                               */
+    double phi_guess;      /* initial phase actually used                   */
+    double nfeval;         /* objective evaluations (passes over the data)  */
+    double status;         /* ppf_status bits                               */
+    double niter;          /* trust-region iterations                       */
+    double dof;
+    double nchanx;         /* channels used                                 */
+    double x_fit_phi;      /* phi at nu_fit (before output transform)      */
+    double x_fit_tau;      /* tau parameter at nu_fit                       */
+    double reserved[3];
+} ppf_result;
+
+/* Batched wideband fit: replaces pptoaslib.fit_portrait_full
+ * (pptoaslib.py:974-1144) per sub-integration, plus -- when guess != 0 --
+ * the initial-phase stage of pptoas.GetTOAs.get_TOAs (pptoas.py:461-499),
+ * and with mode == PPF_MODE_LEGACY2 pplib.fit_portrait (pplib.py:2185-2287). */
+typedef struct ppf_fit_desc {
+    int32_t nsub, nchan, nbin;
+    int32_t data_dtype;           /* PPF_F32 or PPF_F64                        */
+    const void *data;             /* [nsub][nchan][nbin]                       */
+    const double *model;          /* [nmodel][nchan][nbin]                     */
+    int32_t nmodel;
+    const int32_t *model_index;   /* [nsub] or NULL (all use model 0)          */
+    const uint8_t *chan_mask;     /* [nsub][nchan], 1 = use; NULL = all        */
+    const double *freqs;          /* [nsub][nchan] MHz                         */
+    const double *P;              /* [nsub] s                                  */
+    const double *errs;           /* [nsub][nchan] time-domain sigma, or NULL:
+                                     estimated as pplib.get_noise_PS           */
+    const double *init;           /* [nsub][5] initial params                  */
+    const int32_t *fit_flags;     /* [nsub][5]                                 */
+    const double *nu_fits;        /* [nsub][3]; NaN -> mean(freqs)             */
+    const double *nu_outs;        /* [nsub][3]; NaN -> zero-covariance freq    */
+    int32_t log10_tau;
+    int32_t option;               /* get_nu_zeros option (GM cases)            */
+    int32_t is_toa;
+    int32_t mode;                 /* ppf_mode                                  */
+    int32_t max_iter;             /* <= 0: reference default 200 * 5           */
+    /* optional initial-phase stage (GetTOAs): phi_guess from the weighted,
+       DM-dedispersed mean profile (brute grid of guess_Ns points + fmin) */
+    int32_t guess;
+    const double *guess_weights;  /* [nsub][nchan]                             */
+    const double *guess_DM;       /* [nsub] DM used to dedisperse              */
+    const double *guess_tau;      /* [nsub] scattering time [rot] applied to the
+                                     mean model profile (pptoas.py:484-489), or
+                                     NULL for none                             */
+    int32_t guess_Ns;
+    /* outputs */
+    ppf_result *results;          /* [nsub]                                    */
+    double *scales;               /* [nsub][nchan] (0 for masked channels)     */
+    double *scale_errs;           /* [nsub][nchan]                             */
+    double *channel_snrs;         /* [nsub][nchan]                             */
+    double *covariance;           /* [nsub][5][5], fit block in leading corner */
+    void *workspace;
+    size_t workspace_bytes;
+} ppf_fit_desc;
+
+int ppf_abi_version(void);
+/* sizeof(ppf_fit_desc) / sizeof(ppf_result) as compiled, for FFI layout checks */
+size_t ppf_sizeof_fit_desc(void);
+size_t ppf_sizeof_result(void);
+
+/* context: one per device; owns twiddle tables and the error string */
+typedef struct ppf_ctx ppf_ctx;
+int ppf_create(int device, ppf_ctx **out);
+void ppf_destroy(ppf_ctx *ctx);
+const char *ppf_last_error(const ppf_ctx *ctx);
+
+/* Workspace needed by ppf_fit_batch for `desc` (only sizes/flags are read). */
+size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc);
+
+/* pptoaslib.fit_portrait_full (pptoaslib.py:974) / pptoas.get_TOAs inner loop
+ * (pptoas.py:384-533) / pplib.fit_portrait (pplib.py:2185). */
+int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream);
+
+/* Same as ppf_fit_batch with desc->mode forced to PPF_MODE_LEGACY2:
+ * pplib.fit_portrait (pplib.py:2185-2287). */
+int ppf_fit2_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream);
+
+/* Rotate rows: out_r = irfft(rfft(in_r) * exp(2 pi i k phase_r)).
+ * Replaces the FFT core of pplib.rotate_data (pplib.py:2427-2515),
+ * pplib.rotate_portrait (2518-2550), pplib.rotate_profile (2641-2652) and
+ * pptoaslib.rotate_portrait_full (pptoaslib.py:61-90); the host computes the
+ * per-row phase phase + Dconst*DM/P*(nu**-2 - nu_ref**-2) exactly as those
+ * routines do.  in: [nrows][nbin] of in_dtype; phases: [nrows] double;
+ * out: [nrows][nbin] double. */
+int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
+                     int32_t in_dtype, const void *in, const double *phases,
+                     double *out, void *stream);
+
+/* Per-row power-spectrum noise: pplib.get_noise_PS(chans=True)
+ * (pplib.py:2312-2332): sqrt(mean(|rfft(x)|^2/nbin over k >= int((1-1/frac)
+ * * nharm))).  in: [nrows][nbin]; out: [nrows]. */
+int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
+                    int32_t in_dtype, const void *in, int32_t frac,
+                    double *out, void *stream);
+
+/* Batched 1-D FFTFIT: pplib.fit_phase_shift (pplib.py:2136-2182): brute
+ * force over Ns points of [lo, hi] then Nelder-Mead (scipy fmin) polish.
+ * data: [nprof][nbin] (in_dtype); model: [nmodel_prof][nbin] double with
+ * model_index[nprof] (NULL -> 0); noise: [nprof] time-domain sigma or NULL
+ * (estimated); out: [nprof][8] = phase, phase_err, scale, scale_err, snr,
+ * red_chi2, nfev, status. */
+int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin,
+                          int32_t in_dtype, const void *data,
+                          const double *model, const int32_t *model_index,
+                          const double *noise, int32_t Ns, double lo,
+                          double hi, double *out, void *stream);
+
+/* Synthetic sub-integrations for benchmarks/tests (make_fake_pulsar minus
+ * PSRCHIVE, pplib.py:3355-3493): out[s][n] = rotate(model[n], -phi[s],
+ * -DM[s], P[s], freqs[n], nu_ref) + N(0, noise) with a counter-based RNG
+ * keyed by (seed, s, n).  model: [nchan][nbin]; out: [nsub][nchan][nbin]
+ * in out_dtype. */
+int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                    const double *model, const double *freqs,
+                    const double *phi, const double *DM, const double *P,
+                    double nu_ref, double noise, uint64_t seed,
+                    int32_t out_dtype, void *out, void *stream);
+
+/* Host-side (CPU) helper: real roots of a degree <= 8 polynomial, highest
+ * power first, with np.roots semantics (companion-matrix eigenvalues with an
+ * exactly zero imaginary part; pptoaslib.py:834-836, 902-904).  Returns the
+ * root count or a negative value on failure.  The same code runs on the
+ * device inside ppf_fit_batch; this export exists for CPU tests. */
+int ppf_poly_real_roots_host(const double *coeffs, int deg, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPFIT_H */

@@ -1,0 +1,318 @@
+// ppf_api.cpp -- C ABI of libppfit (include/ppfit.h): validation, workspace
+// carving, twiddle-table cache and kernel sequencing.  No compute here.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+
+#include "../../include/ppfit.h"
+#include "ppf_internal.hpp"
+#include "ppf_device.hpp"
+
+struct ppf_ctx {
+    int device;
+    std::string err;
+    std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
+};
+
+namespace {
+
+int fail(ppf_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+int hip_fail(ppf_ctx *ctx, hipError_t e, const char *where) {
+    return fail(ctx, PPF_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+bool pow2_in_range(int nbin) {
+    return nbin >= 32 && nbin <= 8192 && (nbin & (nbin - 1)) == 0;
+}
+
+int ilog2(int n) {
+    int l = 0;
+    while ((1 << l) < n) ++l;
+    return l;
+}
+
+// get_noise_PS cut: int((1 - frac**-1) * nharm)  (pplib.py:2330)
+int noise_kc(int nharm, int frac) {
+    return (int)((1.0 - std::pow((double)frac, -1.0)) * (double)nharm);
+}
+
+int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const double2 **T2) {
+    auto it = ctx->tw.find(nbin);
+    if (it == ctx->tw.end()) {
+        const int N = nbin / 2;
+        double2 *p = nullptr;
+        hipError_t e = hipMalloc(&p, sizeof(double2) * 2 * (size_t)N);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(twiddles)");
+        e = ppf::launch_twiddles(N, p, p + N, st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "k_twiddles");
+        it = ctx->tw.emplace(nbin, p).first;
+    }
+    *T = it->second;
+    *T2 = it->second + nbin / 2;
+    return PPF_OK;
+}
+
+struct FitLayout {
+    size_t M, X, chan, stats, x0, gR, gM, gw, total;
+    int nblk, cb;
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+FitLayout fit_layout(const ppf_fit_desc *d) {
+    FitLayout L{};
+    const size_t nharm = (size_t)d->nbin / 2 + 1;
+    const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
+    L.cb = d->nchan < 32 ? d->nchan : 32;
+    L.nblk = (d->nchan + L.cb - 1) / L.cb;
+    size_t o = 0;
+    L.M = o;     o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
+    L.X = o;     o += align256(sizeof(double2) * nsub * nchan * nharm);
+    L.chan = o;  o += align256(sizeof(double) * nsub * nchan * 4);
+    L.stats = o; o += align256(sizeof(double) * nsub * 2 * nchan * 10);
+    L.x0 = o;    o += align256(sizeof(double) * nsub * 8);
+    if (d->guess) {
+        L.gR = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
+        L.gM = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
+        L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblk * 2);
+    }
+    L.total = o;
+    return L;
+}
+
+int check_fit_desc(ppf_ctx *ctx, const ppf_fit_desc *d) {
+    if (!d) return fail(ctx, PPF_EINVAL, "null descriptor");
+    if (d->nsub < 1 || d->nchan < 1) return fail(ctx, PPF_EINVAL, "nsub=%d nchan=%d", d->nsub, d->nchan);
+    if (!pow2_in_range(d->nbin))
+        return fail(ctx, PPF_EUNSUP, "nbin=%d: must be a power of two in [32, 8192]", d->nbin);
+    if (d->data_dtype != PPF_F32 && d->data_dtype != PPF_F64)
+        return fail(ctx, PPF_EINVAL, "data_dtype=%d", d->data_dtype);
+    if (d->nmodel < 1) return fail(ctx, PPF_EINVAL, "nmodel=%d", d->nmodel);
+    if (!d->data || !d->model || !d->freqs || !d->P || !d->init || !d->fit_flags || !d->nu_fits ||
+        !d->nu_outs || !d->results || !d->scales || !d->scale_errs || !d->channel_snrs ||
+        !d->covariance)
+        return fail(ctx, PPF_EINVAL, "required pointer is NULL");
+    if (d->mode != PPF_MODE_FULL && d->mode != PPF_MODE_LEGACY2)
+        return fail(ctx, PPF_EINVAL, "mode=%d", d->mode);
+    if (d->guess) {
+        if (!d->guess_weights || !d->guess_DM) return fail(ctx, PPF_EINVAL, "guess needs weights and DM");
+        if (d->guess_Ns < 1 || d->guess_Ns > 65536) return fail(ctx, PPF_EINVAL, "guess_Ns=%d", d->guess_Ns);
+    }
+    if (!d->workspace) return fail(ctx, PPF_EINVAL, "workspace is NULL");
+    FitLayout L = fit_layout(d);
+    if (d->workspace_bytes < L.total)
+        return fail(ctx, PPF_ENOMEM, "workspace %zu < %zu bytes", d->workspace_bytes, L.total);
+    return PPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppf_abi_version(void) { return PPF_ABI_VERSION; }
+size_t ppf_sizeof_fit_desc(void) { return sizeof(ppf_fit_desc); }
+size_t ppf_sizeof_result(void) { return sizeof(ppf_result); }
+
+int ppf_create(int device, ppf_ctx **out) {
+    if (!out) return PPF_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return PPF_EHIP;
+    if (device < 0 || device >= n) return PPF_EINVAL;
+    ppf_ctx *c = new ppf_ctx();
+    c->device = device;
+    *out = c;
+    return PPF_OK;
+}
+
+void ppf_destroy(ppf_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    for (auto &kv : ctx->tw) hipFree(kv.second);
+    delete ctx;
+}
+
+const char *ppf_last_error(const ppf_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc) {
+    if (!desc || desc->nsub < 1 || desc->nchan < 1 || !pow2_in_range(desc->nbin)) return 0;
+    return fit_layout(desc).total;
+}
+
+int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    int rc = check_fit_desc(ctx, d);
+    if (rc) return rc;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    if ((rc = twiddles(ctx, d->nbin, st, &T, &T2))) return rc;
+    const FitLayout L = fit_layout(d);
+    char *ws = (char *)d->workspace;
+    double2 *Mft = (double2 *)(ws + L.M);
+    const int nharm = d->nbin / 2 + 1;
+    const int kc = noise_kc(nharm, 4);
+
+    ppf::RfftArgs ra{d->nbin, ilog2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
+    if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_rfft_rows");
+
+    ppf::XspecArgs xa{};
+    xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = ilog2(d->nbin / 2);
+    xa.kc = kc; xa.nblk = L.nblk; xa.cb = L.cb; xa.dtype = d->data_dtype;
+    xa.data = d->data; xa.Mft = Mft; xa.model_index = d->model_index; xa.mask = d->chan_mask;
+    xa.errs = d->errs; xa.freqs = d->freqs; xa.P = d->P; xa.T = T; xa.T2 = T2;
+    xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);
+    xa.guess = d->guess; xa.guess_weights = d->guess_weights; xa.guess_DM = d->guess_DM;
+    xa.gR = d->guess ? (double2 *)(ws + L.gR) : nullptr;
+    xa.gM = d->guess ? (double2 *)(ws + L.gM) : nullptr;
+    xa.gw = d->guess ? (double *)(ws + L.gw) : nullptr;
+    if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
+
+    if (d->guess) {
+        ppf::GuessArgs ga{};
+        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.kc = kc; ga.nblk = L.nblk;
+        ga.Ns = d->guess_Ns; ga.mask = d->chan_mask; ga.freqs = d->freqs; ga.P = d->P;
+        ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau; ga.nu_fits = d->nu_fits; ga.gR = xa.gR; ga.gM = xa.gM;
+        ga.gw = xa.gw; ga.x0 = (double *)(ws + L.x0);
+        if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
+    }
+
+    ppf::SolveArgs sa{};
+    sa.nsub = d->nsub; sa.nchan = d->nchan; sa.nbin = d->nbin;
+    sa.X = xa.X; sa.Mft = Mft; sa.model_index = d->model_index; sa.chan = xa.chan;
+    sa.freqs = d->freqs; sa.P = d->P; sa.mask = d->chan_mask; sa.init = d->init;
+    sa.fit_flags = d->fit_flags; sa.nu_fits = d->nu_fits; sa.nu_outs = d->nu_outs;
+    sa.log10_tau = d->log10_tau; sa.option = d->option; sa.is_toa = d->is_toa; sa.mode = d->mode;
+    sa.max_iter = d->max_iter; sa.guess = d->guess; sa.x0 = (double *)(ws + L.x0);
+    sa.stats = (double *)(ws + L.stats); sa.results = d->results; sa.scales = d->scales;
+    sa.scale_errs = d->scale_errs; sa.channel_snrs = d->channel_snrs; sa.covariance = d->covariance;
+    sa.any_plain = 1;
+    sa.any_scat = 1;
+    if ((e = ppf::launch_solve(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_solve");
+    return PPF_OK;
+}
+
+int ppf_fit2_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream) {
+    if (!desc) return fail(ctx, PPF_EINVAL, "null descriptor");
+    ppf_fit_desc d = *desc;
+    d.mode = PPF_MODE_LEGACY2;
+    return ppf_fit_batch(ctx, &d, stream);
+}
+
+int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
+                     const double *phases, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nrows < 0 || (nrows > 0 && (!in || !phases || !out)))
+        return fail(ctx, PPF_EINVAL, "bad rotate arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (nrows == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    ppf::RotateArgs a{nbin, ilog2(nbin / 2), in_dtype, in, phases, T, T2, out};
+    if ((e = ppf::launch_rotate(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_rotate");
+    return PPF_OK;
+}
+
+int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
+                    int32_t frac, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nrows < 0 || frac < 1 || (nrows > 0 && (!in || !out)))
+        return fail(ctx, PPF_EINVAL, "bad noise arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (nrows == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    ppf::NoiseArgs a{nbin, ilog2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
+    if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise");
+    return PPF_OK;
+}
+
+int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_dtype,
+                          const void *data, const double *model, const int32_t *model_index,
+                          const double *noise, int32_t Ns, double lo, double hi, double *out,
+                          void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nprof < 0 || Ns < 1 || Ns > 65536 || (nprof > 0 && (!data || !model || !out)))
+        return fail(ctx, PPF_EINVAL, "bad phase-shift arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (nprof == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    ppf::PhaseShiftArgs a{};
+    a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
+    a.Ns = Ns; a.lo = lo; a.hi = hi; a.data = data; a.model = model; a.model_index = model_index;
+    a.noise = noise; a.T = T; a.T2 = T2; a.out = out;
+    if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
+    return PPF_OK;
+}
+
+int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, const double *model,
+                    const double *freqs, const double *phi, const double *DM, const double *P,
+                    double nu_ref, double noise, uint64_t seed, int32_t out_dtype, void *out,
+                    void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nsub < 0 || nchan < 1 || (nsub > 0 && (!model || !freqs || !phi || !DM || !P || !out)))
+        return fail(ctx, PPF_EINVAL, "bad synth arguments");
+    if (out_dtype != PPF_F32 && out_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "out_dtype");
+    if (nsub == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    // model spectra into a temporary buffer owned by this call
+    double2 *Mft = nullptr;
+    const size_t nharm = (size_t)nbin / 2 + 1;
+    e = hipMallocAsync((void **)&Mft, sizeof(double2) * nchan * nharm, st);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMallocAsync(synth)");
+    ppf::RfftArgs ra{nbin, ilog2(nbin / 2), PPF_F64, model, T, T2, Mft};
+    if ((e = ppf::launch_rfft_rows(ra, nchan, st)) != hipSuccess) return hip_fail(ctx, e, "k_rfft_rows");
+    ppf::SynthArgs a{};
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = out_dtype;
+    a.Mft = Mft; a.freqs = freqs; a.phi = phi; a.DM = DM; a.P = P; a.nu_ref = nu_ref;
+    a.noise = noise; a.seed = seed; a.T = T; a.T2 = T2; a.out = out;
+    if ((e = ppf::launch_synth(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_synth");
+    hipFreeAsync(Mft, st);
+    return PPF_OK;
+}
+
+int ppf_poly_real_roots_host(const double *coeffs, int deg, double *out) {
+    if (!coeffs || !out || deg < 0 || deg > 8) return -2;
+    return ppf::poly_real_roots(coeffs, deg, out);
+}
+
+}  // extern "C"

@@ -1,0 +1,451 @@
+// ppf_device.hpp -- device building blocks of the gfx950 wideband FFTFIT engine.
+//
+// Complex fp64 helpers, wave64/workgroup reductions, an LDS-resident Stockham
+// radix-4/2 FFT shared by every FFT-using kernel, the real<->half-length
+// complex FFT packing, the scipy trust-ncg replica used by the solver and a
+// companion-matrix polynomial root finder (np.roots replacement for the
+// zero-covariance GM cases).  Everything is fp64: nothing on this path is a
+// dense contraction, so there is no MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ppf {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kTwoPi = 6.28318530717958647692;
+constexpr double kDconst = 1.0 / 0.000241;   // pplib.py:64-67 (Dconst_trad)
+constexpr double kLn10 = 2.30258509299404568402;
+constexpr int kBlock = 256;                  // threads per workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxBfly = 4;                  // radix-4 butterflies / thread / pass
+
+// ---------------------------------------------------------------------------
+// complex fp64
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ double2 cmk(double r, double i) {
+    double2 z; z.x = r; z.y = i; return z;
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return cmk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return cmk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return cmk(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return cmk(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
+    return cmk(fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -a.x * b.y));
+}
+__device__ __forceinline__ double2 cconj(double2 a) { return cmk(a.x, -a.y); }
+__device__ __forceinline__ double cabs2(double2 a) { return fma(a.x, a.x, a.y * a.y); }
+
+// exp(2 pi i t) with exact argument reduction of t to [-1/2, 1/2].
+__device__ __forceinline__ double2 cexp2pi(double t) {
+    double r = t - rint(t);
+    double s, c;
+    sincospi(2.0 * r, &s, &c);
+    return cmk(c, s);
+}
+
+// ---------------------------------------------------------------------------
+// reductions (fixed order -> bitwise reproducible)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Sum K values per thread over the whole block; result valid in every thread.
+// scratch must hold kWaves*K doubles.  Contains two __syncthreads().
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double *scratch) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) scratch[wave * K + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double s = 0.0;
+        for (int w = 0; w < kWaves; ++w) s += scratch[w * K + i];
+        v[i] = s;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// LDS FFT (Stockham autosort, radix-4 with one leading radix-2 pass when
+// log2 N is odd).  In place in buf[0..N); every thread of the block must call
+// it (it synchronises).  T[t] = exp(-2 pi i t / N), t < N (global, cached).
+// inverse: exp(+...) kernel, no 1/N scaling.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 twid(const double2 *__restrict__ T, int idx, bool inverse) {
+    double2 w = T[idx];
+    return inverse ? cconj(w) : w;
+}
+
+__device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, bool inverse) {
+    const int N = 1 << log2N;
+    const int tid = threadIdx.x;
+    int L = 1;
+    if (log2N & 1) {  // radix-2, L = 1: no twiddles
+        const int nb = N >> 1;
+        double2 a[2 * kMaxBfly], b[2 * kMaxBfly];
+#pragma unroll
+        for (int q = 0; q < 2 * kMaxBfly; ++q) {
+            int j = tid + q * kBlock;
+            if (j < nb) { a[q] = buf[j]; b[q] = buf[j + nb]; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 2 * kMaxBfly; ++q) {
+            int j = tid + q * kBlock;
+            if (j < nb) {
+                buf[2 * j] = cadd(a[q], b[q]);
+                buf[2 * j + 1] = csub(a[q], b[q]);
+            }
+        }
+        __syncthreads();
+        L = 2;
+    }
+    const int nb = N >> 2;
+    while (L < N) {
+        const int tstride = N / (4 * L);
+        double2 x[kMaxBfly][4];
+#pragma unroll
+        for (int q = 0; q < kMaxBfly; ++q) {
+            int j = tid + q * kBlock;
+            if (j < nb) {
+                int k = j & (L - 1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[q][r] = buf[j + r * nb];
+                if (k) {
+                    x[q][1] = cmul(x[q][1], twid(T, k * tstride, inverse));
+                    x[q][2] = cmul(x[q][2], twid(T, 2 * k * tstride, inverse));
+                    x[q][3] = cmul(x[q][3], twid(T, 3 * k * tstride, inverse));
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kMaxBfly; ++q) {
+            int j = tid + q * kBlock;
+            if (j < nb) {
+                int k = j & (L - 1);
+                double2 s02 = cadd(x[q][0], x[q][2]), d02 = csub(x[q][0], x[q][2]);
+                double2 s13 = cadd(x[q][1], x[q][3]), d13 = csub(x[q][1], x[q][3]);
+                // forward: y1 = d02 - i d13, y3 = d02 + i d13
+                double2 id13 = inverse ? cmk(-d13.y, d13.x) : cmk(d13.y, -d13.x);
+                int o = (j - k) * 4 + k;
+                buf[o] = cadd(s02, s13);
+                buf[o + L] = cadd(d02, id13);
+                buf[o + 2 * L] = csub(s02, s13);
+                buf[o + 3 * L] = csub(d02, id13);
+            }
+        }
+        __syncthreads();
+        L <<= 2;
+    }
+}
+
+// Real FFT post-pass: X_k (k = 0..N) from Z = FFT_N(x_even + i x_odd).
+// T2[k] = exp(-i pi k / N), k < N.
+__device__ __forceinline__ double2 rfft_bin(const double2 *buf, int N, const double2 *__restrict__ T2, int k) {
+    double2 zk = buf[k & (N - 1)];
+    double2 zc = cconj(buf[(N - k) & (N - 1)]);
+    double2 e = cscale(cadd(zk, zc), 0.5);
+    double2 o = cscale(csub(zk, zc), 0.5);       // (Z_k - conj Z_{N-k}) / 2
+    double2 w = (k < N) ? T2[k] : cmk(-1.0, 0.0);
+    // X_k = e - i w o
+    double2 wo = cmul(w, o);
+    return cmk(e.x + wo.y, e.y - wo.x);
+}
+
+// Inverse real FFT pre-pass: Z_k (k < N) from X_0..X_N (imaginary parts of
+// X_0 and X_N ignored, as numpy.fft.irfft does).  Xk, XNk = X_k, X_{N-k}.
+__device__ __forceinline__ double2 irfft_prebin(double2 Xk, double2 XNk, double2 w /*T2[k]*/) {
+    double2 xc = cconj(XNk);
+    double2 e = cscale(cadd(Xk, xc), 0.5);
+    double2 d = cscale(csub(Xk, xc), 0.5);
+    double2 o = cmul(cconj(w), d);               // exp(+i pi k/N) (X_k - conj X_{N-k}) / 2
+    return cmk(e.x - o.y, e.y + o.x);            // E + i O
+}
+
+// ---------------------------------------------------------------------------
+// scipy trust-ncg replica (scipy/optimize/_trustregion.py:_minimize_trust_region
+// with _trustregion_ncg.py:CGSteihaugSubproblem), on the fitted subspace.
+// ---------------------------------------------------------------------------
+struct TRModel {
+    double f;
+    double g[5];
+    double H[5][5];
+};
+
+__device__ __forceinline__ double dotn(const double *a, const double *b, int n) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += a[i] * b[i];
+    return s;
+}
+__device__ __forceinline__ void hessp(const TRModel &m, const double *p, double *out, int n) {
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += m.H[i][j] * p[j];
+        out[i] = s;
+    }
+}
+__device__ __forceinline__ double model_value(const TRModel &m, const double *p, int n) {
+    double Hp[5];
+    hessp(m, p, Hp, n);
+    return m.f + dotn(m.g, p, n) + 0.5 * dotn(p, Hp, n);
+}
+// || z + t d || == R  ->  (ta, tb) sorted
+__device__ __forceinline__ void boundary_t(const double *z, const double *d, double R, int n,
+                                           double &ta, double &tb) {
+    double a = dotn(d, d, n), b = 2.0 * dotn(z, d, n), c = dotn(z, z, n) - R * R;
+    double sq = sqrt(b * b - 4.0 * a * c);
+    double aux = b + copysign(sq, b);
+    double t1 = -aux / (2.0 * a), t2 = -2.0 * c / aux;
+    ta = fmin(t1, t2);
+    tb = fmax(t1, t2);
+}
+// Returns hits_boundary; p (length n) is the step.
+__device__ bool cg_steihaug(const TRModel &m, double jac_mag, double R, double *p, int n) {
+    double tol = fmin(0.5, sqrt(jac_mag)) * jac_mag;
+    for (int i = 0; i < n; ++i) p[i] = 0.0;
+    if (jac_mag < tol) return false;
+    double z[5], r[5], d[5], Bd[5];
+    for (int i = 0; i < n; ++i) { z[i] = 0.0; r[i] = m.g[i]; d[i] = -m.g[i]; }
+    for (int it = 0; it < 64; ++it) {
+        hessp(m, d, Bd, n);
+        double dBd = dotn(d, Bd, n);
+        if (dBd <= 0.0) {
+            double ta, tb;
+            boundary_t(z, d, R, n, ta, tb);
+            double pa[5], pb[5];
+            for (int i = 0; i < n; ++i) { pa[i] = z[i] + ta * d[i]; pb[i] = z[i] + tb * d[i]; }
+            bool usea = model_value(m, pa, n) < model_value(m, pb, n);
+            for (int i = 0; i < n; ++i) p[i] = usea ? pa[i] : pb[i];
+            return true;
+        }
+        double rr = dotn(r, r, n);
+        double alpha = rr / dBd;
+        double zn[5];
+        for (int i = 0; i < n; ++i) zn[i] = z[i] + alpha * d[i];
+        if (sqrt(dotn(zn, zn, n)) >= R) {
+            double ta, tb;
+            boundary_t(z, d, R, n, ta, tb);
+            for (int i = 0; i < n; ++i) p[i] = z[i] + tb * d[i];
+            return true;
+        }
+        double rn[5];
+        for (int i = 0; i < n; ++i) rn[i] = r[i] + alpha * Bd[i];
+        double rnn = dotn(rn, rn, n);
+        if (sqrt(rnn) < tol) {
+            for (int i = 0; i < n; ++i) p[i] = zn[i];
+            return false;
+        }
+        double beta = rnn / rr;
+        for (int i = 0; i < n; ++i) { d[i] = -rn[i] + beta * d[i]; z[i] = zn[i]; r[i] = rn[i]; }
+    }
+    for (int i = 0; i < n; ++i) p[i] = z[i];
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// small dense inverse (Gauss-Jordan, partial pivoting); returns false if
+// singular.  n <= 5.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline bool invert_small(double (*A)[5], double (*Ainv)[5], int n) {
+    double M[5][10];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 2 * n; ++j) M[i][j] = (j < n) ? A[i][j] : (j - n == i ? 1.0 : 0.0);
+    for (int c = 0; c < n; ++c) {
+        int piv = c;
+        double best = fabs(M[c][c]);
+        for (int r = c + 1; r < n; ++r)
+            if (fabs(M[r][c]) > best) { best = fabs(M[r][c]); piv = r; }
+        if (best == 0.0 || !(best == best)) return false;
+        if (piv != c)
+            for (int j = 0; j < 2 * n; ++j) { double t = M[c][j]; M[c][j] = M[piv][j]; M[piv][j] = t; }
+        double inv = 1.0 / M[c][c];
+        for (int j = 0; j < 2 * n; ++j) M[c][j] *= inv;
+        for (int r = 0; r < n; ++r) {
+            if (r == c) continue;
+            double f = M[r][c];
+            if (f != 0.0)
+                for (int j = 0; j < 2 * n; ++j) M[r][j] -= f * M[c][j];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) Ainv[i][j] = M[i][j + n];
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Polynomial roots as np.roots: eigenvalues of the companion matrix
+// (balanced, then Francis double-shift QR on the Hessenberg form).  Only the
+// real roots (exact zero imaginary part, as LAPACK reports them) are returned.
+// coeffs[0..deg] highest power first.  Returns the number of real roots.
+// ---------------------------------------------------------------------------
+#define PPF_SIGN(a, b) ((b) >= 0.0 ? fabs(a) : -fabs(a))
+
+__host__ __device__ inline void balance_small(double (*a)[8], int n) {
+    const double radix = 2.0, sqrdx = radix * radix;
+    int last = 0;
+    while (last == 0) {
+        last = 1;
+        for (int i = 0; i < n; ++i) {
+            double r = 0.0, c = 0.0;
+            for (int j = 0; j < n; ++j)
+                if (j != i) { c += fabs(a[j][i]); r += fabs(a[i][j]); }
+            if (c != 0.0 && r != 0.0) {
+                double g = r / radix, f = 1.0, s = c + r;
+                while (c < g) { f *= radix; c *= sqrdx; }
+                g = r * radix;
+                while (c > g) { f /= radix; c /= sqrdx; }
+                if ((c + r) / f < 0.95 * s) {
+                    last = 0;
+                    g = 1.0 / f;
+                    for (int j = 0; j < n; ++j) a[i][j] *= g;
+                    for (int j = 0; j < n; ++j) a[j][i] *= f;
+                }
+            }
+        }
+    }
+}
+
+// a: upper Hessenberg n x n (n <= 8), destroyed.  wr/wi eigenvalues.
+// Returns false on non-convergence.
+__host__ __device__ inline bool hqr_small(double (*a)[8], int n, double *wr, double *wi) {
+    int nn, m, l, k, j, its, i, mmin;
+    double z = 0, y, x, w, v, u, t, s, r = 0, q = 0, p = 0, anorm = 0.0;
+    for (i = 0; i < n; ++i)
+        for (j = (i - 1 > 0 ? i - 1 : 0); j < n; ++j) anorm += fabs(a[i][j]);
+    nn = n - 1;
+    t = 0.0;
+    while (nn >= 0) {
+        its = 0;
+        do {
+            for (l = nn; l >= 1; --l) {
+                s = fabs(a[l - 1][l - 1]) + fabs(a[l][l]);
+                if (s == 0.0) s = anorm;
+                if (fabs(a[l][l - 1]) + s == s) { a[l][l - 1] = 0.0; break; }
+            }
+            x = a[nn][nn];
+            if (l == nn) {
+                wr[nn] = x + t;
+                wi[nn--] = 0.0;
+            } else {
+                y = a[nn - 1][nn - 1];
+                w = a[nn][nn - 1] * a[nn - 1][nn];
+                if (l == nn - 1) {
+                    p = 0.5 * (y - x);
+                    q = p * p + w;
+                    z = sqrt(fabs(q));
+                    x += t;
+                    if (q >= 0.0) {
+                        z = p + PPF_SIGN(z, p);
+                        wr[nn - 1] = wr[nn] = x + z;
+                        if (z != 0.0) wr[nn] = x - w / z;
+                        wi[nn - 1] = wi[nn] = 0.0;
+                    } else {
+                        wr[nn - 1] = wr[nn] = x + p;
+                        wi[nn - 1] = -(wi[nn] = z);
+                    }
+                    nn -= 2;
+                } else {
+                    if (its == 60) return false;
+                    if (its == 10 || its == 20) {
+                        t += x;
+                        for (i = 0; i <= nn; ++i) a[i][i] -= x;
+                        s = fabs(a[nn][nn - 1]) + fabs(a[nn - 1][nn - 2]);
+                        y = x = 0.75 * s;
+                        w = -0.4375 * s * s;
+                    }
+                    ++its;
+                    for (m = nn - 2; m >= l; --m) {
+                        z = a[m][m];
+                        r = x - z;
+                        s = y - z;
+                        p = (r * s - w) / a[m + 1][m] + a[m][m + 1];
+                        q = a[m + 1][m + 1] - z - r - s;
+                        r = a[m + 2][m + 1];
+                        s = fabs(p) + fabs(q) + fabs(r);
+                        p /= s; q /= s; r /= s;
+                        if (m == l) break;
+                        u = fabs(a[m][m - 1]) * (fabs(q) + fabs(r));
+                        v = fabs(p) * (fabs(a[m - 1][m - 1]) + fabs(z) + fabs(a[m + 1][m + 1]));
+                        if (u + v == v) break;
+                    }
+                    for (i = m + 2; i <= nn; ++i) {
+                        a[i][i - 2] = 0.0;
+                        if (i != m + 2) a[i][i - 3] = 0.0;
+                    }
+                    for (k = m; k <= nn - 1; ++k) {
+                        if (k != m) {
+                            p = a[k][k - 1];
+                            q = a[k + 1][k - 1];
+                            r = 0.0;
+                            if (k != nn - 1) r = a[k + 2][k - 1];
+                            if ((x = fabs(p) + fabs(q) + fabs(r)) != 0.0) { p /= x; q /= x; r /= x; }
+                        }
+                        if ((s = PPF_SIGN(sqrt(p * p + q * q + r * r), p)) != 0.0) {
+                            if (k == m) {
+                                if (l != m) a[k][k - 1] = -a[k][k - 1];
+                            } else {
+                                a[k][k - 1] = -s * x;
+                            }
+                            p += s;
+                            x = p / s; y = q / s; z = r / s; q /= p; r /= p;
+                            for (j = k; j <= nn; ++j) {
+                                p = a[k][j] + q * a[k + 1][j];
+                                if (k != nn - 1) { p += r * a[k + 2][j]; a[k + 2][j] -= p * z; }
+                                a[k + 1][j] -= p * y;
+                                a[k][j] -= p * x;
+                            }
+                            mmin = nn < k + 3 ? nn : k + 3;
+                            for (i = l; i <= mmin; ++i) {
+                                p = x * a[i][k] + y * a[i][k + 1];
+                                if (k != nn - 1) { p += z * a[i][k + 2]; a[i][k + 2] -= p * r; }
+                                a[i][k + 1] -= p * q;
+                                a[i][k] -= p;
+                            }
+                        }
+                    }
+                }
+            }
+        } while (l < nn - 1);
+    }
+    return true;
+}
+
+// Real roots of sum_i c[i] x^(deg-i).  out receives them; returns count, or
+// -1 if the QR iteration failed.
+__host__ __device__ inline int poly_real_roots(const double *c, int deg, double *out) {
+    int lead = 0;
+    while (lead <= deg && c[lead] == 0.0) ++lead;
+    if (lead > deg) return 0;
+    int trail = 0;
+    while (deg - trail > lead && c[deg - trail] == 0.0) ++trail;
+    int n = deg - lead - trail;  // companion size
+    int cnt = 0;
+    for (int i = 0; i < trail; ++i) out[cnt++] = 0.0;
+    if (n <= 0) return cnt;
+    double a[8][8];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) a[i][j] = 0.0;
+    for (int j = 0; j < n; ++j) a[0][j] = -c[lead + 1 + j] / c[lead];
+    for (int i = 1; i < n; ++i) a[i][i - 1] = 1.0;
+    balance_small(a, n);
+    double wr[8], wi[8];
+    if (!hqr_small(a, n, wr, wi)) return -1;
+    for (int i = 0; i < n; ++i)
+        if (wi[i] == 0.0) out[cnt++] = wr[i];
+    return cnt;
+}
+
+}  // namespace ppf

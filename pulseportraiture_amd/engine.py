@@ -1,0 +1,248 @@
+"""Batched device engine: torch tensors in, libppfit kernels, torch tensors out.
+
+PyTorch supplies device memory, the current HIP stream and (in dist.py) the
+RCCL communicator; all arithmetic happens in libppfit's HIP kernels.  Every
+function here accepts numpy arrays or torch tensors (host or device) and
+returns device tensors; the drop-in modules (pplib / pptoaslib / pptoas)
+convert to the reference's numpy/DataBunch forms.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+DEVICE_TYPE = "cuda"   # torch's name for HIP devices on ROCm
+
+
+def device(dev=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("pulseportraiture_amd needs a HIP device "
+                           "(torch.cuda.is_available() is False); there is "
+                           "no CPU fallback")
+    if dev is None:
+        return torch.device(DEVICE_TYPE, torch.cuda.current_device())
+    dev = torch.device(dev)
+    if dev.type != DEVICE_TYPE:
+        raise ValueError("device must be a HIP device, got %s" % dev)
+    return dev if dev.index is not None else torch.device(
+        DEVICE_TYPE, torch.cuda.current_device())
+
+
+def to_dev(x, dev, dtype):
+    """Contiguous device tensor of dtype (None passes through)."""
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype).to(dev)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _data_dtype(x):
+    if isinstance(x, torch.Tensor):
+        return torch.float32 if x.dtype == torch.float32 else torch.float64
+    return torch.float32 if np.asarray(x).dtype == np.float32 else \
+        torch.float64
+
+
+def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
+              nu_outs=None, errs=None, chan_mask=None, model_index=None,
+              log10_tau=False, option=0, is_toa=True, mode=_lib.PPF_MODE_FULL,
+              max_iter=0, guess=False, guess_weights=None, guess_DM=None,
+              guess_Ns=100, guess_tau=None, dev=None, workspace=None):
+    """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
+    model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
+    P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
+
+    Returns a dict of device tensors: results [nsub, 32] (see
+    _lib.RESULT_INDEX), scales/scale_errs/channel_snrs [nsub, nchan],
+    covariance [nsub, 5, 5], and the workspace (reusable)."""
+    dev = device(dev)
+    f64 = torch.float64
+    data_t = to_dev(data, dev, _data_dtype(data))
+    if data_t.dim() != 3:
+        raise ValueError("data must be [nsub, nchan, nbin]")
+    nsub, nchan, nbin = data_t.shape
+    model_t = to_dev(model, dev, f64)
+    if model_t.dim() == 2:
+        model_t = model_t.unsqueeze(0)
+    if model_t.shape[1:] != (nchan, nbin):
+        raise ValueError("model shape %s != [*, %d, %d]" %
+                         (tuple(model_t.shape), nchan, nbin))
+    nmodel = model_t.shape[0]
+    freqs_t = to_dev(freqs, dev, f64).reshape(-1)
+    if freqs_t.numel() == nchan:
+        freqs_t = freqs_t.repeat(nsub)
+    freqs_t = freqs_t.reshape(nsub, nchan).contiguous()
+    P_t = to_dev(P, dev, f64).reshape(-1)
+    if P_t.numel() == 1:
+        P_t = P_t.repeat(nsub)
+    init_t = to_dev(init, dev, f64).reshape(nsub, 5).contiguous()
+    flags_t = to_dev(fit_flags, dev, torch.int32).reshape(-1)
+    if flags_t.numel() == 5:
+        flags_t = flags_t.repeat(nsub)
+    flags_t = flags_t.reshape(nsub, 5).contiguous()
+    nan3 = torch.full((nsub, 3), float("nan"), dtype=f64, device=dev)
+    nu_fits_t = nan3.clone() if nu_fits is None else \
+        to_dev(nu_fits, dev, f64).reshape(nsub, 3).contiguous()
+    nu_outs_t = nan3.clone() if nu_outs is None else \
+        to_dev(nu_outs, dev, f64).reshape(nsub, 3).contiguous()
+    errs_t = None if errs is None else \
+        to_dev(errs, dev, f64).reshape(nsub, nchan).contiguous()
+    mask_t = None if chan_mask is None else \
+        to_dev(chan_mask, dev, torch.uint8).reshape(nsub, nchan).contiguous()
+    mi_t = None if model_index is None else \
+        to_dev(model_index, dev, torch.int32).reshape(nsub).contiguous()
+    gw_t = gdm_t = gtau_t = None
+    if guess:
+        if guess_tau is not None:
+            gtau_t = to_dev(guess_tau, dev, f64).reshape(-1)
+            if gtau_t.numel() == 1:
+                gtau_t = gtau_t.repeat(nsub)
+        gw_t = to_dev(guess_weights, dev, f64).reshape(nsub, nchan).contiguous()
+        gdm_t = to_dev(guess_DM, dev, f64).reshape(-1)
+        if gdm_t.numel() == 1:
+            gdm_t = gdm_t.repeat(nsub)
+    results = torch.zeros((nsub, _lib.RESULT_DOUBLES), dtype=f64, device=dev)
+    scales = torch.zeros((nsub, nchan), dtype=f64, device=dev)
+    scale_errs = torch.zeros_like(scales)
+    channel_snrs = torch.zeros_like(scales)
+    cov = torch.zeros((nsub, 5, 5), dtype=f64, device=dev)
+    d = _lib.FitDesc()
+    d.nsub, d.nchan, d.nbin = nsub, nchan, nbin
+    d.data_dtype = _lib.PPF_F32 if data_t.dtype == torch.float32 else \
+        _lib.PPF_F64
+    d.data, d.model, d.nmodel = _p(data_t), _p(model_t), nmodel
+    d.model_index, d.chan_mask = _p(mi_t), _p(mask_t)
+    d.freqs, d.P, d.errs = _p(freqs_t), _p(P_t), _p(errs_t)
+    d.init, d.fit_flags = _p(init_t), _p(flags_t)
+    d.nu_fits, d.nu_outs = _p(nu_fits_t), _p(nu_outs_t)
+    d.log10_tau, d.option, d.is_toa = int(bool(log10_tau)), int(option), \
+        int(bool(is_toa))
+    d.mode, d.max_iter = int(mode), int(max_iter)
+    d.guess, d.guess_Ns = int(bool(guess)), int(guess_Ns)
+    d.guess_weights, d.guess_DM = _p(gw_t), _p(gdm_t)
+    d.guess_tau = _p(gtau_t)
+    d.results, d.scales, d.scale_errs = _p(results), _p(scales), \
+        _p(scale_errs)
+    d.channel_snrs, d.covariance = _p(channel_snrs), _p(cov)
+    lib = _lib.load()
+    nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    if nbytes == 0:
+        raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
+                                  " (nbin must be a power of two in "
+                                  "[32, 8192])" % (nsub, nchan, nbin))
+    if workspace is None or workspace.numel() < nbytes or \
+            workspace.device != dev:
+        workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d.workspace, d.workspace_bytes = _p(workspace), workspace.numel()
+    ctx = _lib.context(dev.index)
+    _lib.check(lib.ppf_fit_batch(ctx, ctypes.byref(d), _stream(dev)), ctx)
+    # keep inputs alive until the stream has consumed them
+    keep = (data_t, model_t, freqs_t, P_t, init_t, flags_t, nu_fits_t,
+            nu_outs_t, errs_t, mask_t, mi_t, gw_t, gdm_t, gtau_t)
+    return dict(results=results, scales=scales, scale_errs=scale_errs,
+                channel_snrs=channel_snrs, covariance=cov,
+                workspace=workspace, _keep=keep)
+
+
+def rotate_rows(rows, phases, dev=None):
+    """irfft(rfft(row) * exp(2 pi i k phase)) for each row of rows [..., nbin]
+    (float64 output, same leading shape)."""
+    dev = device(dev)
+    r = to_dev(rows, dev, _data_dtype(rows))
+    shape = r.shape
+    nbin = shape[-1]
+    r2 = r.reshape(-1, nbin).contiguous()
+    ph = to_dev(phases, dev, torch.float64).reshape(-1).contiguous()
+    if ph.numel() != r2.shape[0]:
+        raise ValueError("need one phase per row")
+    out = torch.empty((r2.shape[0], nbin), dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_rotate_batch(
+        ctx, r2.shape[0], nbin,
+        _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
+        _p(r2), _p(ph), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out.reshape(shape)
+
+
+def noise_rows(rows, frac=4, dev=None):
+    """get_noise_PS per row of rows [..., nbin] -> [...] float64."""
+    dev = device(dev)
+    r = to_dev(rows, dev, _data_dtype(rows))
+    shape = r.shape
+    r2 = r.reshape(-1, shape[-1]).contiguous()
+    out = torch.empty(r2.shape[0], dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_noise_batch(
+        ctx, r2.shape[0], shape[-1],
+        _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
+        _p(r2), int(frac), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out.reshape(shape[:-1])
+
+
+def phase_shift_batch(data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
+                      model_index=None, dev=None):
+    """Batched pplib.fit_phase_shift: data [nprof, nbin], model
+    [nmodel, nbin] -> [nprof, 8] (phase, phase_err, scale, scale_err, snr,
+    red_chi2, nfev, status)."""
+    dev = device(dev)
+    d = to_dev(data, dev, _data_dtype(data))
+    if d.dim() == 1:
+        d = d.unsqueeze(0)
+    m = to_dev(model, dev, torch.float64)
+    if m.dim() == 1:
+        m = m.unsqueeze(0)
+    nz = None if noise is None else \
+        to_dev(noise, dev, torch.float64).reshape(-1).contiguous()
+    mi = None if model_index is None else \
+        to_dev(model_index, dev, torch.int32).reshape(-1).contiguous()
+    out = torch.zeros((d.shape[0], 8), dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_phase_shift_batch(
+        ctx, d.shape[0], d.shape[1],
+        _lib.PPF_F32 if d.dtype == torch.float32 else _lib.PPF_F64,
+        _p(d), _p(m), _p(mi), _p(nz), int(Ns), float(bounds[0]),
+        float(bounds[1]), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
+def synth(model, freqs, phi, DM, P, nu_ref, noise, seed, out_dtype=torch.float32,
+          dev=None):
+    """Synthetic sub-integrations [nsub, nchan, nbin] on the device."""
+    dev = device(dev)
+    m = to_dev(model, dev, torch.float64)
+    nchan, nbin = m.shape
+    f = to_dev(freqs, dev, torch.float64).reshape(-1).contiguous()
+    ph = to_dev(phi, dev, torch.float64).reshape(-1).contiguous()
+    dm = to_dev(DM, dev, torch.float64).reshape(-1).contiguous()
+    Pt = to_dev(P, dev, torch.float64).reshape(-1).contiguous()
+    nsub = ph.numel()
+    out = torch.empty((nsub, nchan, nbin), dtype=out_dtype, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_synth_batch(
+        ctx, nsub, nchan, nbin, _p(m), _p(f), _p(ph), _p(dm), _p(Pt),
+        float(nu_ref), float(noise), ctypes.c_uint64(int(seed)),
+        _lib.PPF_F32 if out_dtype == torch.float32 else _lib.PPF_F64,
+        _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
+def results_numpy(res):
+    """Device fit_batch output -> dict of numpy arrays (synchronises)."""
+    out = {k: v.detach().cpu().numpy() for k, v in res.items()
+           if isinstance(v, torch.Tensor) and k != "workspace"}
+    return out

@@ -1,0 +1,527 @@
+"""Drop-in mirror of PulsePortraiture's ``pptoas`` wideband-TOA driver.
+
+``GetTOAs.get_TOAs`` keeps the reference signature and fills the same
+attributes, but instead of fitting one sub-integration at a time it gathers
+every usable sub-integration of an archive into ONE batched device call
+(initial-phase FFTFIT + wideband fit + post-fit, ``ppf_fit_batch``) and then
+does the unchanged per-sub-integration host bookkeeping (TOA epochs, Doppler
+corrections, TOA flags, DeltaDM).  Archive I/O stays on PSRCHIVE via
+``load_data`` (host side, out of the accelerated path).
+
+Reference: /root/reference/pptoas.py (file:line cited per block).
+"""
+import time
+
+import numpy as np
+
+from . import _lib, engine
+from . import pplib as _pplib
+from .pplib import (DataBunch, file_is_type, guess_fit_freq, read_model,
+                    scattering_alpha, write_TOAs, weighted_mean,
+                    scattering_times, scattering_portrait_FT,
+                    gen_gaussian_portrait, _raise_status)
+from .pptoaslib import unpack_result, _status_message, _nu_zero_messages
+
+max_nfile = 999                    # pptoas.py:33
+rm_baseline = bool(_pplib.F0_fact)  # pptoas.py:36-39
+
+
+def load_data(filename, **kwargs):
+    """Indirection so tests / users can supply archives without PSRCHIVE."""
+    return _pplib.load_data(filename, **kwargs)
+
+
+def _MJD(days):
+    import psrchive as pr
+    return pr.MJD(days)
+
+
+class TOA(object):
+    """pptoas.py:42-84."""
+
+    def __init__(self, archive, frequency, MJD, TOA_error, telescope,
+                 telescope_code, DM=None, DM_error=None, flags={}):
+        self.archive = archive
+        self.frequency = frequency
+        self.MJD = MJD
+        self.TOA_error = TOA_error
+        self.telescope = telescope
+        self.telescope_code = telescope_code
+        self.DM = DM
+        self.DM_error = DM_error
+        self.flags = flags
+
+    def write_TOA(self, inf_is_zero=True, outfile=None):
+        write_TOAs(self, inf_is_zero=inf_is_zero, outfile=outfile,
+                   append=True)
+
+
+_ATTRS = ["obs", "doppler_fs", "nu0s", "nu_fits", "nu_refs", "ok_idatafiles",
+          "ok_isubs", "epochs", "MJDs", "Ps", "phis", "phi_errs", "TOAs",
+          "TOA_errs", "DM0s", "DMs", "DM_errs", "DeltaDM_means",
+          "DeltaDM_errs", "GMs", "GM_errs", "taus", "tau_errs", "alphas",
+          "alpha_errs", "scales", "scale_errs", "snrs", "channel_snrs",
+          "profile_fluxes", "profile_flux_errs", "fluxes", "flux_errs",
+          "flux_freqs", "red_chi2s", "channel_red_chi2s", "covariances",
+          "nfevals", "rcs", "fit_durations", "order", "TOA_list",
+          "zap_channels"]
+
+
+class GetTOAs(object):
+    """pptoas.py:87-159."""
+
+    def __init__(self, datafiles, modelfile, quiet=False):
+        if file_is_type(datafiles, "ASCII"):
+            with open(datafiles) as fh:
+                self.datafiles = [ln.rstrip("\n") for ln in fh.readlines()
+                                  if ln.strip()]
+        else:
+            self.datafiles = [datafiles]
+        if len(self.datafiles) > max_nfile:
+            print("Too many archives.  See/change max_nfile(=%d) in pptoas.py."
+                  % max_nfile)
+            raise SystemExit
+        self.is_FITS_model = file_is_type(modelfile, "FITS")
+        self.modelfile = modelfile
+        for a in _ATTRS:
+            setattr(self, a, [])
+        self.instrumental_response_dict = self.ird = \
+            {"DM": 0.0, "wids": [], "irf_types": []}
+        self.quiet = quiet
+
+    # ------------------------------------------------------------------
+    def _models(self, d, ok_isubs, fit_scat, quiet):
+        """Model portrait per sub-integration (pptoas.py:385-419), built once
+        per distinct frequency set (host precompute)."""
+        if self.is_FITS_model:
+            raise NotImplementedError("FITS (archive) templates need PSRCHIVE")
+        cache, models, index = {}, [], []
+        for isub in ok_isubs:
+            key = d.freqs[isub].tobytes()
+            if key not in cache:
+                if not fit_scat:
+                    self.model_name, self.ngauss, model = read_model(
+                        self.modelfile, d.phases, d.freqs[isub], d.Ps[isub],
+                        quiet=True)
+                else:
+                    self.model_name, self.ngauss, _ = read_model(
+                        self.modelfile, d.phases, d.freqs[isub], d.Ps[isub],
+                        quiet=True)
+                    (self.model_name, self.model_code, self.model_nu_ref,
+                     self.ngauss, self.gparams, _mff, self.alpha,
+                     _mfa) = read_model(self.modelfile, quiet=True)
+                    unscat = np.copy(self.gparams)
+                    unscat[1] = 0.0
+                    model = gen_gaussian_portrait(self.model_code, unscat, 0.0,
+                                                  d.phases, d.freqs[isub],
+                                                  self.model_nu_ref)
+                cache[key] = len(models)
+                models.append(model)
+            index.append(cache[key])
+        return np.array(models), np.array(index, dtype=np.int32)
+
+    def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None,
+                 bary=True, fit_DM=True, fit_GM=False, fit_scat=False,
+                 log10_tau=True, scat_guess=None, fix_alpha=False,
+                 print_phase=False, print_flux=False, print_parangle=False,
+                 add_instrumental_response=False, addtnl_toa_flags={},
+                 method="trust-ncg", bounds=None, nu_fits=None,
+                 show_plot=False, quiet=None):
+        """pptoas.py:161-792, batched per archive on the GPU."""
+        if quiet is None:
+            quiet = self.quiet
+        if show_plot:
+            raise NotImplementedError("plotting is outside the accelerated "
+                                      "path (SURVEY.md section 2, row 20)")
+        if add_instrumental_response and (self.ird["DM"] or
+                                          len(self.ird["wids"])):
+            raise NotImplementedError("instrumental response (SURVEY.md row "
+                                      "19) is not on the accelerated path")
+        if method not in ("trust-ncg", "Newton-CG", "TNC"):
+            print("Method '%s' is not implemented." % method)
+            raise SystemExit
+        already_warned = False
+        warning_message = \
+            "You are using an experimental functionality of pptoas!"
+        self.nfit = 1 + int(fit_DM) + int(fit_GM) + 2 * int(fit_scat) - \
+            int(fix_alpha)
+        self.fit_phi = True
+        self.fit_DM, self.fit_GM = fit_DM, fit_GM
+        self.fit_tau = self.fit_alpha = fit_scat
+        if fit_scat:
+            self.fit_alpha = not fix_alpha
+        self.fit_flags = [int(self.fit_phi), int(self.fit_DM),
+                          int(self.fit_GM), int(self.fit_tau),
+                          int(self.fit_alpha)]
+        self.log10_tau = log10_tau
+        if not fit_scat:
+            self.log10_tau = log10_tau = False
+        if self.fit_GM or fit_scat or self.fit_tau or self.fit_alpha:
+            print(warning_message)
+            already_warned = True
+        self.scat_guess = scat_guess
+        nu_ref_tuple, nu_fit_tuple = nu_refs, nu_fits
+        self.DM0, self.bary = DM0, bary
+        start = time.time()
+        tot_duration = 0.0
+        datafiles = self.datafiles if datafile is None else [datafile]
+        self.tscrunch = tscrunch
+        self.add_instrumental_response = add_instrumental_response
+        fit_flags = None    # carried across sub-ints as in pptoas.py:519-529
+        for iarch, datafile in enumerate(datafiles):
+            fit_duration = 0.0
+            try:
+                data = load_data(datafile, dedisperse=False,
+                                 dededisperse=False, tscrunch=tscrunch,
+                                 pscrunch=True, fscrunch=False,
+                                 rm_baseline=rm_baseline, flux_prof=False,
+                                 refresh_arch=False, return_arch=False,
+                                 quiet=quiet)
+                if data.dmc:
+                    if not quiet:
+                        print("%s is dedispersed (dmc = 1).  Reloading it." %
+                              datafile)
+                    data = load_data(datafile, dedisperse=False,
+                                     dededisperse=True, tscrunch=tscrunch,
+                                     pscrunch=True, fscrunch=False,
+                                     rm_baseline=rm_baseline,
+                                     flux_prof=False, refresh_arch=False,
+                                     return_arch=False, quiet=quiet)
+                if np.isnan(data.prof_SNR) or (data.prof_SNR == 0.0):
+                    print("Profile has a nan or zero  snr, must skip")
+                    continue
+                nnan = len(data.SNRs[np.isnan(data.SNRs)])
+                if nnan > 10:
+                    print("More than 10 frequency channels with nan SNR. "
+                          "Skipping it")
+                    continue
+                if nnan > 0:
+                    print("This file has %s frequency channels with a nan SNR"
+                          % nnan)
+                    print(datafile)
+                    for isub in data.ok_isubs:
+                        for ipol in range(data.npol):
+                            oc = np.array(data.ok_ichans[isub])
+                            data.ok_ichans[isub] = oc[~np.isnan(
+                                data.SNRs[isub, ipol][oc])]
+                if not len(data.ok_isubs):
+                    if not quiet:
+                        print("No subints to fit for %s.  Skipping it." %
+                              datafile)
+                    continue
+                self.ok_idatafiles.append(iarch)
+            except RuntimeError:
+                if not quiet:
+                    print("Cannot load_data(%s).  Skipping it." % datafile)
+                continue
+            d = data
+            nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
+            if d.source is None:
+                d.source = "noname"
+            obs = DataBunch(telescope=d.telescope, backend=d.backend,
+                            frontend=d.frontend)
+            nu_fits_a = list(np.zeros([nsub, 3], dtype=np.float64))
+            nu_refs_a = list(np.zeros([nsub, 3], dtype=np.float64))
+            phis = np.zeros(nsub)
+            phi_errs = np.zeros(nsub)
+            TOAs = np.zeros(nsub, dtype="object")
+            TOA_errs = np.zeros(nsub, dtype="object")
+            DMs, DM_errs = np.zeros(nsub), np.zeros(nsub)
+            GMs, GM_errs = np.zeros(nsub), np.zeros(nsub)
+            taus, tau_errs = np.zeros(nsub), np.zeros(nsub)
+            alphas, alpha_errs = np.zeros(nsub), np.zeros(nsub)
+            scales = np.zeros([nsub, nchan])
+            scale_errs = np.zeros([nsub, nchan])
+            snrs = np.zeros(nsub)
+            channel_snrs = np.zeros([nsub, nchan])
+            profile_fluxes = np.zeros([nsub, nchan])
+            profile_flux_errs = np.zeros([nsub, nchan])
+            fluxes, flux_errs = np.zeros(nsub), np.zeros(nsub)
+            flux_freqs = np.zeros(nsub)
+            red_chi2s = np.zeros(nsub)
+            covariances = np.zeros([nsub, self.nfit, self.nfit])
+            nfevals = np.zeros(nsub, dtype="int")
+            rcs = np.zeros(nsub, dtype="int")
+            MJDs = np.array([d.epochs[isub].in_days() for isub in range(nsub)],
+                            dtype=np.double)
+            DM_stored = d.DM
+            DM0 = DM_stored if self.DM0 is None else self.DM0
+            if not quiet:
+                print("\nEach of the %d TOAs is approximately %.2f s" % (
+                    len(d.ok_isubs), d.integration_length / nsub))
+            ok_isubs = list(d.ok_isubs)
+            nok = len(ok_isubs)
+            models, model_index = self._models(d, ok_isubs, fit_scat, quiet)
+            # ---- gather the batch (pptoas.py:384-529) --------------------
+            mask = np.zeros((nok, nchan), dtype=np.uint8)
+            init = np.zeros((nok, 5))
+            flags_b = np.zeros((nok, 5), dtype=np.int32)
+            nu_fit_b = np.zeros((nok, 3))
+            nu_out_b = np.full((nok, 3), np.nan)
+            guess_tau = np.zeros(nok)
+            for j, isub in enumerate(ok_isubs):
+                ok = np.asarray(d.ok_ichans[isub], dtype=int)
+                mask[j, ok] = 1
+                freqsx = d.freqs[isub, ok]
+                SNRsx = d.SNRs[isub, 0, ok]
+                P = d.Ps[isub]
+                if nu_fit_tuple is None:
+                    nu_fit = guess_fit_freq(freqsx, SNRsx)
+                    nu_fit_DM = nu_fit_GM = nu_fit_tau = nu_fit
+                else:
+                    nu_fit_DM = nu_fit_GM = nu_fit_tuple[0]
+                    nu_fit_tau = nu_fit_tuple[-1]
+                nu_fits_a[isub] = [nu_fit_DM, nu_fit_GM, nu_fit_tau]
+                nu_fit_b[j] = nu_fits_a[isub]
+                if nu_ref_tuple is None:
+                    nu_ref_DM = nu_ref_GM = nu_ref_tau = None
+                else:
+                    nu_ref_DM = nu_ref_GM = nu_ref_tuple[0]
+                    nu_ref_tau = nu_ref_tuple[-1]
+                    if bary and nu_ref_tau:
+                        nu_ref_tau /= d.doppler_factors[isub]
+                nu_refs_a[isub] = [nu_ref_DM, nu_ref_GM, nu_ref_tau]
+                nu_out_b[j] = [np.nan if v is None else v for v in
+                               nu_refs_a[isub]]
+                tau_guess = alpha_guess = 0.0
+                if fit_scat:
+                    if self.scat_guess is not None:
+                        tg_s, tg_ref, alpha_guess = self.scat_guess
+                        tau_guess = (tg_s / P) * (nu_fit_tau / tg_ref) ** \
+                            alpha_guess
+                    else:
+                        alpha_guess = self.alpha if hasattr(self, "alpha") \
+                            else scattering_alpha
+                        tau_guess = (self.gparams[1] / P) * (
+                            nu_fit_tau / self.model_nu_ref) ** alpha_guess \
+                            if hasattr(self, "gparams") else 0.0
+                    guess_tau[j] = tau_guess
+                    if self.log10_tau:
+                        if tau_guess == 0.0:
+                            tau_guess = nbin ** -1
+                        tau_guess = np.log10(tau_guess)
+                init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
+                if len(freqsx) == 1:
+                    fit_flags = [1, 0, 0, 0, 0]
+                    if not quiet:
+                        print("TOA #%d only has 1 frequency channel...fitting "
+                              "for phase only..." % (j + 1))
+                elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
+                    if fit_flags is None:
+                        raise UnboundLocalError(
+                            "local variable 'fit_flags' referenced before "
+                            "assignment (pptoas.py:525)")
+                    fit_flags = list(fit_flags)
+                    fit_flags[2] = 0
+                else:
+                    fit_flags = list(np.copy(self.fit_flags))
+                flags_b[j] = fit_flags
+            data_rows = np.asarray(d.subints)[ok_isubs, 0]
+            d32 = data_rows.astype(np.float32)
+            if np.array_equal(d32.astype(np.float64), data_rows):
+                data_rows = d32      # PSRCHIVE amplitudes are float32
+            t_fit = time.time()
+            res = engine.fit_batch(
+                data_rows, models, d.freqs[ok_isubs], d.Ps[ok_isubs], init,
+                flags_b, nu_fits=nu_fit_b, nu_outs=nu_out_b,
+                errs=np.asarray(d.noise_stds)[ok_isubs, 0],
+                chan_mask=mask, model_index=model_index,
+                log10_tau=self.log10_tau, option=0, is_toa=True, guess=True,
+                guess_weights=np.asarray(d.weights)[ok_isubs],
+                guess_DM=np.full(nok, DM_stored), guess_Ns=100,
+                guess_tau=guess_tau if fit_scat else None)
+            r = engine.results_numpy(res)
+            batch_duration = time.time() - t_fit
+            # ---- per-sub-integration bookkeeping (pptoas.py:567-711) -----
+            for j, isub in enumerate(ok_isubs):
+                fit_flags_j = [int(v) for v in flags_b[j]]
+                ok = mask[j].astype(bool)
+                R = r["results"][j]
+                status = int(R[_lib.RESULT_INDEX["status"]])
+                _nu_zero_messages(fit_flags_j, nu_refs_a[isub])
+                _raise_status(status)
+                if (status & 0xff) not in (0, 1, 2, 4):
+                    _status_message(status & 0xff, datafile + "_%d" % isub)
+                results = unpack_result(
+                    R, r["scales"][j][ok], r["scale_errs"][j][ok],
+                    r["channel_snrs"][j][ok], r["covariance"][j], fit_flags_j,
+                    batch_duration / nok)
+                fit_duration += results.duration
+                P = d.Ps[isub]
+                epoch = d.epochs[isub]
+                results.TOA = epoch + _MJD((results.phi * P + d.backend_delay)
+                                           / (3600 * 24.))
+                results.TOA_err = results.phi_err * P * 1e6
+                if self.bary:
+                    df = d.doppler_factors[isub]
+                    if fit_flags_j[1]:
+                        results.DM *= df
+                    if fit_flags_j[2]:
+                        results.GM *= df ** 3
+                else:
+                    df = 1.0
+                freqsx = d.freqs[isub, ok]
+                if print_flux:
+                    modelx = models[model_index[j]][ok]
+                    if results.tau != 0.0:
+                        tau = 10 ** results.tau if self.log10_tau else \
+                            results.tau
+                        scat_model = np.fft.irfft(scattering_portrait_FT(
+                            scattering_times(tau, results.alpha, freqsx,
+                                             results.nu_tau), nbin) *
+                            np.fft.rfft(modelx, axis=1), axis=1)
+                    else:
+                        scat_model = np.copy(modelx)
+                    smm = scat_model.mean(axis=1)
+                    profile_fluxes[isub, ok] = smm * results.scales
+                    profile_flux_errs[isub, ok] = abs(smm) * results.scale_errs
+                    flux, flux_err = weighted_mean(profile_fluxes[isub, ok],
+                                                   profile_flux_errs[isub, ok])
+                    flux_freq, _ = weighted_mean(freqsx,
+                                                 profile_flux_errs[isub, ok])
+                    fluxes[isub], flux_errs[isub] = flux, flux_err
+                    flux_freqs[isub] = flux_freq
+                nu_refs_a[isub] = [results.nu_DM, results.nu_GM,
+                                   results.nu_tau]
+                phis[isub], phi_errs[isub] = results.phi, results.phi_err
+                TOAs[isub], TOA_errs[isub] = results.TOA, results.TOA_err
+                DMs[isub], DM_errs[isub] = results.DM, results.DM_err
+                GMs[isub], GM_errs[isub] = results.GM, results.GM_err
+                taus[isub], tau_errs[isub] = results.tau, results.tau_err
+                alphas[isub], alpha_errs[isub] = results.alpha, \
+                    results.alpha_err
+                nfevals[isub], rcs[isub] = results.nfeval, results.return_code
+                scales[isub, ok] = results.scales
+                scale_errs[isub, ok] = results.scale_errs
+                snrs[isub] = results.snr
+                channel_snrs[isub, ok] = results.channel_snrs
+                try:
+                    covariances[isub] = results.covariance_matrix
+                except ValueError:
+                    ifit = np.where(fit_flags_j)[0]
+                    for ii, a in enumerate(ifit):
+                        for jj, b in enumerate(ifit):
+                            covariances[isub][a, b] = \
+                                results.covariance_matrix[ii, jj]
+                red_chi2s[isub] = results.red_chi2
+                toa_flags = {}
+                if not fit_flags_j[1]:
+                    results.DM = None
+                    results.DM_err = None
+                if fit_flags_j[2]:
+                    toa_flags["gm"] = results.GM
+                    toa_flags["gm_err"] = results.GM_err
+                if fit_flags_j[3]:
+                    if self.log10_tau:
+                        toa_flags["scat_time"] = 10 ** results.tau * P / df * 1e6
+                        toa_flags["log10_scat_time"] = results.tau + \
+                            np.log10(P / df)
+                        toa_flags["log10_scat_time_err"] = results.tau_err
+                    else:
+                        toa_flags["scat_time"] = results.tau * P / df * 1e6
+                        toa_flags["scat_time_err"] = results.tau_err * P / df \
+                            * 1e6
+                    toa_flags["scat_ref_freq"] = results.nu_tau * df
+                    toa_flags["scat_ind"] = results.alpha
+                if fit_flags_j[4]:
+                    toa_flags["scat_ind_err"] = results.alpha_err
+                toa_flags["be"] = d.backend
+                toa_flags["fe"] = d.frontend
+                toa_flags["f"] = d.frontend + "_" + d.backend
+                toa_flags["nbin"] = nbin
+                toa_flags["nch"] = nchan
+                toa_flags["nchx"] = len(freqsx)
+                toa_flags["bw"] = freqsx.max() - freqsx.min()
+                toa_flags["chbw"] = abs(d.bw) / nchan
+                toa_flags["subint"] = isub
+                toa_flags["tobs"] = d.subtimes[isub]
+                toa_flags["fratio"] = freqsx.max() / freqsx.min()
+                toa_flags["tmplt"] = self.modelfile
+                toa_flags["snr"] = results.snr
+                if nu_ref_tuple is not None and np.all(fit_flags_j[:2]):
+                    toa_flags["phi_DM_cov"] = results.covariance_matrix[0, 1]
+                toa_flags["gof"] = results.red_chi2
+                if print_phase:
+                    toa_flags["phs"] = results.phi
+                    toa_flags["phs_err"] = results.phi_err
+                if print_flux:
+                    toa_flags["flux"] = fluxes[isub]
+                    toa_flags["flux_err"] = flux_errs[isub]
+                    toa_flags["flux_ref_freq"] = flux_freqs[isub]
+                if print_parangle:
+                    toa_flags["par_angle"] = d.parallactic_angles[isub]
+                for k, v in addtnl_toa_flags.items():
+                    toa_flags[k] = v
+                self.TOA_list.append(TOA(datafile, results.nu_DM, results.TOA,
+                                         results.TOA_err, d.telescope,
+                                         d.telescope_code, results.DM,
+                                         results.DM_err, toa_flags))
+            # ---- DeltaDM (pptoas.py:713-729) ------------------------------
+            DeltaDMs = DMs - DM0
+            oks = np.asarray(d.ok_isubs)
+            if np.all(DM_errs[oks]):
+                DM_weights = DM_errs[oks] ** -2
+            else:
+                DM_weights = np.ones(len(DM_errs[oks]))
+            DeltaDM_mean, DeltaDM_var = np.average(DeltaDMs[oks],
+                                                   weights=DM_weights,
+                                                   returned=True)
+            DeltaDM_var = DeltaDM_var ** -1
+            if len(oks) > 1:
+                DeltaDM_var *= np.sum(((DeltaDMs[oks] - DeltaDM_mean) ** 2) *
+                                      DM_weights) / (len(DeltaDMs[oks]) - 1)
+            DeltaDM_err = DeltaDM_var ** 0.5
+            self.order.append(datafile)
+            self.obs.append(obs)
+            self.doppler_fs.append(d.doppler_factors)
+            self.nu0s.append(d.nu0)
+            self.nu_fits.append(nu_fits_a)
+            self.nu_refs.append(nu_refs_a)
+            self.ok_isubs.append(d.ok_isubs)
+            self.epochs.append(d.epochs)
+            self.MJDs.append(MJDs)
+            self.Ps.append(d.Ps)
+            self.phis.append(phis)
+            self.phi_errs.append(phi_errs)
+            self.TOAs.append(TOAs)
+            self.TOA_errs.append(TOA_errs)
+            self.DM0s.append(DM0)
+            self.DMs.append(DMs)
+            self.DM_errs.append(DM_errs)
+            self.DeltaDM_means.append(DeltaDM_mean)
+            self.DeltaDM_errs.append(DeltaDM_err)
+            self.GMs.append(GMs)
+            self.GM_errs.append(GM_errs)
+            self.taus.append(taus)
+            self.tau_errs.append(tau_errs)
+            self.alphas.append(alphas)
+            self.alpha_errs.append(alpha_errs)
+            self.scales.append(scales)
+            self.scale_errs.append(scale_errs)
+            self.snrs.append(snrs)
+            self.channel_snrs.append(channel_snrs)
+            self.profile_fluxes.append(profile_fluxes)
+            self.profile_flux_errs.append(profile_flux_errs)
+            self.fluxes.append(fluxes)
+            self.flux_errs.append(flux_errs)
+            self.flux_freqs.append(flux_freqs)
+            self.covariances.append(covariances)
+            self.red_chi2s.append(red_chi2s)
+            self.nfevals.append(nfevals)
+            self.rcs.append(rcs)
+            self.fit_durations.append(fit_duration)
+            if not quiet:
+                print("--------------------------")
+                print(datafile)
+                print("~%.4f sec/TOA" % (fit_duration / len(d.ok_isubs)))
+                print("Med. TOA error is %.3f us" % (np.median(
+                    phi_errs[oks]) * d.Ps.mean() * 1e6))
+            tot_duration = time.time() - start
+            if not quiet and len(self.ok_isubs):
+                print("--------------------------")
+                print("Total time: %.2f sec, ~%.4f sec/TOA" % (
+                    tot_duration,
+                    tot_duration / np.array(list(map(len, self.ok_isubs))
+                                            ).sum()))
+        if not already_warned:
+            pass

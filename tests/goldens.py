@@ -1,0 +1,119 @@
+"""Loaders for the golden vectors in tests/golden/ (produced by make_golden.py
+from the reference itself; see that script's header)."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# Parity bar (BASELINE.json north_star): fitted parameters within 0.01 sigma of
+# the reference's own reported uncertainty, chi2_red within 1e-8 relative.
+SIGMA_TOL = 0.01
+RCHI2_RTOL = 1e-8
+
+PARAM_NAMES = ("phi", "DM", "GM", "tau", "alpha")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def case_names(fname):
+    z = _load(fname)
+    return sorted(set(k.split("/")[0] for k in z.files))
+
+
+class Case(dict):
+    __getattr__ = dict.__getitem__
+
+
+def load_case(fname, name):
+    z = _load(fname)
+    out = Case()
+    for k in z.files:
+        if k.startswith(name + "/"):
+            v = z[k]
+            out[k[len(name) + 1:]] = v[()] if v.shape == () else v
+    return out
+
+
+def full_case(name):
+    return load_case("fit_portrait_full.npz", name)
+
+
+def fp_case(name):
+    return load_case("fit_portrait.npz", name)
+
+
+def misc():
+    z = _load("misc.npz")
+    return Case({k: z[k] for k in z.files})
+
+
+def gettoas():
+    z = _load("get_toas.npz")
+    return Case({k: z[k] for k in z.files})
+
+
+def full_case_args(c):
+    """Positional/keyword arguments of fit_portrait_full for a golden case."""
+    errs = None if np.all(np.isnan(c["errs"])) else c["errs"]
+    nu_outs = [None if np.isnan(v) else float(v) for v in c["nu_outs"]]
+    return dict(data_port=c["data"].astype(np.float64),
+                model_port=c["model"].astype(np.float64),
+                init_params=list(c["init"]), P=float(c["P"]),
+                freqs=c["freqs"], nu_fits=list(c["nu_fits"]),
+                nu_outs=nu_outs, errs=errs,
+                fit_flags=[int(x) for x in c["flags"]],
+                log10_tau=bool(c["log10_tau"]), option=int(c["option"]))
+
+
+def phase_diff(a, b):
+    """Difference of two phases modulo 1, in [-0.5, 0.5)."""
+    d = (np.asarray(a) - np.asarray(b) + 0.5) % 1.0 - 0.5
+    return d
+
+
+DCONST = 0.000241 ** -1
+
+
+def to_reference_frequencies(got, ref, P, log10_tau):
+    """Re-express ``got``'s phase and scattering time at ``ref``'s output
+    reference frequencies: phi moves with the fitted
+    DM/GM (phase_transform semantics, pplib.py:2688-2712, plus the nu**-4
+    term), tau with the fitted alpha (pptoaslib.py:1107-1113)."""
+    phi, DM, GM, tau, alpha = (float(v) for v in got["params"])
+    phi = (phi + DCONST * DM / P * (ref["nu_DM"] ** -2 - got["nu_DM"] ** -2) +
+           DCONST ** 2 * GM / P * (ref["nu_GM"] ** -4 - got["nu_GM"] ** -4))
+    if log10_tau:
+        tau = tau + alpha * np.log10(ref["nu_tau"] / got["nu_tau"])
+    else:
+        tau = tau * (ref["nu_tau"] / got["nu_tau"]) ** alpha
+    return [phi, DM, GM, tau, alpha]
+
+
+def param_deviation_sigma(got, ref, P=None, log10_tau=False):
+    """|got - ref| / ref_err per parameter (phase mod 1), after moving got to
+    ref's reference frequencies when both carry nu_DM/nu_GM/nu_tau.
+
+    Returns an array of 5 deviations (0 where the parameter is not fit)."""
+    if P is not None and "nu_DM" in got and "nu_DM" in ref:
+        gp = np.asarray(to_reference_frequencies(got, ref, P, log10_tau))
+    else:
+        gp = np.asarray(got["params"], float)
+    rp = np.asarray(ref["params"], float)
+    re = np.asarray(ref["param_errs"], float)
+    dev = np.zeros(5)
+    for i in range(5):
+        if re[i] == 0:
+            continue
+        d = phase_diff(gp[i], rp[i]) if i == 0 else gp[i] - rp[i]
+        dev[i] = abs(d) / re[i]
+    return dev
+
+
+def ref_bunch(c):
+    """The reference's DataBunch fields of a golden fit_portrait_full case."""
+    return dict(params=c["out_params"], param_errs=c["out_param_errs"],
+                nu_DM=float(c["out_nu_DM"]), nu_GM=float(c["out_nu_GM"]),
+                nu_tau=float(c["out_nu_tau"]))

@@ -1,0 +1,235 @@
+#!/usr/bin/env python
+"""Headline benchmark: subint portrait fits/sec (phase+DM, 512ch x 2048bin).
+
+Workload (BASELINE.json configs[1]): synthetic 512-channel x 2048-bin
+sub-integrations, N_sub per GPU (default 10,000), the full GetTOAs hot path
+per sub-integration on the device: power-spectrum noise, cross spectrum,
+initial phase from the dedispersed mean profile (brute grid + Nelder-Mead),
+the trust-region wideband fit (phi, DM), zero-covariance frequency, output
+transform, covariance, scales and S/N.  Inputs are resident in HBM (float32
+amplitudes, generated on the device) before the timed region; one "step" =
+one pass of the hot path over the whole batch, plus the RCCL all-gather of
+the result records when N > 1 (weak scaling: N_sub per GPU is fixed).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  It carries `roofline` for the dominant kernel
+(algorithmic bytes from HIP events around each kernel on the launch stream)
+and `cpu_baseline` (the NumPy/SciPy oracle on a bounded sample, 1 core).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("subint portrait fits/sec (phase+DM, 512ch×2048bin) at "
+          "1/2/4/8 MI355X")
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nsub", type=int, default=10000,
+                    help="sub-integrations per GPU")
+    ap.add_argument("--nchan", type=int, default=512)
+    ap.add_argument("--nbin", type=int, default=2048)
+    ap.add_argument("--chunk", type=int, default=2500,
+                    help="sub-integrations per ppf_fit_batch call")
+    ap.add_argument("--cpu-sample", type=int, default=8,
+                    help="sub-integrations for the CPU baseline (0: skip)")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
+                                                  "pmc_summary.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, nsample, nchan, nbin):
+    """Oracle (NumPy/SciPy restatement of the reference get_TOAs inner loop)
+    on `nsample` sub-integrations of the same workload, one core."""
+    import oracle.ppfit_oracle as O
+    from threadpoolctl import threadpool_limits
+    data = batch["data"][:nsample].double().cpu().numpy()
+    freqs = np.tile(batch["freqs"], (nsample, 1))
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        O.get_toas_archive(data, batch["model"], freqs,
+                           np.ones((nsample, nchan)),
+                           np.ones((nsample, nchan)),
+                           batch["P"][:nsample], O_DM0(), np.ones(nsample))
+        dt = time.perf_counter() - t0
+    return dict(value=nsample / dt, unit="subint-fits/s", cores=1,
+                kind="port",
+                sample="%d sub-integrations of %dch x %dbin, oracle "
+                       "get_TOAs loop (noise, FFTFIT guess, trust-ncg fit, "
+                       "post-fit), %.1f s" % (nsample, nchan, nbin, dt))
+
+
+def O_DM0():
+    from pulseportraiture_amd.synth import DM0
+    return DM0
+
+
+def main():
+    args = parse()
+    import torch
+    from pulseportraiture_amd import _lib, dist, engine, synth
+    from pulseportraiture_amd.pplib import guess_fit_freq
+    rank, world, local = dist.init("nccl")
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world),
+              file=sys.stderr)
+    dev = torch.device("cuda", local)
+    total = args.nsub * world
+    first, count = dist.shard(total, rank, world)
+    nchan, nbin = args.nchan, args.nbin
+    nharm = nbin // 2 + 1
+
+    # ---- resident inputs (untimed) ------------------------------------------
+    batch = synth.make_batch(count, nchan, nbin, first=first, dev=dev)
+    data = batch["data"]
+    f64 = torch.float64
+    model_t = torch.as_tensor(batch["model"], dtype=f64, device=dev)
+    freqs_t = torch.as_tensor(np.tile(batch["freqs"], (count, 1)), dtype=f64,
+                              device=dev)
+    P_t = torch.as_tensor(batch["P"], dtype=f64, device=dev)
+    init = np.zeros((count, 5))
+    init[:, 1] = synth.DM0                       # DM_guess = DM_stored
+    init_t = torch.as_tensor(init, dtype=f64, device=dev)
+    flags_t = torch.tensor([1, 1, 0, 0, 0], dtype=torch.int32,
+                           device=dev).repeat(count, 1)
+    nu_fit = guess_fit_freq(batch["freqs"])      # pptoas.py:442
+    nu_fits_t = torch.full((count, 3), nu_fit, dtype=f64, device=dev)
+    nu_outs_t = torch.full((count, 3), float("nan"), dtype=f64, device=dev)
+    gw_t = torch.ones((count, nchan), dtype=f64, device=dev)
+    gdm_t = torch.full((count,), synth.DM0, dtype=f64, device=dev)
+    lib = _lib.load()
+    ctx = _lib.context(dev.index)
+    lib.ppf_set_profiling(ctx, 1)
+    ws = None
+    chunks = [(c0, min(count, c0 + args.chunk))
+              for c0 in range(0, count, args.chunk)]
+
+    def step():
+        nonlocal ws
+        outs = []
+        for c0, c1 in chunks:
+            sl = slice(c0, c1)
+            res = engine.fit_batch(
+                data[sl], model_t, freqs_t[sl], P_t[sl], init_t[sl],
+                flags_t[sl], nu_fits=nu_fits_t[sl], nu_outs=nu_outs_t[sl],
+                guess=True, guess_weights=gw_t[sl], guess_DM=gdm_t[sl],
+                guess_Ns=100, dev=dev, workspace=ws)
+            ws = res["workspace"]
+            outs.append(res["results"])
+        results = torch.cat(outs, 0)
+        return dist.allgather_rows(results, total, world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    ncall0 = len(chunks) * args.warmup
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    dt = dist.max_over_ranks(dt, dev)
+
+    # ---- per-kernel times of the timed region (HIP events on the stream) ---
+    ncalls = len(chunks) * args.steps
+    hist = np.zeros((ncalls, 4))
+    got = lib.ppf_stage_ms_history(ctx, ncalls, hist.ctypes.data)
+    stage_ms = hist[:got].sum(axis=0)
+    res_np = last.cpu().numpy()
+    I = _lib.RESULT_INDEX
+    nfev = res_np[:, I["nfeval"]]
+    status = res_np[:, I["status"]].astype(int)
+    # algorithmic bytes per sub-integration
+    xspec_bytes = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
+    model_bytes = nchan * nbin * 8 + nchan * nharm * 16
+    solve_bytes_per_pass = nchan * nharm * 16 + nchan * 10 * 8
+    steps_subints = count * args.steps
+    mean_passes = float(nfev[first:first + count].mean()) if world > 1 else \
+        float(nfev.mean())
+    kern = {
+        "xspec": dict(ms=stage_ms[1],
+                      bytes=steps_subints * xspec_bytes +
+                      ncalls * nchan * nharm * 16),
+        "solve": dict(ms=stage_ms[3],
+                      bytes=steps_subints * mean_passes *
+                      solve_bytes_per_pass),
+        "guess": dict(ms=stage_ms[2], bytes=None),
+        "model_rfft": dict(ms=stage_ms[0], bytes=ncalls * model_bytes),
+    }
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    dk = kern[dom]
+    if dk["bytes"] is None:
+        dom = "solve" if kern["solve"]["ms"] >= kern["xspec"]["ms"] else \
+            "xspec"
+        dk = kern[dom]
+    achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pm = json.load(open(args.pmc))
+            if pm.get("kernel") and dom in pm["kernel"]:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    n_launch = ncalls
+    roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
+                unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                traffic=traffic, kernel="k_" + dom,
+                algorithmic_bytes_per_launch=dk["bytes"] / n_launch,
+                avg_launch_ms=dk["ms"] / n_launch)
+    stages = {k: dict(total_ms=round(v["ms"], 3),
+                      gbs=(None if not v["bytes"] or not v["ms"] else
+                           round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
+              for k, v in kern.items()}
+    value = total * args.steps / dt
+    out = dict(metric=METRIC, value=round(value, 2), unit="subint-fits/s",
+               n_gpus=world, steps=args.steps, warmup=args.warmup,
+               ms_per_step=round(dt / args.steps * 1e3, 3),
+               higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="f64", data="synthetic (device-generated example.gmodel "
+               "portraits + white noise; float32 amplitudes)",
+               config=dict(workload="configs[1]: %d subints/GPU x %dch x "
+                           "%dbin, phase+DM wideband fit (GetTOAs path)" %
+                           (args.nsub, nchan, nbin), nsub_per_gpu=args.nsub,
+                           nchan=nchan, nbin=nbin, chunk=args.chunk,
+                           fit="phase+DM", parallelism="dp%d" % world),
+               roofline=roof, stages=stages,
+               mean_passes_per_fit=round(mean_passes, 3),
+               fits_converged_frac=round(float(np.mean(
+                   (status & 0xff) == 2)), 5))
+    # sanity: fitted DM / phase agree with the injected truths
+    if rank == 0:
+        dm = res_np[:count, I["params"]][:, 1]
+        dme = res_np[:count, I["param_errs"]][:, 1]
+        pull = (dm - batch["DM_true"]) / dme
+        out["dm_pull_rms"] = round(float(np.sqrt(np.mean(pull ** 2))), 3)
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(batch, args.cpu_sample, nchan,
+                                           nbin)
+        out["vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"],
+                                       1)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

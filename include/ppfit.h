@@ -135,6 +135,17 @@ int ppf_create(int device, ppf_ctx **out);
 void ppf_destroy(ppf_ctx *ctx);
 const char *ppf_last_error(const ppf_ctx *ctx);
 
+/* Stage timing with HIP events recorded on the caller's stream around each
+ * kernel of ppf_fit_batch (model rfft, xspec, guess, solve).  Off by
+ * default; ppf_last_stage_ms waits for the last call's events and returns
+ * the four stage durations in milliseconds (0 for a skipped stage). */
+int ppf_set_profiling(ppf_ctx *ctx, int enable);
+int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4);
+/* The stage times of the last n (<= 256) profiled ppf_fit_batch calls,
+ * oldest first, into ms[n][4]; returns the number written.  Events are kept
+ * in a ring, so a timed loop records without synchronising. */
+int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms);
+
 /* Workspace needed by ppf_fit_batch for `desc` (only sizes/flags are read). */
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc);
 
@@ -179,13 +190,15 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin,
 /* Synthetic sub-integrations for benchmarks/tests (make_fake_pulsar minus
  * PSRCHIVE, pplib.py:3355-3493): out[s][n] = rotate(model[n], -phi[s],
  * -DM[s], P[s], freqs[n], nu_ref) + N(0, noise) with a counter-based RNG
- * keyed by (seed, s, n).  model: [nchan][nbin]; out: [nsub][nchan][nbin]
+ * keyed by (seed, first_sub + s, n), so a sub-integration's data do not
+ * depend on how a job is sharded.  model: [nchan][nbin]; out: [nsub][nchan][nbin]
  * in out_dtype. */
 int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
                     const double *model, const double *freqs,
                     const double *phi, const double *DM, const double *P,
                     double nu_ref, double noise, uint64_t seed,
-                    int32_t out_dtype, void *out, void *stream);
+                    int64_t first_sub, int32_t out_dtype, void *out,
+                    void *stream);
 
 /* Host-side (CPU) helper: real roots of a degree <= 8 polynomial, highest
  * power first, with np.roots semantics (companion-matrix eigenvalues with an

@@ -69,6 +69,9 @@ SIGNATURES = {
     "ppf_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "ppf_destroy": (None, [_vp]),
     "ppf_last_error": (ctypes.c_char_p, [_vp]),
+    "ppf_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "ppf_last_stage_ms": (ctypes.c_int, [_vp, _vp]),
+    "ppf_stage_ms_history": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_fit_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FitDesc)]),
     "ppf_fit_batch": (ctypes.c_int, [_vp, ctypes.POINTER(FitDesc), _vp]),
     "ppf_fit2_batch": (ctypes.c_int, [_vp, ctypes.POINTER(FitDesc), _vp]),
@@ -81,8 +84,8 @@ SIGNATURES = {
                                              ctypes.c_double, _vp, _vp]),
     "ppf_synth_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp,
                                        _vp, _vp, ctypes.c_double,
-                                       ctypes.c_double, ctypes.c_uint64, _i32,
-                                       _vp, _vp]),
+                                       ctypes.c_double, ctypes.c_uint64,
+                                       ctypes.c_int64, _i32, _vp, _vp]),
     "ppf_poly_real_roots_host": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
 }
 

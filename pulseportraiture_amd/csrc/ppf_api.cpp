@@ -17,6 +17,11 @@ struct ppf_ctx {
     int device;
     std::string err;
     std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
+    bool prof = false;
+    static constexpr int kRing = 256;
+    hipEvent_t ring[kRing][5] = {};
+    bool ran[kRing][4] = {};
+    long ncalls = 0;
 };
 
 namespace {
@@ -142,9 +147,52 @@ int ppf_create(int device, ppf_ctx **out) {
 
 void ppf_destroy(ppf_ctx *ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
-    for (auto &kv : ctx->tw) hipFree(kv.second);
+    (void)hipSetDevice(ctx->device);
+    for (auto &kv : ctx->tw) (void)hipFree(kv.second);
+    for (auto &set : ctx->ring)
+        for (auto &e : set)
+            if (e) (void)hipEventDestroy(e);
     delete ctx;
+}
+
+int ppf_set_profiling(ppf_ctx *ctx, int enable) {
+    if (!ctx) return PPF_EINVAL;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    if (enable && !ctx->ring[0][0])
+        for (auto &set : ctx->ring)
+            for (auto &ev : set)
+                if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(ctx, e, "hipEventCreate");
+    ctx->prof = enable != 0;
+    ctx->ncalls = 0;
+    return PPF_OK;
+}
+
+int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms) {
+    if (!ctx || !ms || n < 0) return PPF_EINVAL;
+    if (!ctx->prof) return fail(ctx, PPF_EINVAL, "profiling is off");
+    long avail = ctx->ncalls < ppf_ctx::kRing ? ctx->ncalls : ppf_ctx::kRing;
+    if (n > avail) n = (int)avail;
+    for (int c = 0; c < n; ++c) {
+        int slot = (int)((ctx->ncalls - n + c) % ppf_ctx::kRing);
+        hipError_t e = hipEventSynchronize(ctx->ring[slot][4]);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+        for (int i = 0; i < 4; ++i) {
+            float t = 0.f;
+            if (ctx->ran[slot][i]) {
+                e = hipEventElapsedTime(&t, ctx->ring[slot][i], ctx->ring[slot][i + 1]);
+                if (e != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+            }
+            ms[c * 4 + i] = (double)t;
+        }
+    }
+    return n;
+}
+
+int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4) {
+    int n = ppf_stage_ms_history(ctx, 1, ms4);
+    if (n < 0) return n;
+    return n == 1 ? PPF_OK : fail(ctx, PPF_EINVAL, "no profiled call yet");
 }
 
 const char *ppf_last_error(const ppf_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -169,9 +217,17 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     const int nharm = d->nbin / 2 + 1;
     const int kc = noise_kc(nharm, 4);
 
+    const int slot = (int)(ctx->ncalls % ppf_ctx::kRing);
+    auto mark = [&](int i) {
+        if (ctx->prof) (void)hipEventRecord(ctx->ring[slot][i], st);
+    };
+    for (int i = 0; i < 4; ++i) ctx->ran[slot][i] = true;
+    ctx->ran[slot][2] = d->guess != 0;
+    mark(0);
     ppf::RfftArgs ra{d->nbin, ilog2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_rfft_rows");
+    mark(1);
 
     ppf::XspecArgs xa{};
     xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = ilog2(d->nbin / 2);
@@ -184,6 +240,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.gM = d->guess ? (double2 *)(ws + L.gM) : nullptr;
     xa.gw = d->guess ? (double *)(ws + L.gw) : nullptr;
     if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
+    mark(2);
 
     if (d->guess) {
         ppf::GuessArgs ga{};
@@ -193,6 +250,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.gw = xa.gw; ga.x0 = (double *)(ws + L.x0);
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
     }
+    mark(3);
 
     ppf::SolveArgs sa{};
     sa.nsub = d->nsub; sa.nchan = d->nchan; sa.nbin = d->nbin;
@@ -206,6 +264,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.any_plain = 1;
     sa.any_scat = 1;
     if ((e = ppf::launch_solve(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_solve");
+    mark(4);
+    if (ctx->prof) ++ctx->ncalls;
     return PPF_OK;
 }
 
@@ -280,8 +340,8 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
 
 int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, const double *model,
                     const double *freqs, const double *phi, const double *DM, const double *P,
-                    double nu_ref, double noise, uint64_t seed, int32_t out_dtype, void *out,
-                    void *stream) {
+                    double nu_ref, double noise, uint64_t seed, int64_t first_sub,
+                    int32_t out_dtype, void *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
     if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nsub < 0 || nchan < 1 || (nsub > 0 && (!model || !freqs || !phi || !DM || !P || !out)))
@@ -304,9 +364,9 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, con
     ppf::SynthArgs a{};
     a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = out_dtype;
     a.Mft = Mft; a.freqs = freqs; a.phi = phi; a.DM = DM; a.P = P; a.nu_ref = nu_ref;
-    a.noise = noise; a.seed = seed; a.T = T; a.T2 = T2; a.out = out;
+    a.noise = noise; a.seed = seed; a.first = first_sub; a.T = T; a.T2 = T2; a.out = out;
     if ((e = ppf::launch_synth(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_synth");
-    hipFreeAsync(Mft, st);
+    (void)hipFreeAsync(Mft, st);
     return PPF_OK;
 }
 

@@ -90,6 +90,7 @@ struct SynthArgs {
     const double *freqs, *phi, *DM, *P;
     double nu_ref, noise;
     uint64_t seed;
+    int64_t first;
     const double2 *T, *T2;
     void *out;
 };

@@ -594,7 +594,6 @@ enum { NZ_MAX = 16 };
 template <bool SCAT>
 __global__ __launch_bounds__(kBlock) void k_solve(SolveArgs a) {
     __shared__ double red[kWaves * 32];
-    __shared__ double sh_out[24];
     __shared__ double sh_theta[8];
     __shared__ int sh_cmd;
     __shared__ double sh_x[8];
@@ -885,7 +884,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(SolveArgs a) {
                         for (int j = i; j < 4; ++j) { T[i][j] = T[j][i] = c[q]; ++q; }
                     double H11 = T[0][0], H22 = T[1][1], H33 = T[2][2], H44 = T[3][3];
                     double H12 = T[0][1], H13 = T[0][2], H14 = T[0][3], H23 = T[1][2],
-                           H24 = T[1][3], H34 = T[2][3];
+                           H34 = T[2][3];
                     num = (H34 * H34 - H33 * H44) * c[0] + (H13 * H44 - H14 * H34) * c[1] +
                           (H14 * H33 - H13 * H34) * c[2];
                     den = (H34 * H34 - H33 * H44) * c[3] + (H13 * H44 - H14 * H34) * c[4] +
@@ -1243,7 +1242,8 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
     const double sc = 1.0 / (double)N;
     const int64_t row = (int64_t)s * a.nchan + n;
     for (int j = threadIdx.x; j < N; j += kBlock) {
-        uint64_t h = splitmix64(a.seed ^ splitmix64((uint64_t)row * 0x100000001B3ull + j));
+        const uint64_t grow = (uint64_t)(a.first + s) * (uint64_t)a.nchan + (uint64_t)n;
+        uint64_t h = splitmix64(a.seed ^ splitmix64(grow * 0x100000001B3ull + (uint64_t)j));
         double u1 = u01(h), u2 = u01(splitmix64(h));
         double r = sqrt(-2.0 * log(u1));
         double sn, cs;

@@ -1,0 +1,79 @@
+"""Multi-GPU sharding: one process per GPU, torch.distributed over RCCL.
+
+Sub-integrations (and archives) are independent:
+nothing couples two of them inside the fit, so each rank fits a contiguous
+block of the global sub-integration index with NO data-path collective; the
+only exchange is one all-gather of the fixed-size result records at the end
+of a batch (``backend="nccl"`` is RCCL over xGMI on ROCm).  ``gloo`` runs the
+same code on CPU tensors for tests.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_world():
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    return rank, world, local
+
+
+def init(backend="nccl"):
+    """Initialise the process group from torchrun's env (no-op at world 1)."""
+    rank, world, local = env_rank_world()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(
+                "cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif backend == "nccl" and torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def shard(n_total, rank, world):
+    """Contiguous, balanced block of [0, n_total) for `rank`: (first, count).
+    Ranks differ by at most one sub-integration."""
+    base, extra = divmod(n_total, world)
+    count = base + (1 if rank < extra else 0)
+    first = rank * base + min(rank, extra)
+    return first, count
+
+
+def allgather_rows(local, n_total, world):
+    """All-gather per-sub-integration rows [count, ...] from every rank into
+    [n_total, ...] in global order (blocks padded to equal size for the
+    collective, then trimmed)."""
+    if world == 1:
+        return local
+    per = -(-n_total // world)
+    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    pad[:local.shape[0]] = local
+    out = torch.empty((per * world,) + tuple(local.shape[1:]),
+                      dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    rows = []
+    for r in range(world):
+        first, count = shard(n_total, r, world)
+        rows.append(out[r * per:r * per + count])
+    return torch.cat(rows, 0)
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def max_over_ranks(x, device=None):
+    """Max of a python float over ranks (used for timings)."""
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -220,7 +220,7 @@ def phase_shift_batch(data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
 
 
 def synth(model, freqs, phi, DM, P, nu_ref, noise, seed, out_dtype=torch.float32,
-          dev=None):
+          dev=None, first=0):
     """Synthetic sub-integrations [nsub, nchan, nbin] on the device."""
     dev = device(dev)
     m = to_dev(model, dev, torch.float64)
@@ -234,7 +234,7 @@ def synth(model, freqs, phi, DM, P, nu_ref, noise, seed, out_dtype=torch.float32
     ctx = _lib.context(dev.index)
     rc = _lib.load().ppf_synth_batch(
         ctx, nsub, nchan, nbin, _p(m), _p(f), _p(ph), _p(dm), _p(Pt),
-        float(nu_ref), float(noise), ctypes.c_uint64(int(seed)),
+        float(nu_ref), float(noise), ctypes.c_uint64(int(seed)), int(first),
         _lib.PPF_F32 if out_dtype == torch.float32 else _lib.PPF_F64,
         _p(out), _stream(dev))
     _lib.check(rc, ctx)

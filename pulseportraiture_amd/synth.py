@@ -1,0 +1,70 @@
+"""Synthetic wideband sub-integrations for benchmarks and tests.
+
+Mirrors make_fake_pulsar (pplib.py:3302-3499) minus PSRCHIVE, as specified in
+SURVEY.md section 8(d): a 3-component Gaussian template portrait (the
+example.gmodel of the reference's examples, parameters below), channel
+centres linspace(lo + cw/2, lo + bw - cw/2, nchan), each sub-integration the
+template rotated by (-phi, -DM) at nu_ref plus white noise.  The data are
+generated ON the device (ppf_synth_batch, counter-based RNG keyed by
+(seed, sub-integration, channel)), so a shard is reproducible on any rank.
+"""
+import numpy as np
+
+from . import engine, pplib
+
+P0 = 1.0 / 345.67890123456789      # examples/example.par F0
+DM0 = 34.56789                      # examples/example.par DM
+
+# examples/example.gmodel: CODE 000, FREQ 1300 MHz, DC, TAU, ALPHA, then per
+# component (loc, m_loc, wid, m_wid, amp, m_amp)
+GMODEL_CODE = "000"
+GMODEL_NU_REF = 1300.0
+GMODEL_ALPHA = -4.0
+GMODEL_PARAMS = np.array([
+    0.00889801, 0.0,
+    0.21925557, -0.00518501, 0.04823579, -2.08031160, 5.13274758, -1.65717015,
+    0.23409622, -0.00271530, 0.01573809, 1.61520300, 9.46117549, -2.07617616,
+    0.25844309, 0.00288377, 0.02348129, -3.30015260, 2.71065613, -0.90424701,
+])
+
+
+def channel_freqs(nchan, lo=1100.0, bw=800.0):
+    cw = bw / nchan
+    return np.linspace(lo + cw / 2, lo + bw - cw / 2, nchan)
+
+
+def template(nchan, nbin, lo=1100.0, bw=800.0):
+    """(model [nchan, nbin] float64, freqs [nchan]) of the example template."""
+    freqs = channel_freqs(nchan, lo, bw)
+    model = pplib.gen_gaussian_portrait(GMODEL_CODE, GMODEL_PARAMS,
+                                        GMODEL_ALPHA,
+                                        pplib.get_bin_centers(nbin), freqs,
+                                        GMODEL_NU_REF)
+    return model, freqs
+
+
+def truths(nsub, seed, first=0):
+    """Per-sub-integration (phi, DM) drawn as in SURVEY.md 8(d), keyed by the
+    global sub-integration index so shards are reproducible."""
+    phi = np.empty(nsub)
+    dm = np.empty(nsub)
+    for i in range(nsub):
+        rng = np.random.default_rng(seed + first + i)
+        phi[i] = rng.uniform(-0.5, 0.5)
+        dm[i] = DM0 + rng.normal(3e-4, 2e-4)
+    return phi, dm
+
+
+def make_batch(nsub, nchan, nbin, seed=20250217, first=0, noise=1.5,
+               nu_ref=1500.0, dtype="float32", dev=None):
+    """Device batch: dict(data [nsub,nchan,nbin] device tensor, model, freqs,
+    P, phi_true, DM_true)."""
+    import torch
+    model, freqs = template(nchan, nbin)
+    phi, dm = truths(nsub, seed, first)
+    P = np.full(nsub, P0)
+    data = engine.synth(model, freqs, phi, dm, P, nu_ref, noise, seed,
+                        torch.float32 if dtype == "float32" else torch.float64,
+                        dev=dev, first=first)
+    return dict(data=data, model=model, freqs=freqs, P=P, phi_true=phi,
+                DM_true=dm, nu_ref=nu_ref)

@@ -191,14 +191,16 @@ def test_masked_channels_equal_subset_fit(ppt):
     rng = np.random.default_rng(11)
     keep = np.ones(128, dtype=bool)
     keep[rng.choice(128, 17, replace=False)] = False
+    lt = a["log10_tau"]          # False: tau = 0 exactly (no scattering)
     ref = O.fit_portrait_full(c["data"][keep].astype(float),
                               a["model_port"][keep], a["init_params"], a["P"],
                               a["freqs"][keep], a["nu_fits"], a["nu_outs"],
-                              a["errs"][keep], a["fit_flags"])
+                              a["errs"][keep], a["fit_flags"], log10_tau=lt)
     init = np.array(ref["x_fit"]) + np.array([3e-5, 1e-4, 0, 0, 0])
     sub = ppt.fit_portrait_full(c["data"][keep], a["model_port"][keep], init,
                                 a["P"], a["freqs"][keep], a["nu_fits"],
-                                a["nu_outs"], a["errs"][keep], a["fit_flags"])
+                                a["nu_outs"], a["errs"][keep], a["fit_flags"],
+                                log10_tau=lt)
     res = engine.results_numpy(engine.fit_batch(
         c["data"][None], a["model_port"][None], a["freqs"][None], [a["P"]],
         init[None], a["fit_flags"], nu_fits=np.asarray(a["nu_fits"])[None],
@@ -319,6 +321,8 @@ def test_get_toas_matches_reference(monkeypatch, tmp_path, capsys):
         ta, tb = a.split(), b.split()
         assert len(ta) == len(tb)
         for x, y in zip(ta, tb):
+            if x.endswith("example.gmodel"):     # -tmplt path differs
+                continue
             assert _same_printed_number(x, y), (a, b)
 
 

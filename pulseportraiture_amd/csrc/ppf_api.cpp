@@ -22,6 +22,7 @@ struct ppf_ctx {
     hipEvent_t ring[kRing][5] = {};
     bool ran[kRing][4] = {};
     long ncalls = 0;
+    unsigned *host_active = nullptr;   // pinned, for the iteration loop
 };
 
 namespace {
@@ -72,7 +73,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gR, gM, gw, total;
+    size_t M, X, chan, stats, x0, gR, gM, gw, state, partials, active, total;
     int nblk, cb;
 };
 
@@ -90,6 +91,9 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.chan = o;  o += align256(sizeof(double) * nsub * nchan * 4);
     L.stats = o; o += align256(sizeof(double) * nsub * 2 * nchan * 10);
     L.x0 = o;    o += align256(sizeof(double) * nsub * 8);
+    L.state = o; o += align256(ppf::tr_state_bytes() * nsub);
+    L.partials = o; o += align256(sizeof(double) * nsub * (size_t)ppf::pass_blocks(d->nchan) * 21);
+    L.active = o; o += 256;
     if (d->guess) {
         L.gR = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
         L.gM = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
@@ -152,6 +156,7 @@ void ppf_destroy(ppf_ctx *ctx) {
     for (auto &set : ctx->ring)
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
+    if (ctx->host_active) (void)hipHostFree(ctx->host_active);
     delete ctx;
 }
 
@@ -263,7 +268,34 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.scale_errs = d->scale_errs; sa.channel_snrs = d->channel_snrs; sa.covariance = d->covariance;
     sa.any_plain = 1;
     sa.any_scat = 1;
-    if ((e = ppf::launch_solve(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_solve");
+    sa.state = (ppf::TRState *)(ws + L.state);
+    sa.partials = (double *)(ws + L.partials);
+    sa.active = (unsigned *)(ws + L.active);
+    if (!ctx->host_active) {
+        e = hipHostMalloc((void **)&ctx->host_active, sizeof(unsigned));
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
+    }
+    if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
+    // trust-region iterations: each = one streaming pass + one step.  Groups
+    // of iterations are queued without host synchronisation; the count of
+    // still-iterating sub-ints is read back between groups.
+    const int maxiter = d->max_iter > 0 ? d->max_iter : 200 * 5;
+    int iter = 0;
+    for (int group = 6;; group = 4) {
+        for (int g = 0; g < group; ++g) {
+            if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
+            if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
+                return hip_fail(ctx, e, "hipMemsetAsync");
+            if ((e = ppf::launch_tr_step(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_step");
+        }
+        iter += group;
+        if ((e = hipMemcpyAsync(ctx->host_active, sa.active, sizeof(unsigned), hipMemcpyDeviceToHost,
+                                st)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMemcpyAsync");
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+        if (*ctx->host_active == 0 || iter > maxiter + 2) break;
+    }
+    if ((e = ppf::launch_postfit(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_postfit");
     mark(4);
     if (ctx->prof) ++ctx->ncalls;
     return PPF_OK;

@@ -40,6 +40,8 @@ struct GuessArgs {
     double *x0;                  // [nsub][8]
 };
 
+struct TRState;
+
 struct SolveArgs {
     int nsub, nchan, nbin;
     const double2 *X, *Mft;
@@ -56,6 +58,9 @@ struct SolveArgs {
     ppf_result *results;
     double *scales, *scale_errs, *channel_snrs, *covariance;
     int any_plain, any_scat;
+    TRState *state;              // [nsub]
+    double *partials;            // [nsub][pass_blocks(nchan)][21]
+    unsigned *active;            // sub-ints still iterating (k_tr_step)
 };
 
 struct RotateArgs {
@@ -99,7 +104,12 @@ hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st);
-hipError_t launch_solve(const SolveArgs &a, hipStream_t st);
+hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st);
+hipError_t launch_pass(const SolveArgs &a, hipStream_t st);
+hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st);
+hipError_t launch_postfit(const SolveArgs &a, hipStream_t st);
+size_t tr_state_bytes();
+int pass_blocks(int nchan);
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st);

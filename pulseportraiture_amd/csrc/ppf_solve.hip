@@ -1,0 +1,934 @@
+// ppf_solve.hip -- the batched wideband solver (pptoaslib.py:564-1144).
+//
+// One ppf_fit_batch call runs, after k_xspec / k_guess:
+//   k_tr_init                     per sub-int: prologue (usable channels,
+//                                 nu_fit defaults, Sd, dof, start point)
+//   repeat { k_pass ; k_tr_step } until every sub-int has stopped
+//     k_pass<SCAT,U>              grid (sub-int x block of 64 channels): one
+//                                 streaming pass over the cross spectrum at
+//                                 the point each sub-int wants evaluated ->
+//                                 per-channel C, C', C'' (+ scattering sums)
+//                                 and the block's share of f, g, H
+//     k_tr_step                   one wave per sub-int: fixed-order reduction
+//                                 of the block partials, then one iteration
+//                                 of the scipy trust-ncg replica (accept /
+//                                 reject, radius, CG-Steihaug subproblem)
+//   k_postfit                     one workgroup per sub-int: zero-covariance
+//                                 frequencies, output transform, Schur
+//                                 covariance, scales, channel S/N, chi2
+// Splitting the cold trust-region / post-fit code out of the streaming pass
+// keeps the pass at <= 128 VGPRs (>= 4 waves/SIMD) with every harmonic load
+// of a channel row in flight.
+#include "ppf_device.hpp"
+#include "ppf_internal.hpp"
+
+namespace ppf {
+
+// ===========================================================================
+// per-channel likelihood terms (pptoaslib.py:195-561)
+// stats: 0 C, 1 C', 2 C'', 3 Q1, 4 Q1', 5 Q2, 6 S, 7 S1, 8 S2a, 9 S2b
+// (all already normalised by sigma~_n^2)
+// ===========================================================================
+struct Fac {
+    double dphi[3];   // d phi_n / d(phi, DM, GM)
+    double t[2];      // (d tau_n / d theta_j) / tau_n for j = tau, alpha
+    double u[3];      // (d2 tau_n / d theta_i d theta_j) / tau_n: tt, ta, aa
+    bool br_tt, br_ta, br_aa;   // reference bracket gates (pptoaslib.py:371-379)
+};
+
+__device__ __forceinline__ void chan_derivs(const double *st, const Fac &fc, double dC[5],
+                                            double dS[5], double d2C[5][5], double d2S[5][5]) {
+    const double Cp = st[1], Cpp = st[2], Q1 = st[3], Q1p = st[4], Q2 = st[5];
+    const double S1 = st[7], S2a = st[8], S2b = st[9];
+    for (int i = 0; i < 3; ++i) { dC[i] = Cp * fc.dphi[i]; dS[i] = 0.0; }
+    for (int j = 0; j < 2; ++j) { dC[3 + j] = Q1 * fc.t[j]; dS[3 + j] = S1 * fc.t[j]; }
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) { d2C[i][j] = Cpp * fc.dphi[i] * fc.dphi[j]; d2S[i][j] = 0.0; }
+        for (int j = 0; j < 2; ++j) {
+            d2C[i][3 + j] = d2C[3 + j][i] = fc.dphi[i] * fc.t[j] * Q1p;
+            d2S[i][3 + j] = d2S[3 + j][i] = 0.0;
+        }
+    }
+    const bool br[3] = {fc.br_tt, fc.br_ta, fc.br_aa};
+    const int ii[3] = {0, 0, 1}, jj[3] = {0, 1, 1};
+    for (int q = 0; q < 3; ++q) {
+        double tt = fc.t[ii[q]] * fc.t[jj[q]];
+        double c2, s2;
+        if (br[q]) {
+            c2 = 2.0 * tt * Q2 + fc.u[q] * Q1;
+            s2 = tt * S2a + 2.0 * tt * S2b + fc.u[q] * S1;
+        } else {
+            c2 = tt * Q1;
+            s2 = tt * S2a + tt * S1;
+        }
+        d2C[3 + ii[q]][3 + jj[q]] = d2C[3 + jj[q]][3 + ii[q]] = c2;
+        d2S[3 + ii[q]][3 + jj[q]] = d2S[3 + jj[q]][3 + ii[q]] = s2;
+    }
+}
+
+// per-channel profiled Hessian H_n (pptoaslib.py:662-671, no division by C)
+__device__ __forceinline__ void chan_hess(const double *st, const Fac &fc, double H[5][5]) {
+    double dC[5], dS[5], d2C[5][5], d2S[5][5];
+    chan_derivs(st, fc, dC, dS, d2C, d2S);
+    const double C = st[0], S = st[6];
+    const double iS = 1.0 / S, iS2 = iS * iS, iS3 = iS2 * iS, C2 = C * C;
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 5; ++j)
+            H[i][j] = -2.0 * (C * d2C[i][j] * iS - 0.5 * C2 * d2S[i][j] * iS2 + dC[i] * dC[j] * iS +
+                              C2 * dS[i] * dS[j] * iS3 - C * (dC[i] * dS[j] + dS[i] * dC[j]) * iS2);
+}
+
+struct FitGeom {           // per-sub-integration reference frequencies etc.
+    double P, nu_DM, nu_GM, nu_tau, tau_lin;  // tau_lin: linear tau at nu_tau
+    int log10_tau;
+    bool g_sum, g_tau, g_alpha;    // taus.sum(), dtau.sum(), dalpha.sum() != 0
+};
+
+__device__ __forceinline__ Fac make_fac(double nu, const FitGeom &g, double alpha) {
+    Fac f;
+    const double P = g.P;
+    f.dphi[0] = 1.0;
+    f.dphi[1] = kDconst * (pow(nu, -2.0) - pow(g.nu_DM, -2.0)) / P;
+    f.dphi[2] = kDconst * kDconst * (pow(nu, -4.0) - pow(g.nu_GM, -4.0)) / P;
+    const double lnf = log(nu / g.nu_tau);
+    if (!g.g_sum) {
+        f.t[0] = f.t[1] = 0.0;
+        f.u[0] = f.u[1] = f.u[2] = 0.0;
+    } else if (g.log10_tau) {
+        f.t[0] = kLn10;
+        f.t[1] = lnf;
+        f.u[0] = kLn10 * kLn10;
+        f.u[1] = kLn10 * lnf;
+        f.u[2] = lnf * lnf;
+    } else {
+        f.t[0] = 1.0 / g.tau_lin;
+        f.t[1] = lnf;
+        f.u[0] = 0.0;
+        f.u[1] = lnf / g.tau_lin;
+        f.u[2] = lnf * lnf;
+    }
+    (void)alpha;
+    f.br_tt = g.g_tau;
+    f.br_aa = g.g_alpha;
+    f.br_ta = g.g_alpha && g.g_tau;
+    return f;
+}
+
+// ===========================================================================
+// per-sub-integration solver state (workspace)
+// ===========================================================================
+enum { PH_INIT = 0, PH_PROPOSAL = 1, PH_DONE = 2 };
+
+struct TRState {
+    double x[5];          // accepted point
+    double th[5];         // point the next pass evaluates
+    double f, g[5], H[15];  // model at x (H upper triangle, all 5 params)
+    double radius, pred;
+    double nu_fit[3], nu_mean, Sd, dof, phi_guess;
+    int k, status, nfev, phase;
+    int slot_cur, slot_eval, flagmask, nchanx;
+    int scat, hb, g_sum, g_tau;
+    int g_alpha, pad0, pad1, pad2;
+};
+
+__device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j
+    return i * 5 - (i * (i - 1)) / 2 + (j - i);
+}
+
+// reference gates (taus.sum(), dtau.sum(), dalpha.sum()) at (tau_lin, alpha)
+// over the usable channels; wave-level (all 64 lanes of the calling wave).
+__device__ void wave_gates(const double *fr, const uint8_t *mask, int nchan, double tau_lin,
+                           double alpha, double nu_tau, int log10_tau, int &g_sum, int &g_tau,
+                           int &g_alpha) {
+    const int lane = threadIdx.x & 63;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int n = lane; n < nchan; n += 64) {
+        if (mask && !mask[n]) continue;
+        double tn = tau_lin * pow(fr[n] / nu_tau, alpha);
+        s0 += tn;
+        s1 += log10_tau ? kLn10 * tn : tn / tau_lin;
+        s2 += log(fr[n] / nu_tau) * tn;
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2);
+    g_sum = s0 != 0.0;
+    g_tau = g_sum && s1 != 0.0;
+    g_alpha = s2 != 0.0;
+}
+
+// ===========================================================================
+// k_tr_init: one wave per sub-integration (4 per workgroup)
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int s = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (s >= a.nsub) return;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *chan = a.chan + (int64_t)s * a.nchan * 4;
+    double sf = 0.0, cnt = 0.0, sd = 0.0;
+    for (int n = lane; n < a.nchan; n += 64)
+        if (!mask || mask[n]) { sf += fr[n]; cnt += 1.0; sd += chan[n * 4 + 2]; }
+    sf = wave_sum(sf); cnt = wave_sum(cnt); sd = wave_sum(sd);
+    TRState &S = a.state[s];
+    int flagmask = 0, nf = 0;
+    for (int i = 0; i < 5; ++i)
+        if (a.fit_flags[(int64_t)s * 5 + i]) { flagmask |= 1 << i; ++nf; }
+    double x[5];
+    for (int i = 0; i < 5; ++i) x[i] = a.init[(int64_t)s * 5 + i];
+    if (a.guess) x[0] = a.x0[(int64_t)s * 8 + 0];
+    const double tau0 = a.log10_tau ? pow(10.0, x[3]) : x[3];
+    const int scat = ((flagmask & 0x18) || tau0 != 0.0) ? 1 : 0;
+    const double nu_mean = sf / cnt;
+    double nu_fit[3];
+    for (int i = 0; i < 3; ++i) {
+        nu_fit[i] = a.nu_fits[(int64_t)s * 3 + i];
+        if (nu_fit[i] != nu_fit[i]) nu_fit[i] = nu_mean;
+    }
+    int gs = 0, gt = 0, ga = 0;
+    if (scat) wave_gates(fr, mask, a.nchan, tau0, x[4], nu_fit[2], a.log10_tau, gs, gt, ga);
+    if (lane == 0) {
+        for (int i = 0; i < 5; ++i) { S.x[i] = x[i]; S.th[i] = x[i]; S.g[i] = 0.0; }
+        S.f = 0.0;
+        for (int i = 0; i < 15; ++i) S.H[i] = 0.0;
+        S.radius = 1.0;                 // scipy initial_trust_radius
+        S.pred = 0.0;
+        for (int i = 0; i < 3; ++i) S.nu_fit[i] = nu_fit[i];
+        S.nu_mean = nu_mean;
+        S.Sd = sd;
+        S.dof = cnt * (double)a.nbin - (double)(nf + (int)cnt);
+        S.phi_guess = x[0];
+        S.k = 0;
+        S.status = PPF_ST_CONVERGED;
+        S.nfev = 0;
+        S.slot_cur = 0;
+        S.slot_eval = 0;
+        S.flagmask = flagmask;
+        S.nchanx = (int)cnt;
+        S.scat = scat;
+        S.hb = 0;
+        S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga;
+        if (nf == 0 || cnt == 0.0) {
+            S.phase = PH_DONE;
+            S.status = PPF_ST_NOFIT;
+        } else {
+            S.phase = PH_INIT;
+        }
+    }
+}
+
+// ===========================================================================
+// k_pass: one streaming pass over X for the sub-ints that asked for one
+// grid = nsub * nblk; workgroup = 4 waves; block = kPassChans channels
+// ===========================================================================
+constexpr int kPassChans = 64;                 // channels per workgroup
+constexpr int kWaveChans = kPassChans / kWaves; // 16 per wave
+
+template <bool SCAT, int U>
+__global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
+    __shared__ double red[kWaves * 21];
+    const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
+    const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    const TRState &S = a.state[s];
+    if (S.phase == PH_DONE || S.scat != (SCAT ? 1 : 0)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nharm = (a.nbin >> 1) + 1;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *chan = a.chan + (int64_t)s * a.nchan * 4;
+    const double2 *X = a.X + (int64_t)s * a.nchan * nharm;
+    const double2 *M = a.Mft + (int64_t)(a.model_index ? a.model_index[s] : 0) * a.nchan * nharm;
+    double *stats = a.stats + ((int64_t)s * 2 + S.slot_eval) * a.nchan * 10;
+    double th[5];
+    for (int i = 0; i < 5; ++i) th[i] = S.th[i];
+    const int flagmask = S.flagmask;
+    FitGeom g;
+    g.P = a.P[s];
+    g.nu_DM = S.nu_fit[0];
+    g.nu_GM = S.nu_fit[1];
+    g.nu_tau = S.nu_fit[2];
+    g.log10_tau = a.log10_tau;
+    const double tau_lin = a.log10_tau ? pow(10.0, th[3]) : th[3];
+    const double alpha = th[4];
+    g.tau_lin = tau_lin;
+    g.g_sum = S.g_sum; g.g_tau = S.g_tau; g.g_alpha = S.g_alpha;
+    const double nuDM2 = pow(g.nu_DM, -2.0), nuGM4 = pow(g.nu_GM, -4.0);
+
+    double acc[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) acc[i] = 0.0;
+    const int c0 = blk * kPassChans + wave * kWaveChans;
+    const int c1 = min(a.nchan, c0 + kWaveChans);
+    double my[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) my[q] = 0.0;
+    for (int n = c0; n < c1; ++n) {
+        if (mask && !mask[n]) continue;
+        const double nu = fr[n];
+        const double phin = th[0] + kDconst * th[1] * (pow(nu, -2.0) - nuDM2) / g.P +
+                            kDconst * kDconst * th[2] * (pow(nu, -4.0) - nuGM4) / g.P;
+        const double2 W = cexp2pi(64.0 * phin);
+        const double2 *Xr = X + (int64_t)n * nharm;
+        const double2 *Mr = M + (int64_t)n * nharm;
+        double aa = 0.0, inv_e2 = 0.0;
+        if (SCAT) {
+            aa = kTwoPi * tau_lin * pow(nu / g.nu_tau, alpha);
+            inv_e2 = chan[n * 4 + 1];
+        }
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        double q1 = 0.0, q1p = 0.0, q2 = 0.0, s0 = 0.0, s1 = 0.0, s2a = 0.0, s2b = 0.0;
+        double2 E = cexp2pi((double)lane * phin);
+        for (int kb = lane; kb < nharm; kb += 64 * U) {
+            double2 xv[U];
+            double pk[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = kb + 64 * u;
+                xv[u] = (k < nharm) ? Xr[k] : cmk(0.0, 0.0);
+                if (SCAT) pk[u] = (k < nharm && k > 0) ? cabs2(Mr[k]) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double kk = (double)(kb + 64 * u);
+                const double2 y = cmul(xv[u], E);
+                if (!SCAT) {
+                    a0 += y.x;
+                    a1 = fma(kk, y.y, a1);
+                    a2 = fma(kk * kk, y.x, a2);
+                } else {
+                    const double uu = aa * kk;
+                    const double d = 1.0 / fma(uu, uu, 1.0);
+                    const double2 B = cmk(d, -uu * d);
+                    const double2 Bm1 = cmk(d - 1.0, -uu * d);
+                    const double2 be = cmul(B, Bm1);
+                    const double2 be2 = cmul(be, Bm1);
+                    const double2 cy = cmulc(y, B);
+                    const double2 qy = cmulc(y, be);
+                    a0 += cy.x;
+                    a1 = fma(kk, cy.y, a1);
+                    a2 = fma(kk * kk, cy.x, a2);
+                    q1 += qy.x;
+                    q1p = fma(kk, qy.y, q1p);
+                    q2 += fma(y.x, be2.x, y.y * be2.y);
+                    const double Pk = pk[u] * inv_e2;
+                    s0 = fma(d, Pk, s0);
+                    s1 = fma(2.0 * fma(B.x, be.x, B.y * be.y), Pk, s1);
+                    s2a = fma(2.0 * cabs2(be), Pk, s2a);
+                    s2b = fma(2.0 * fma(B.x, be2.x, B.y * be2.y), Pk, s2b);
+                }
+                E = cmul(E, W);
+            }
+        }
+        double r0 = wave_sum(a0), r1 = -kTwoPi * wave_sum(a1);
+        double r2 = -kTwoPi * kTwoPi * wave_sum(a2);
+        if (lane == n - c0) { my[0] = r0; my[1] = r1; my[2] = r2; }
+        if (SCAT) {
+            double r3 = wave_sum(q1), r4 = -kTwoPi * wave_sum(q1p), r5 = wave_sum(q2);
+            double r6 = wave_sum(s0), r7 = wave_sum(s1), r8 = wave_sum(s2a), r9 = wave_sum(s2b);
+            if (lane == n - c0) {
+                my[3] = r3; my[4] = r4; my[5] = r5; my[6] = r6; my[7] = r7; my[8] = r8; my[9] = r9;
+            }
+        } else if (lane == n - c0) {
+            my[6] = chan[n * 4 + 3];
+        }
+    }
+    // lane l owns channel c0 + l (l < kWaveChans)
+    const int n = c0 + lane;
+    if (lane < kWaveChans && n < c1 && (!mask || mask[n])) {
+        double *dst = stats + (int64_t)n * 10;
+#pragma unroll
+        for (int q = 0; q < 10; ++q) dst[q] = my[q];
+        const double C = my[0], Sn = my[6], iS = 1.0 / Sn;
+        if (!SCAT) {
+            const double nu = fr[n];
+            const double dph[3] = {1.0, kDconst * (pow(nu, -2.0) - nuDM2) / g.P,
+                                   kDconst * kDconst * (pow(nu, -4.0) - nuGM4) / g.P};
+            const double Cp = my[1], Cpp = my[2];
+            const double hn = -2.0 * (C * Cpp + Cp * Cp) * iS;
+            acc[0] = -C * C * iS;
+            for (int i = 0; i < 3; ++i) {
+                if (!(flagmask >> i & 1)) continue;
+                acc[1 + i] = -2.0 * C * Cp * dph[i] * iS;
+                for (int j = i; j < 3; ++j)
+                    if (flagmask >> j & 1) acc[6 + uidx(i, j)] = hn * dph[i] * dph[j];
+            }
+        } else {
+            Fac fc = make_fac(fr[n], g, alpha);
+            double dC[5], dS[5], d2C[5][5], d2S[5][5];
+            chan_derivs(my, fc, dC, dS, d2C, d2S);
+            const double iS2 = iS * iS, iS3 = iS2 * iS, C2 = C * C;
+            acc[0] = -C2 * iS;
+            for (int i = 0; i < 5; ++i) {
+                if (!(flagmask >> i & 1)) continue;
+                acc[1 + i] = -(2.0 * C * dC[i] * iS - C2 * dS[i] * iS2);
+                for (int j = i; j < 5; ++j)
+                    if (flagmask >> j & 1)
+                        acc[6 + uidx(i, j)] =
+                            -2.0 * (C * d2C[i][j] * iS - 0.5 * C2 * d2S[i][j] * iS2 +
+                                    dC[i] * dC[j] * iS + C2 * dS[i] * dS[j] * iS3 -
+                                    C * (dC[i] * dS[j] + dS[i] * dC[j]) * iS2);
+            }
+        }
+    }
+    // fixed-order reduction: lanes (channel order) -> waves -> block partial
+#pragma unroll
+    for (int i = 0; i < 21; ++i) acc[i] = wave_sum(acc[i]);
+    if (lane == 0)
+        for (int i = 0; i < 21; ++i) red[wave * 21 + i] = acc[i];
+    __syncthreads();
+    if (threadIdx.x < 21) {
+        double v = 0.0;
+        for (int w = 0; w < kWaves; ++w) v += red[w * 21 + threadIdx.x];
+        a.partials[((int64_t)s * nblk + blk) * 21 + threadIdx.x] = v;
+    }
+}
+
+// ===========================================================================
+// k_tr_step: one wave per sub-integration; scipy _minimize_trust_region
+// (scipy/optimize/_trustregion.py) with CGSteihaugSubproblem
+// (_trustregion_ncg.py), gtol = -1 (pptoaslib.py:1047-1048), eta 0.15,
+// initial radius 1, max radius 1000, maxiter 200 * len(x0).
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
+    __shared__ double thb[kWaves][8];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int s = blockIdx.x * kWaves + wave;
+    if (s >= a.nsub) return;
+    TRState &S = a.state[s];
+    const int phase = S.phase;
+    if (phase == PH_DONE) return;
+    const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
+    double o[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) o[i] = 0.0;
+    for (int b = lane; b < nblk; b += 64) {
+        const double *p = a.partials + ((int64_t)s * nblk + b) * 21;
+#pragma unroll
+        for (int i = 0; i < 21; ++i) o[i] += p[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 21; ++i) o[i] = wave_sum(o[i]);
+    int cmd = 0;
+    if (lane == 0) {
+        const int flagmask = S.flagmask;
+        int idx[5], nf = 0;
+        for (int i = 0; i < 5; ++i)
+            if (flagmask >> i & 1) idx[nf++] = i;
+        const int maxiter = a.max_iter > 0 ? a.max_iter : 200 * 5;
+        TRModel m;
+        bool done = false;
+        if (phase == PH_INIT) {
+            S.nfev = 1;
+            S.f = o[0];
+            for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+            for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+            if (!(o[0] == o[0])) { S.status = PPF_ST_NONFINITE; done = true; }
+        } else {
+            S.nfev += 1;
+            const double fp = o[0];
+            const double actual = S.f - fp, pred = S.f - S.pred;
+            const double rho = actual / pred;
+            if (rho < 0.25) S.radius *= 0.25;
+            else if (rho > 0.75 && S.hb) S.radius = fmin(2.0 * S.radius, 1000.0);
+            if (rho > 0.15) {
+                for (int i = 0; i < 5; ++i) S.x[i] = S.th[i];
+                S.f = fp;
+                for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+                for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+                S.slot_cur = S.slot_eval;
+            }
+            S.k += 1;
+            if (!(fp == fp)) { S.status = PPF_ST_NONFINITE; done = true; }
+            if (S.k >= maxiter) { S.status = PPF_ST_MAXITER; done = true; }
+        }
+        if (!done) {
+            m.f = S.f;
+            for (int q = 0; q < nf; ++q) {
+                m.g[q] = S.g[idx[q]];
+                for (int r = 0; r < nf; ++r) {
+                    int i = min(idx[q], idx[r]), j = max(idx[q], idx[r]);
+                    m.H[q][r] = S.H[uidx(i, j)];
+                }
+            }
+            double p[5];
+            const double jm = sqrt(dotn(m.g, m.g, nf));
+            const bool hb = cg_steihaug(m, jm, S.radius, p, nf);
+            const double pv = model_value(m, p, nf);
+            if (m.f - pv <= 0.0) {
+                done = true;                 // warnflag 2: no predicted improvement
+            } else {
+                for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
+                for (int q = 0; q < nf; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
+                S.pred = pv;
+                S.hb = hb ? 1 : 0;
+                S.slot_eval = S.slot_cur ^ 1;
+                cmd = 1;
+            }
+        }
+        if (done) S.phase = PH_DONE;
+        else S.phase = PH_PROPOSAL;
+        for (int i = 0; i < 5; ++i) thb[wave][i] = S.th[i];
+        thb[wave][5] = (double)cmd;
+    }
+    cmd = __shfl(cmd, 0, 64);
+    if (!cmd) return;
+    if (lane == 0) atomicAdd(a.active, 1u);
+    if (S.scat) {
+        // reference gates at the proposal (taus.sum(), dtau.sum(), dalpha.sum())
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const double t3 = __shfl(lane == 0 ? S.th[3] : 0.0, 0, 64);
+        const double t4 = __shfl(lane == 0 ? S.th[4] : 0.0, 0, 64);
+        const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+        int gs, gt, ga;
+        wave_gates(a.freqs + (int64_t)s * a.nchan, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
+                   a.nchan, tl, t4, S.nu_fit[2], a.log10_tau, gs, gt, ga);
+        if (lane == 0) { S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga; }
+    }
+}
+
+// nu_zero-case accumulation slots
+enum { NZ_MAX = 16 };
+
+// ===========================================================================
+// k_postfit: one workgroup per sub-integration
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
+    __shared__ double red[kWaves * 32];
+    __shared__ double sh_Xinv[25];
+    __shared__ double sh_misc[16];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const TRState &S = a.state[s];
+    ppf_result *res = a.results + s;
+    if (S.status == PPF_ST_NOFIT) {
+        if (tid == 0) {
+            for (int i = 0; i < 32; ++i) reinterpret_cast<double *>(res)[i] = 0.0;
+            res->status = PPF_ST_NOFIT;
+            res->phi_guess = S.phi_guess;
+        }
+        for (int n = tid; n < a.nchan; n += kBlock) {
+            const int64_t o2 = (int64_t)s * a.nchan + n;
+            a.scales[o2] = 0.0; a.scale_errs[o2] = 0.0; a.channel_snrs[o2] = 0.0;
+        }
+        return;
+    }
+    struct { const double *fr; const uint8_t *mask; int nchan; } v;
+    v.fr = a.freqs + (int64_t)s * a.nchan;
+    v.mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    v.nchan = a.nchan;
+    const int flagmask = S.flagmask;
+    int idx[5], nf = 0;
+    for (int i = 0; i < 5; ++i)
+        if (flagmask >> i & 1) idx[nf++] = i;
+    double x[5];
+    for (int i = 0; i < 5; ++i) x[i] = S.x[i];
+    const double fun = S.f;
+    const int status = S.status, nfev = S.nfev, k = S.k;
+    const bool scat = S.scat != 0;
+    const double nu_mean = S.nu_mean, Sd = S.Sd, dof = S.dof, phi_guess = S.phi_guess;
+    const int nchanx = S.nchanx;
+    FitGeom g;
+    g.P = a.P[s];
+    g.nu_DM = S.nu_fit[0];
+    g.nu_GM = S.nu_fit[1];
+    g.nu_tau = S.nu_fit[2];
+    g.log10_tau = a.log10_tau;
+    g.tau_lin = 0.0;
+    g.g_sum = g.g_tau = g.g_alpha = false;
+    const double *st_fit = a.stats + ((int64_t)s * 2 + S.slot_cur) * a.nchan * 10;
+
+    // ---- gates at the fit point ---------------------------------------------------
+    const double tau_fit_lin = a.log10_tau ? pow(10.0, x[3]) : x[3];
+    auto gates = [&](FitGeom &gg, double taulin, double alpha) {
+        gg.tau_lin = taulin;
+        if (!scat) { gg.g_sum = gg.g_tau = gg.g_alpha = false; return; }
+        double sm[3] = {0.0, 0.0, 0.0};
+        for (int n = tid; n < v.nchan; n += kBlock) {
+            if (v.mask && !v.mask[n]) continue;
+            double tn = taulin * pow(v.fr[n] / gg.nu_tau, alpha);
+            sm[0] += tn;
+            sm[1] += gg.log10_tau ? kLn10 * tn : tn / taulin;
+            sm[2] += log(v.fr[n] / gg.nu_tau) * tn;
+        }
+        block_sum<3>(sm, red);
+        gg.g_sum = sm[0] != 0.0;
+        gg.g_tau = gg.g_sum && sm[1] != 0.0;
+        gg.g_alpha = sm[2] != 0.0;
+    };
+    gates(g, tau_fit_lin, x[4]);
+
+    // ---- zero-covariance frequencies (pptoaslib.py:776-950) -------------------------
+    double nu_out[3];
+    bool need_nz = false;
+    for (int i = 0; i < 3; ++i) {
+        nu_out[i] = a.nu_outs[(int64_t)s * 3 + i];
+        if (!(nu_out[i] == nu_out[i]) || nu_out[i] == 0.0) need_nz = true;
+    }
+    int nzcase = flagmask;
+    if (a.mode == PPF_MODE_LEGACY2) nzcase = 0x3;
+    if (nzcase == 0x1f) nzcase = 0x1b;   // [1,1,1,1,1] -> [1,1,0,1,1]
+    double nz[3] = {g.nu_DM, g.nu_GM, g.nu_tau};
+    bool no_root = false;
+    const bool closed = (nzcase == 0x3 || nzcase == 0x5 || nzcase == 0x18 || nzcase == 0xb ||
+                         nzcase == 0x7 || nzcase == 0x1b || nzcase == 0xf);
+    if (need_nz && closed) {
+        double accv[NZ_MAX + 8];
+        for (int i = 0; i < NZ_MAX + 8; ++i) accv[i] = 0.0;
+        const double cD = kDconst / g.P, cG = kDconst * kDconst / g.P;
+        for (int n = tid; n < v.nchan; n += kBlock) {
+            if (v.mask && !v.mask[n]) continue;
+            const double *st = st_fit + (int64_t)n * 10;
+            const double nu = v.fr[n];
+            Fac fc = make_fac(nu, g, x[4]);
+            double H[5][5], Hd[5][5], Hg[5][5], Ha[5][5];
+            chan_hess(st, fc, H);
+            Fac f1 = fc; f1.dphi[1] = 1.0; chan_hess(st, f1, Hd);
+            Fac f2 = fc; f2.dphi[2] = 1.0; chan_hess(st, f2, Hg);
+            double rd[5], rg[5], ra[5];
+            for (int b = 0; b < 5; ++b) { rd[b] = Hd[1][b]; rg[b] = Hg[2][b]; }
+            rd[1] = Hd[1][1] * fc.dphi[1];
+            rg[2] = Hg[2][2] * fc.dphi[2];
+            if (nzcase == 0x18 || nzcase == 0x1b) {
+                Fac f3 = fc;
+                if (fc.t[1] != 0.0) {
+                    f3.u[1] = fc.u[1] / fc.t[1];
+                    f3.u[2] = fc.u[2] / fc.t[1];
+                }
+                f3.t[1] = 1.0;
+                chan_hess(st, f3, Ha);
+                for (int b = 0; b < 5; ++b) ra[b] = Ha[4][b];
+            }
+            const double w2 = pow(nu, -2.0), w4 = pow(nu, -4.0), wl = log(nu);
+            double *c = accv;
+            switch (nzcase) {
+                case 0x3: c[0] += w2 * rd[0]; c[1] += rd[0]; break;
+                case 0x5: c[0] += w4 * rg[0]; c[1] += rg[0]; break;
+                case 0x18: c[0] += wl * ra[3]; c[1] += ra[3]; break;
+                case 0xb:
+                    c[0] += w2 * rd[3]; c[1] += w2 * rd[0]; c[2] += rd[3]; c[3] += rd[0];
+                    c[16] += H[3][0]; c[17] += H[3][3];
+                    break;
+                case 0x7:
+                    if (a.option == 0) {
+                        c[0] += w4 * rg[0]; c[1] += rg[0]; c[2] += w2 * rd[2]; c[3] += rd[2];
+                        c[4] += w4 * rg[2]; c[5] += rg[2]; c[6] += w2 * rd[0]; c[7] += rd[0];
+                    } else {
+                        c[0] += w4 * rd[0]; c[1] += rd[0]; c[2] += w2 * rg[1]; c[3] += rg[1];
+                        c[4] += w4 * rd[1]; c[5] += rd[1]; c[6] += w2 * rg[0]; c[7] += rg[0];
+                    }
+                    break;
+                case 0x1b:
+                    c[0] += w2 * rd[0]; c[1] += w2 * rd[3]; c[2] += w2 * rd[4];
+                    c[3] += rd[0]; c[4] += rd[3]; c[5] += rd[4];
+                    c[6] += wl * ra[0]; c[7] += wl * ra[1]; c[8] += wl * ra[3];
+                    c[9] += ra[0]; c[10] += ra[1]; c[11] += ra[3];
+                    {   // totals over (phi, DM, tau, alpha): 10 unique
+                        const int r4[4] = {0, 1, 3, 4};
+                        int q = 12;
+                        for (int i = 0; i < 4; ++i)
+                            for (int j = i; j < 4; ++j) c[q++] += H[r4[i]][r4[j]];
+                    }
+                    break;
+                case 0xf: {
+                    double d0 = rd[0] * cD, d1 = rd[1] * cD, d2 = rd[2] * cD, d3 = rd[3] * cD;
+                    double e0 = rg[0] * cG, e1 = rg[1] * cG, e2 = rg[2] * cG, e3 = rg[3] * cG;
+                    if (a.option == 0) {
+                        c[0] += w4 * e3; c[1] += e3; c[2] += w2 * d0; c[3] += d0;
+                        c[4] += w4 * e0; c[5] += e0; c[6] += w2 * d2; c[7] += d2;
+                        c[8] += w4 * e2; c[9] += e2; c[10] += w2 * d3; c[11] += d3;
+                    } else {
+                        c[0] += w2 * d3; c[1] += d3; c[2] += w4 * e0; c[3] += e0;
+                        c[4] += w2 * d0; c[5] += d0; c[6] += w4 * e1; c[7] += e1;
+                        c[8] += w2 * d1; c[9] += d1; c[10] += w4 * e3; c[11] += e3;
+                    }
+                    c[16] += H[3][0]; c[17] += H[3][3];
+                    break;
+                }
+                default: break;
+            }
+        }
+        block_sum<NZ_MAX + 8>(accv, red);
+        if (tid == 0) {
+            const double *c = accv;
+            double num, den;
+            switch (nzcase) {
+                case 0x3: nz[0] = pow(c[0] / c[1], -0.5); break;
+                case 0x5: nz[1] = pow(c[0] / c[1], -0.25); break;
+                case 0x18: nz[2] = exp(c[0] / c[1]); break;
+                case 0xb: {
+                    double H13 = c[16], H33 = c[17];
+                    num = H13 * c[0] - H33 * c[1];
+                    den = H13 * c[2] - H33 * c[3];
+                    nz[0] = pow(num / den, -0.5);
+                    break;
+                }
+                case 0x7: {
+                    if (a.option == 0 || a.option == 1) {
+                        double A = c[0], B = c[1], C = c[2], D = c[3], E = c[4], F = c[5], G = c[6],
+                               H = c[7];
+                        double co[7] = {A * C - E * G, 0.0, E * H - A * D, 0.0, F * G - B * C, 0.0,
+                                        B * D - F * H};
+                        double roots[8];
+                        int nr = poly_real_roots(co, 6, roots);
+                        double best = 0.0, bd = 1e300;
+                        bool any = false;
+                        for (int i = 0; i < nr; ++i)
+                            if (roots[i] > 0.0 && fabs(nu_mean - roots[i]) < bd) {
+                                bd = fabs(nu_mean - roots[i]); best = roots[i]; any = true;
+                            }
+                        if (any) { nz[0] = nz[1] = best; } else no_root = true;
+                    }
+                    break;
+                }
+                case 0x1b: {
+                    double T[4][4];
+                    int q = 12;
+                    for (int i = 0; i < 4; ++i)
+                        for (int j = i; j < 4; ++j) { T[i][j] = T[j][i] = c[q]; ++q; }
+                    double H11 = T[0][0], H22 = T[1][1], H33 = T[2][2], H44 = T[3][3];
+                    double H12 = T[0][1], H13 = T[0][2], H14 = T[0][3], H23 = T[1][2],
+                           H34 = T[2][3];
+                    num = (H34 * H34 - H33 * H44) * c[0] + (H13 * H44 - H14 * H34) * c[1] +
+                          (H14 * H33 - H13 * H34) * c[2];
+                    den = (H34 * H34 - H33 * H44) * c[3] + (H13 * H44 - H14 * H34) * c[4] +
+                          (H14 * H33 - H13 * H34) * c[5];
+                    nz[0] = pow(num / den, -0.5);
+                    num = (H13 * H22 - H12 * H23) * c[6] + (H11 * H23 - H12 * H13) * c[7] +
+                          (H12 * H12 - H11 * H22) * c[8];
+                    den = (H13 * H22 - H12 * H23) * c[9] + (H11 * H23 - H12 * H13) * c[10] +
+                          (H12 * H12 - H11 * H22) * c[11];
+                    nz[2] = exp(num / den);
+                    break;
+                }
+                case 0xf: {
+                    if (a.option == 0 || a.option == 1) {
+                        double H14 = c[16], H44 = c[17];
+                        double A = c[0], aa = c[1], B = c[2], b = c[3], C = c[4], cc = c[5],
+                               D = c[6], d = c[7], E = c[8], e = c[9], F = c[10], f = c[11];
+                        double co[6];
+                        int deg;
+                        if (a.option == 0) {
+                            co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
+                                    H14 * A * D;
+                            co[1] = -A * A * b - H44 * C * d - H14 * E * f + H44 * b * E + A * C * f +
+                                    H14 * A * d;
+                            co[2] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
+                                    (A * cc + aa * C) * F + H14 * aa * D;
+                            co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
+                                    (A * cc + aa * C) * f - H14 * aa * d;
+                            co[4] = aa * aa * B - aa * cc * F;
+                            co[5] = -aa * aa * b + aa * cc * f;
+                            deg = 5;
+                        } else {
+                            co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
+                                    H14 * A * D;
+                            co[1] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
+                                    (A * cc + aa * C) * F + H14 * aa * D;
+                            co[2] = -(A * A * b - aa * aa * B) - H44 * C * d - H14 * E * f +
+                                    H44 * b * E + (A * C * f - aa * cc * F) + H14 * A * d;
+                            co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
+                                    (A * cc + aa * C) * f - H14 * aa * d;
+                            co[4] = -aa * aa * b + aa * cc * f;
+                            deg = 4;
+                        }
+                        double roots[8];
+                        int nr = poly_real_roots(co, deg, roots);
+                        double best = 0.0, bd = 1e300;
+                        bool any = false;
+                        for (int i = 0; i < nr; ++i)
+                            if (roots[i] > 0.0) {
+                                double rr = sqrt(roots[i]);
+                                if (fabs(nu_mean - rr) < bd) { bd = fabs(nu_mean - rr); best = rr; any = true; }
+                            }
+                        if (any) { nz[0] = nz[1] = best; } else no_root = true;
+                    }
+                    break;
+                }
+                default: break;
+            }
+            sh_misc[4] = nz[0]; sh_misc[5] = nz[1]; sh_misc[6] = nz[2];
+            sh_misc[7] = no_root ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        nz[0] = sh_misc[4]; nz[1] = sh_misc[5]; nz[2] = sh_misc[6];
+        no_root = sh_misc[7] != 0.0;
+        __syncthreads();
+    }
+    if (need_nz)
+        for (int i = 0; i < 3; ++i)
+            if (!(nu_out[i] == nu_out[i]) || nu_out[i] == 0.0) nu_out[i] = nz[i];
+    if (a.mode == PPF_MODE_LEGACY2) { nu_out[1] = nu_out[0]; nu_out[2] = g.nu_tau; }
+    if (a.is_toa) {
+        if (flagmask & 2) nu_out[1] = nu_out[0];
+        else if (flagmask & 4) nu_out[0] = nu_out[1];
+    }
+
+    // ---- output transform (pptoaslib.py:1100-1114) -----------------------------------
+    const double P = g.P;
+    double phi_inf = x[0] + kDconst * x[1] * (0.0 - pow(g.nu_DM, -2.0)) / P +
+                     kDconst * kDconst * x[2] * (0.0 - pow(g.nu_GM, -4.0)) / P;
+    double phi_out = phi_inf + (kDconst / P) * x[1] * pow(nu_out[0], -2.0) +
+                     (kDconst * kDconst / P) * x[2] * pow(nu_out[1], -4.0);
+    if (fabs(phi_out) >= 0.5) phi_out = phi_out - floor(phi_out);
+    if (phi_out >= 0.5) phi_out -= 1.0;
+    double tau_out_lin = tau_fit_lin * pow(nu_out[2] / g.nu_tau, x[4]);
+    double tau_out = a.log10_tau ? log10(tau_out_lin) : tau_out_lin;
+
+    // ---- covariance at the output reference frequencies (Schur complement of
+    //      fit_portrait_full_function_2deriv_with_scales, pptoaslib.py:687-773)
+    FitGeom go = g;
+    go.nu_DM = nu_out[0];
+    go.nu_GM = nu_out[1];
+    go.nu_tau = nu_out[2];
+    gates(go, tau_out_lin, x[4]);
+    double cv[31];
+    for (int i = 0; i < 31; ++i) cv[i] = 0.0;
+    for (int n = tid; n < v.nchan; n += kBlock) {
+        if (v.mask && !v.mask[n]) continue;
+        const double *st = st_fit + (int64_t)n * 10;
+        Fac fc = make_fac(v.fr[n], go, x[4]);
+        double dC[5], dS[5], d2C[5][5], d2S[5][5];
+        chan_derivs(st, fc, dC, dS, d2C, d2S);
+        const double C = st[0], S = st[6], an = C / S;
+        double U[5];
+        for (int i = 0; i < 5; ++i) U[i] = (flagmask >> i & 1) ? -2.0 * (dC[i] - an * dS[i]) : 0.0;
+        const double cinv = 1.0 / (2.0 * S);
+        int q = 0;
+        for (int i = 0; i < 5; ++i)
+            for (int j = i; j < 5; ++j) {
+                if ((flagmask >> i & 1) && (flagmask >> j & 1)) {
+                    cv[q] += -2.0 * (C * d2C[i][j] / S - 0.5 * C * C * d2S[i][j] / (S * S));
+                    cv[15 + q] += U[i] * U[j] * cinv;
+                }
+                ++q;
+            }
+    }
+    block_sum<31>(cv, red);
+    int sing = 0;
+    if (tid == 0) {
+        double Xm[5][5], Xi[5][5];
+        double full[5][5];
+        int q = 0;
+        for (int i = 0; i < 5; ++i)
+            for (int j = i; j < 5; ++j) { full[i][j] = full[j][i] = cv[q] - cv[15 + q]; ++q; }
+        for (int i2 = 0; i2 < nf; ++i2)
+            for (int j2 = 0; j2 < nf; ++j2) Xm[i2][j2] = full[idx[i2]][idx[j2]];
+        if (!invert_small(Xm, Xi, nf)) sing = 1;
+        for (int i2 = 0; i2 < 25; ++i2) sh_Xinv[i2] = 0.0;
+        for (int i2 = 0; i2 < nf; ++i2)
+            for (int j2 = 0; j2 < nf; ++j2) sh_Xinv[i2 * 5 + j2] = Xi[i2][j2];
+        sh_misc[8] = (double)sing;
+    }
+    __syncthreads();
+    sing = (int)sh_misc[8];
+    double Xinv[5][5];
+    for (int i2 = 0; i2 < 5; ++i2)
+        for (int j2 = 0; j2 < 5; ++j2) Xinv[i2][j2] = sh_Xinv[i2 * 5 + j2];
+    // per-channel scales, scale errors, channel S/N
+    double sn[1] = {0.0};
+    for (int n = tid; n < v.nchan; n += kBlock) {
+        const int64_t o2 = (int64_t)s * a.nchan + n;
+        if (v.mask && !v.mask[n]) {
+            a.scales[o2] = 0.0; a.scale_errs[o2] = 0.0; a.channel_snrs[o2] = 0.0;
+            continue;
+        }
+        const double *st = st_fit + (int64_t)n * 10;
+        Fac fc = make_fac(v.fr[n], go, x[4]);
+        double dC[5], dS[5], d2C[5][5], d2S[5][5];
+        chan_derivs(st, fc, dC, dS, d2C, d2S);
+        const double C = st[0], S = st[6], an = C / S;
+        double U[5];
+        for (int i2 = 0; i2 < nf; ++i2) U[i2] = -2.0 * (dC[idx[i2]] - an * dS[idx[i2]]);
+        double quad = 0.0;
+        for (int i2 = 0; i2 < nf; ++i2)
+            for (int j2 = 0; j2 < nf; ++j2) quad += U[i2] * Xinv[i2][j2] * U[j2];
+        const double cinv = 1.0 / (2.0 * S);
+        double var = 2.0 * (cinv + quad * cinv * cinv);
+        double serr = (a.mode == PPF_MODE_LEGACY2) ? pow(S, -0.5) : sqrt(var);
+        double csnr = an * sqrt(S);
+        a.scales[o2] = an;
+        a.scale_errs[o2] = serr;
+        a.channel_snrs[o2] = csnr;
+        sn[0] += csnr * csnr;
+    }
+    block_sum<1>(sn, red);
+    if (tid == 0) {
+        double pe[5] = {0, 0, 0, 0, 0};
+        double *cov = a.covariance + (int64_t)s * 25;
+        for (int i2 = 0; i2 < 25; ++i2) cov[i2] = 0.0;
+        for (int i2 = 0; i2 < nf; ++i2) {
+            for (int j2 = 0; j2 < nf; ++j2) cov[i2 * 5 + j2] = 2.0 * Xinv[i2][j2];
+            pe[idx[i2]] = sqrt(2.0 * Xinv[i2][i2]);
+        }
+        double params[5] = {phi_out, x[1], x[2], tau_out, x[4]};
+        for (int i2 = 0; i2 < 5; ++i2) { res->params[i2] = params[i2]; res->param_errs[i2] = pe[i2]; }
+        for (int i2 = 0; i2 < 3; ++i2) res->nu_out[i2] = nu_out[i2];
+        res->nu_fit[0] = g.nu_DM; res->nu_fit[1] = g.nu_GM; res->nu_fit[2] = g.nu_tau;
+        res->chi2 = Sd + fun;
+        res->red_chi2 = (Sd + fun) / dof;
+        res->snr = sqrt(sn[0]);
+        res->fun = fun;
+        res->Sd = Sd;
+        res->phi_guess = phi_guess;
+        res->nfeval = (double)nfev;
+        int st2 = status;
+        if (no_root) st2 |= PPF_ST_NO_ROOT;
+        if (sing) st2 |= PPF_ST_SINGULAR;
+        if (!(fun == fun)) st2 |= PPF_ST_NONFINITE;
+        res->status = (double)st2;
+        res->niter = (double)k;
+        res->dof = dof;
+        res->nchanx = (double)nchanx;
+        res->x_fit_phi = x[0];
+        res->x_fit_tau = x[3];
+        res->reserved[0] = res->reserved[1] = res->reserved[2] = 0.0;
+    }
+}
+
+// ===========================================================================
+// launchers
+// ===========================================================================
+static int pass_unroll(int nharm) {
+    int j = (nharm + 63) / 64;
+    return j >= 17 ? 17 : j >= 9 ? 9 : j >= 5 ? 5 : j >= 3 ? 3 : j >= 2 ? 2 : 1;
+}
+
+hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_tr_init, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
+                       st, a);
+    return hipGetLastError();
+}
+
+template <bool SCAT>
+static void launch_pass_t(const SolveArgs &a, hipStream_t st, dim3 g) {
+    switch (pass_unroll(a.nbin / 2 + 1)) {
+        case 1: hipLaunchKernelGGL((k_pass<SCAT, 1>), g, dim3(kBlock), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_pass<SCAT, 2>), g, dim3(kBlock), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((k_pass<SCAT, 3>), g, dim3(kBlock), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((k_pass<SCAT, 5>), g, dim3(kBlock), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((k_pass<SCAT, 9>), g, dim3(kBlock), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_pass<SCAT, 17>), g, dim3(kBlock), 0, st, a); break;
+    }
+}
+
+hipError_t launch_pass(const SolveArgs &a, hipStream_t st) {
+    const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
+    dim3 g((unsigned)((int64_t)a.nsub * nblk));
+    if (a.any_plain) launch_pass_t<false>(a, st, g);
+    if (a.any_scat) launch_pass_t<true>(a, st, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_tr_step, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
+                       st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_postfit(const SolveArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_postfit, dim3((unsigned)a.nsub), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
+size_t tr_state_bytes() { return sizeof(TRState); }
+int pass_blocks(int nchan) { return (nchan + kPassChans - 1) / kPassChans; }
+
+}  // namespace ppf

@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--nbin", type=int, default=2048)
     ap.add_argument("--chunk", type=int, default=2500,
                     help="sub-integrations per ppf_fit_batch call")
-    ap.add_argument("--cpu-sample", type=int, default=8,
+    ap.add_argument("--cpu-sample", type=int, default=48,
                     help="sub-integrations for the CPU baseline (0: skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
                                                   "pmc_summary.json"))

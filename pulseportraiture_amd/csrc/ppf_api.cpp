@@ -237,6 +237,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ppf::XspecArgs xa{};
     xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = ilog2(d->nbin / 2);
     xa.kc = kc; xa.nblk = L.nblk; xa.cb = L.cb; xa.dtype = d->data_dtype;
+    xa.xcd_swizzle = (L.nblk % 8 == 0) ? 1 : 0;
     xa.data = d->data; xa.Mft = Mft; xa.model_index = d->model_index; xa.mask = d->chan_mask;
     xa.errs = d->errs; xa.freqs = d->freqs; xa.P = d->P; xa.T = T; xa.T2 = T2;
     xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);

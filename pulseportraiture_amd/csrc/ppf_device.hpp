@@ -152,6 +152,72 @@ __device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, 
     }
 }
 
+// Compile-time-size variant of lds_fft (exact register footprint, unrolled
+// passes); T may live in LDS or global memory.
+template <int LOG2N, bool INV>
+__device__ __forceinline__ void lds_fft_t(double2 *buf, const double2 *T) {
+    constexpr int N = 1 << LOG2N;
+    const int tid = threadIdx.x;
+    int L = 1;
+    if constexpr ((LOG2N & 1) != 0) {
+        constexpr int nb = N / 2;
+        constexpr int Q = (nb + kBlock - 1) / kBlock;
+        double2 a[Q], b[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < nb) { a[q] = buf[j]; b[q] = buf[j + nb]; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < nb) { buf[2 * j] = cadd(a[q], b[q]); buf[2 * j + 1] = csub(a[q], b[q]); }
+        }
+        __syncthreads();
+        L = 2;
+    }
+    constexpr int nb = N / 4;
+    constexpr int Q = (nb + kBlock - 1) / kBlock;
+#pragma unroll
+    for (int pass = 0; pass < LOG2N / 2; ++pass) {
+        const int tstride = N / (4 * L);
+        double2 x[Q][4];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < nb) {
+                const int k = j & (L - 1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[q][r] = buf[j + r * nb];
+                if (k) {
+                    x[q][1] = cmul(x[q][1], twid(T, k * tstride, INV));
+                    x[q][2] = cmul(x[q][2], twid(T, 2 * k * tstride, INV));
+                    x[q][3] = cmul(x[q][3], twid(T, 3 * k * tstride, INV));
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < nb) {
+                const int k = j & (L - 1);
+                const double2 s02 = cadd(x[q][0], x[q][2]), d02 = csub(x[q][0], x[q][2]);
+                const double2 s13 = cadd(x[q][1], x[q][3]), d13 = csub(x[q][1], x[q][3]);
+                const double2 id13 = INV ? cmk(-d13.y, d13.x) : cmk(d13.y, -d13.x);
+                const int o = (j - k) * 4 + k;
+                buf[o] = cadd(s02, s13);
+                buf[o + L] = cadd(d02, id13);
+                buf[o + 2 * L] = csub(s02, s13);
+                buf[o + 3 * L] = csub(d02, id13);
+            }
+        }
+        __syncthreads();
+        L <<= 2;
+    }
+}
+
 // Real FFT post-pass: X_k (k = 0..N) from Z = FFT_N(x_even + i x_odd).
 // T2[k] = exp(-i pi k / N), k < N.
 __device__ __forceinline__ double2 rfft_bin(const double2 *buf, int N, const double2 *__restrict__ T2, int k) {

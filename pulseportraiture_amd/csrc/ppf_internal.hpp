@@ -15,7 +15,7 @@ struct RfftArgs {
 };
 
 struct XspecArgs {
-    int nsub, nchan, nbin, log2N, kc, nblk, cb, dtype;
+    int nsub, nchan, nbin, log2N, kc, nblk, cb, dtype, xcd_swizzle;
     const void *data;
     const double2 *Mft;          // [nmodel][nchan][N+1]
     const int32_t *model_index;

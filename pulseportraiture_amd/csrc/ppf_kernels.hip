@@ -12,6 +12,8 @@
 //                   streaming pass over X; then zero-covariance frequencies,
 //                   output transform, O(nchan) Schur covariance, scales, S/N
 // Standalone kernels: k_rotate, k_noise, k_phase_shift, k_synth.
+#include <type_traits>
+
 #include "ppf_device.hpp"
 #include "ppf_internal.hpp"
 
@@ -65,18 +67,39 @@ __global__ __launch_bounds__(kBlock) void k_rfft_rows(RfftArgs a) {
 // ===========================================================================
 // k_xspec: one workgroup per (sub-integration, block of channels)
 // ===========================================================================
-template <int KMAX>
+template <int LOG2N, int DT>
 __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
+    constexpr int N = 1 << LOG2N, NH = N + 1;
+    constexpr bool TWL = (N <= 1024);                 // twiddles in LDS
+    constexpr int ZP = (N + kBlock - 1) / kBlock;      // row elements / thread
+    constexpr int KM = (NH + kBlock - 1) / kBlock;     // harmonics / thread
+    using RowT = typename std::conditional<DT == 0, float2, double2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
-    const int N = a.nbin >> 1, nharm = N + 1;
-    const int s = blockIdx.x / a.nblk, cb = blockIdx.x % a.nblk;
-    const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
+    double2 *buf = lds;
     const int tid = threadIdx.x;
+    if (TWL) {
+        for (int j = tid; j < N; j += kBlock) { lds[N + j] = a.T[j]; lds[2 * N + j] = a.T2[j]; }
+    }
+    const double2 *T = TWL ? lds + N : a.T;
+    const double2 *T2 = TWL ? lds + 2 * N : a.T2;
+    // XCD-aware block -> (sub-int, channel block): blocks b and b+8 share an
+    // XCD, so each XCD keeps only its channel blocks' model rows in its L2
+    int s, cb;
+    if (a.xcd_swizzle) {
+        const int per = a.nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
+        cb = x * per + r % per;
+        s = r / per;
+    } else {
+        s = blockIdx.x / a.nblk;
+        cb = blockIdx.x % a.nblk;
+    }
+    const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
-    const double sqrt_half_nbin = sqrt((double)a.nbin / 2.0);
+    const double sqrt_half_nbin = sqrt((double)(2 * N) / 2.0);
+    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
 
     // guess stage: dedispersion phase of each channel, relative to the mean
     // frequency of the usable channels (pptoas.py:439,462-464)
@@ -86,78 +109,101 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         for (int n = tid; n < a.nchan; n += kBlock)
             if (!mask || mask[n]) { v[0] += fr[n]; v[1] += 1.0; }
         block_sum<2>(v, red);
-        double nu_mean = v[0] / v[1];
         Dg = kDconst * a.guess_DM[s] / a.P[s];
-        nu_mean_m2 = pow(nu_mean, -2.0);
+        nu_mean_m2 = pow(v[0] / v[1], -2.0);
     }
-    // per-thread guess accumulators for harmonics k = tid + kBlock*i
-    double2 R[KMAX], Mb[KMAX];
-    if (a.guess) {
+    double2 R[KM], Mb[KM];
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) { R[i] = cmk(0, 0); Mb[i] = cmk(0, 0); }
-    }
+    for (int i = 0; i < KM; ++i) { R[i] = cmk(0, 0); Mb[i] = cmk(0, 0); }
     double wsum = 0.0, wcnt = 0.0;
 
-    for (int n = c0; n < c1; ++n) {
-        const int64_t crow = (int64_t)s * a.nchan + n;
-        double *chan = a.chan + crow * 4;
-        if (mask && !mask[n]) {
-            if (tid == 0) { chan[0] = 0.0; chan[1] = 0.0; chan[2] = 0.0; chan[3] = 0.0; }
-            continue;
+    auto skip_masked = [&](int n) {
+        while (n < c1 && mask && !mask[n]) {
+            if (tid < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + tid] = 0.0;
+            ++n;
         }
-        load_row(lds, a.data, a.dtype, crow, a.nbin);
-        __syncthreads();
-        lds_fft(lds, a.log2N, a.T, false);
-        // D_k for my harmonics, noise power over k >= kc, data power k >= 1
-        double2 Dk[KMAX];
-        double acc[2] = {0.0, 0.0};
+        return n;
+    };
+    RowT zr[ZP];
+    auto prefetch = [&](int n) {
+        const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) {
-            int k = tid + i * kBlock;
-            if (k <= N) {
-                Dk[i] = rfft_bin(lds, N, a.T2, k);
-                double p2 = cabs2(Dk[i]);
-                if (k >= a.kc) acc[0] += p2;
-                if (k >= 1) acc[1] += p2;
-            }
+        for (int q = 0; q < ZP; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < N) zr[q] = src[j];
         }
-        block_sum<2>(acc, red);   // (also orders the LDS reads before reuse)
-        double errs_FT;
-        if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
-        else errs_FT = sqrt(acc[0] / (double)(nharm - a.kc) / (double)a.nbin) * sqrt_half_nbin;
-        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-        // cross spectrum and model power
-        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * nharm;
-        double2 *Xrow = a.X + crow * nharm;
-        double mpow[1] = {0.0};
+    };
+    int n = skip_masked(c0);
+    if (n < c1) prefetch(n);
+    while (n < c1) {
+        const int64_t crow = (int64_t)s * a.nchan + n;
+#pragma unroll
+        for (int q = 0; q < ZP; ++q) {
+            const int j = tid + q * kBlock;
+            if (j < N) buf[j] = cmk((double)zr[q].x, (double)zr[q].y);
+        }
+        const int nn = skip_masked(n + 1);
+        if (nn < c1) prefetch(nn);              // next row in flight during this FFT
+        // guess phasors first: the sincos temporaries are dead before the
+        // FFT / spectrum registers go live
         double2 Eg = cmk(1, 0), Wg = cmk(1, 0);
         double wn = 0.0;
         if (a.guess) {
-            double phg = Dg * (pow(fr[n], -2.0) - nu_mean_m2);
+            const double phg = Dg * (pow(fr[n], -2.0) - nu_mean_m2);
             Eg = cexp2pi((double)tid * phg);
             Wg = cexp2pi((double)kBlock * phg);
             wn = a.guess_weights[crow];
         }
+        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+        double2 Mv[KM];
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) {
-            int k = tid + i * kBlock;
+        for (int i = 0; i < KM; ++i) {
+            const int k = tid + i * kBlock;
+            if (k <= N) Mv[i] = Mrow[k];
+        }
+        __syncthreads();
+        lds_fft_t<LOG2N, false>(buf, T);
+        // pass 1 over my harmonics: power sums and the guess accumulation
+        double acc[2] = {0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+            const int k = tid + i * kBlock;
             if (k <= N) {
-                double2 M = Mrow[k];
-                if (k == 0) {
-                    Xrow[0] = cmk(0.0, 0.0);       // F0_fact = 0 (pplib.py:82)
-                } else {
-                    mpow[0] += cabs2(M);
-                    Xrow[k] = cscale(cmulc(Dk[i], M), inv_e2);
-                }
+                const double2 D = rfft_bin(buf, N, T2, k);
+                const double p2 = cabs2(D);
+                if (k >= a.kc) acc[0] += p2;
+                if (k >= 1) acc[1] += p2;
                 if (a.guess) {
-                    R[i] = cadd(R[i], cscale(cmul(Dk[i], Eg), wn));
-                    Mb[i] = cadd(Mb[i], M);
+                    R[i] = cadd(R[i], cscale(cmul(D, Eg), wn));
                     Eg = cmul(Eg, Wg);
                 }
             }
         }
+        block_sum<2>(acc, red);                 // buf is not modified here
+        double errs_FT;
+        if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
+        else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)(2 * N)) * sqrt_half_nbin;
+        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+        double2 *Xrow = a.X + crow * NH;
+        double mpow[1] = {0.0};
+        // pass 2: cross spectrum (D recomputed from the LDS spectrum)
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {
+            const int k = tid + i * kBlock;
+            if (k <= N) {
+                const double2 M = Mv[i];
+                if (k == 0) {
+                    Xrow[0] = cmk(0.0, 0.0);       // F0_fact = 0 (pplib.py:82)
+                } else {
+                    mpow[0] += cabs2(M);
+                    Xrow[k] = cscale(cmulc(rfft_bin(buf, N, T2, k), M), inv_e2);
+                }
+                if (a.guess) Mb[i] = cadd(Mb[i], M);
+            }
+        }
         block_sum<1>(mpow, red);
         if (tid == 0) {
+            double *chan = a.chan + crow * 4;
             chan[0] = errs_FT;
             chan[1] = inv_e2;
             chan[2] = acc[1] * inv_e2;     // Sd_n
@@ -165,12 +211,13 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         }
         wsum += wn;
         wcnt += 1.0;
+        n = nn;
     }
     if (a.guess) {
-        const int64_t base = ((int64_t)s * a.nblk + cb) * nharm;
+        const int64_t base = ((int64_t)s * a.nblk + cb) * NH;
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) {
-            int k = tid + i * kBlock;
+        for (int i = 0; i < KM; ++i) {
+            const int k = tid + i * kBlock;
             if (k <= N) { a.gR[base + k] = R[i]; a.gM[base + k] = Mb[i]; }
         }
         if (tid == 0) {
@@ -520,18 +567,26 @@ hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st) {
     hipLaunchKernelGGL(k_rfft_rows, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
-static inline int kmax_for(int N) { return (N + 1 + kBlock - 1) / kBlock; }
+template <int L2>
+static void launch_xspec_t(const XspecArgs &a, hipStream_t st) {
+    constexpr int N = 1 << L2;
+    size_t lds = (size_t)N * sizeof(double2) * (N <= 1024 ? 3 : 1);
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(kBlock);
+    if (a.dtype == 0) hipLaunchKernelGGL((k_xspec<L2, 0>), g, b, lds, st, a);
+    else hipLaunchKernelGGL((k_xspec<L2, 1>), g, b, lds, st, a);
+}
 
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(kBlock);
-    switch (kmax_for(a.nbin / 2)) {
-        case 1: hipLaunchKernelGGL(k_xspec<1>, g, b, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_xspec<2>, g, b, lds, st, a); break;
-        case 3: hipLaunchKernelGGL(k_xspec<3>, g, b, lds, st, a); break;
-        case 5: hipLaunchKernelGGL(k_xspec<5>, g, b, lds, st, a); break;
-        case 9: hipLaunchKernelGGL(k_xspec<9>, g, b, lds, st, a); break;
-        case 17: hipLaunchKernelGGL(k_xspec<17>, g, b, lds, st, a); break;
+    switch (a.log2N) {
+        case 4: launch_xspec_t<4>(a, st); break;
+        case 5: launch_xspec_t<5>(a, st); break;
+        case 6: launch_xspec_t<6>(a, st); break;
+        case 7: launch_xspec_t<7>(a, st); break;
+        case 8: launch_xspec_t<8>(a, st); break;
+        case 9: launch_xspec_t<9>(a, st); break;
+        case 10: launch_xspec_t<10>(a, st); break;
+        case 11: launch_xspec_t<11>(a, st); break;
+        case 12: launch_xspec_t<12>(a, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

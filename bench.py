@@ -163,14 +163,15 @@ def main():
     mean_passes = float(nfev[first:first + count].mean()) if world > 1 else \
         float(nfev.mean())
     kern = {
-        "xspec": dict(ms=stage_ms[1],
+        "xspec": dict(ms=stage_ms[1], unit=xspec_bytes,
                       bytes=steps_subints * xspec_bytes +
                       ncalls * nchan * nharm * 16),
-        "solve": dict(ms=stage_ms[3],
+        "solve": dict(ms=stage_ms[3], unit=solve_bytes_per_pass,
                       bytes=steps_subints * mean_passes *
                       solve_bytes_per_pass),
-        "guess": dict(ms=stage_ms[2], bytes=None),
-        "model_rfft": dict(ms=stage_ms[0], bytes=ncalls * model_bytes),
+        "guess": dict(ms=stage_ms[2], unit=None, bytes=None),
+        "model_rfft": dict(ms=stage_ms[0], unit=model_bytes,
+                           bytes=ncalls * model_bytes),
     }
     dom = max(kern, key=lambda k: kern[k]["ms"])
     dk = kern[dom]
@@ -179,12 +180,14 @@ def main():
             "xspec"
         dk = kern[dom]
     achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
+    # HBM traffic per launch from the PMC passes (profiles/pmc_reduce.py):
+    # measured bytes per unit x the units one launch processes
     traffic = None
     if os.path.exists(args.pmc):
         try:
-            pm = json.load(open(args.pmc))
-            if pm.get("kernel") and dom in pm["kernel"]:
-                traffic = pm.get("hbm_bytes_per_launch")
+            pm = json.load(open(args.pmc))["kernels"][dom]
+            traffic = round(pm["hbm_bytes"] * (dk["bytes"] / ncalls) /
+                            dk["unit"])
         except Exception:
             traffic = None
     n_launch = ncalls

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -73,7 +74,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gR, gM, gw, state, partials, active, total;
+    size_t M, X, chan, stats, x0, gR, gM, gw, Msum, state, partials, active, total;
     int nblk, cb;
 };
 
@@ -98,6 +99,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
         L.gR = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
         L.gM = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
         L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblk * 2);
+        L.Msum = o; o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nharm);
     }
     L.total = o;
     return L;
@@ -245,7 +247,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.gR = d->guess ? (double2 *)(ws + L.gR) : nullptr;
     xa.gM = d->guess ? (double2 *)(ws + L.gM) : nullptr;
     xa.gw = d->guess ? (double *)(ws + L.gw) : nullptr;
-    if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
+    const char *xenv = getenv("PPF_XSPEC");
+    const bool wave = ppf::xspec_wave_supported(xa.log2N, xa.cb) && !(xenv && !strcmp(xenv, "block"));
+    if (wave) {
+        if ((e = ppf::launch_xspec_wave(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec_w");
+    } else {
+        if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
+    }
     mark(2);
 
     if (d->guess) {
@@ -254,6 +262,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.Ns = d->guess_Ns; ga.mask = d->chan_mask; ga.freqs = d->freqs; ga.P = d->P;
         ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau; ga.nu_fits = d->nu_fits; ga.gR = xa.gR; ga.gM = xa.gM;
         ga.gw = xa.gw; ga.x0 = (double *)(ws + L.x0);
+        if (wave) {   // mean model spectrum from the all-channel sum (k_model_sum)
+            double2 *msum = (double2 *)(ws + L.Msum);
+            ga.Msum = msum;
+            ga.Mft = Mft; ga.model_index = d->model_index;
+            if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
+                return hip_fail(ctx, e, "k_model_sum");
+        }
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
     }
     mark(3);

@@ -38,6 +38,10 @@ struct GuessArgs {
     const double2 *gR, *gM;
     const double *gw;
     double *x0;                  // [nsub][8]
+    // wave xspec path: mean model = (Msum - masked rows) / count
+    const double2 *Msum;         // [nmodel][N+1] or null (use gM partials)
+    const double2 *Mft;
+    const int32_t *model_index;
 };
 
 struct TRState;
@@ -104,6 +108,10 @@ hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st);
+bool xspec_wave_supported(int log2N, int cb);
+hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);
+hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out,
+                            hipStream_t st);
 hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st);
 hipError_t launch_pass(const SolveArgs &a, hipStream_t st);
 hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st);

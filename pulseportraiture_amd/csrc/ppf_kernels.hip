@@ -339,7 +339,16 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
         for (int b = 0; b < a.nblk; ++b) {
             int64_t o = ((int64_t)s * a.nblk + b) * nharm + k;
             R = cadd(R, a.gR[o]);
-            M = cadd(M, a.gM[o]);
+            if (!a.Msum) M = cadd(M, a.gM[o]);
+        }
+        if (a.Msum) {
+            const int mi = a.model_index ? a.model_index[s] : 0;
+            const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
+            const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+            M = a.Msum[(int64_t)mi * nharm + k];
+            if (mask)
+                for (int n = 0; n < a.nchan; ++n)
+                    if (!mask[n]) M = csub(M, Mm[(int64_t)n * nharm + k]);
         }
         R = cscale(R, 1.0 / wsum);
         M = cscale(M, 1.0 / cnt);

@@ -1,0 +1,232 @@
+// ppf_wfft.hpp -- wave-private register/LDS FFT for gfx950 (wave64).
+//
+// One wave transforms one row of N = 2^LOG2N complex points (128 <= N <= 1024)
+// with no workgroup barrier: each lane holds R = N/64 points in registers,
+// every Stockham stage is a radix-R (last stage: the remaining radix) DFT
+// done entirely in registers, and the data is exchanged between stages
+// through the wave's own LDS buffer.  The buffer is padded by one slot per
+// 2^S (pad(idx) = idx + (idx >> S), S = max(3, log2 R)) so the stride-R
+// stores of the first stage and the strided reads of the later stages are
+// bank-conflict free for ds_*_b128, and every access is a lane-dependent base
+// plus a compile-time offset (folded into the ds_* immediate: no per-element
+// address registers held across the row loop).
+// Stage twiddles: one read of w = T[k N/(radix L)] (global table, L1/L2
+// resident) per butterfly, the other powers by recurrence.
+//
+// Plan for N = 1024: radix 16 (L=1) -> radix 16 (L=16) -> radix 4 (L=256).
+#pragma once
+#include "ppf_device.hpp"
+
+namespace ppf {
+namespace wfft {
+
+// exp(-2 pi i j / 16), j < 16 (exact decimal expansions)
+__device__ constexpr double kC16[16] = {
+    1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173,
+    0.0, -0.38268343236508977173, -0.70710678118654752440, -0.92387953251128675613,
+    -1.0, -0.92387953251128675613, -0.70710678118654752440, -0.38268343236508977173,
+    0.0, 0.38268343236508977173, 0.70710678118654752440, 0.92387953251128675613};
+__device__ constexpr double kS16[16] = {
+    0.0, -0.38268343236508977173, -0.70710678118654752440, -0.92387953251128675613,
+    -1.0, -0.92387953251128675613, -0.70710678118654752440, -0.38268343236508977173,
+    0.0, 0.38268343236508977173, 0.70710678118654752440, 0.92387953251128675613,
+    1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173};
+
+// multiply by exp(-2 pi i e / 16) (compile-time e), special-casing the
+// trivial and 45-degree factors
+template <int E>
+__device__ __forceinline__ double2 mul_w16(double2 a) {
+    constexpr int e = E & 15;
+    if constexpr (e == 0) return a;
+    else if constexpr (e == 4) return cmk(a.y, -a.x);            // -i
+    else if constexpr (e == 8) return cmk(-a.x, -a.y);           // -1
+    else if constexpr (e == 12) return cmk(-a.y, a.x);           // +i
+    else if constexpr (e == 2) {
+        constexpr double h = 0.70710678118654752440;
+        return cmk((a.x + a.y) * h, (a.y - a.x) * h);
+    } else if constexpr (e == 6) {
+        constexpr double h = 0.70710678118654752440;
+        return cmk((a.y - a.x) * h, -(a.x + a.y) * h);
+    } else if constexpr (e == 10) {
+        constexpr double h = 0.70710678118654752440;
+        return cmk(-(a.x + a.y) * h, (a.x - a.y) * h);
+    } else if constexpr (e == 14) {
+        constexpr double h = 0.70710678118654752440;
+        return cmk((a.x - a.y) * h, (a.x + a.y) * h);
+    } else {
+        return cmul(a, cmk(kC16[e], kS16[e]));
+    }
+}
+
+template <int R>
+__device__ constexpr int log2c() { return R <= 1 ? 0 : 1 + log2c<R / 2>(); }
+
+template <int I, int BITS>
+__device__ constexpr int bitrev() {
+    int r = 0;
+    for (int b = 0; b < BITS; ++b) r |= ((I >> b) & 1) << (BITS - 1 - b);
+    return r;
+}
+
+// in-register forward DFT of R = 2, 4, 8 or 16 points, natural order in/out
+template <int R, int LEN, int I, int J>
+__device__ __forceinline__ void dft_bfly(double2 (&y)[R]) {
+    if constexpr (J < LEN / 2) {
+        constexpr int a = I + J, b = I + J + LEN / 2;
+        const double2 v = mul_w16<J * (16 / LEN)>(y[b]);
+        const double2 u = y[a];
+        y[a] = cadd(u, v);
+        y[b] = csub(u, v);
+        dft_bfly<R, LEN, I, J + 1>(y);
+    }
+}
+template <int R, int LEN, int I>
+__device__ __forceinline__ void dft_group(double2 (&y)[R]) {
+    if constexpr (I < R) {
+        dft_bfly<R, LEN, I, 0>(y);
+        dft_group<R, LEN, I + LEN>(y);
+    }
+}
+template <int R, int LEN>
+__device__ __forceinline__ void dft_levels(double2 (&y)[R]) {
+    if constexpr (LEN <= R) {
+        dft_group<R, LEN, 0>(y);
+        dft_levels<R, LEN * 2>(y);
+    }
+}
+template <int R, int I>
+__device__ __forceinline__ void dft_perm(const double2 *x, double2 (&y)[R]) {
+    if constexpr (I < R) {
+        y[I] = x[bitrev<I, log2c<R>()>()];
+        dft_perm<R, I + 1>(x, y);
+    }
+}
+template <int R>
+__device__ __forceinline__ void dft(double2 *x) {   // x[0..R) in place
+    double2 y[R];
+    dft_perm<R, 0>(x, y);
+    dft_levels<R, 2>(y);
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = y[i];
+}
+
+// compile-time plan: lane-local radix R = N/64 while it fits, then the rest
+template <int LOG2N>
+struct Plan {
+    static constexpr int N = 1 << LOG2N;
+    static constexpr int R = N / 64;                  // points per lane
+    static constexpr int LR = LOG2N - 6;
+    static constexpr int NFULL = LOG2N / LR;          // full radix-R stages
+    static constexpr int LAST = 1 << (LOG2N - NFULL * LR);   // 1: none
+    static constexpr int NST = NFULL + (LAST > 1 ? 1 : 0);
+    static constexpr int S = LR > 3 ? LR : 3;          // swizzle shift
+    static constexpr int radix(int s) { return s < NFULL ? R : LAST; }
+    static constexpr int L(int s) { return s == 0 ? 1 : L(s - 1) * radix(s - 1); }
+    static constexpr int L2 = NST > 1 ? R : N;         // L of stage 1
+    // twiddle-table offset of stage s >= 1: L(s) - L(1)
+    static constexpr int toff(int s) { return L(s) - L2; }
+};
+
+template <int LOG2N>
+__device__ __forceinline__ constexpr int pad(int idx) {
+    return idx + (idx >> Plan<LOG2N>::S);
+}
+// LDS slots of one wave buffer
+template <int LOG2N>
+__host__ __device__ constexpr int buf_slots() { return Plan<LOG2N>::N + (Plan<LOG2N>::N >> Plan<LOG2N>::S); }
+
+// slot of element lane + C (C a compile-time multiple of 64): base + const
+template <int LOG2N, int C>
+__device__ __forceinline__ int slot_lane(int lane_base /* pad(lane) */) {
+    return lane_base + C + (C >> Plan<LOG2N>::S);
+}
+
+// wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
+// operations are processed in issue order; this keeps the compiler from
+// moving them across the exchange point)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One Stockham stage ST >= 1: read from buf, twiddle, DFT, write to buf.
+// Reads j + q NB (j = lane + 64 b): pad(lane) + const.  Writes o + q L with
+// o = (j - k) rad + k: pad(o) + const when 2^S divides L, else computed.
+template <int LOG2N, int ST, int B>
+__device__ __forceinline__ void stage_read(double2 *buf, int lb, double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int rad = P::radix(ST), NB = P::N / rad, BPL = NB / 64;
+    if constexpr (B < BPL) {
+#pragma unroll
+        for (int q = 0; q < rad; ++q) v[B][q] = buf[lb + (64 * B + q * NB) + ((64 * B + q * NB) >> P::S)];
+        stage_read<LOG2N, ST, B + 1>(buf, lb, v);
+    }
+}
+template <int LOG2N, int ST>
+__device__ __forceinline__ void stage(double2 *buf, const double2 *__restrict__ T, int lane) {
+    using P = Plan<LOG2N>;
+    constexpr int N = P::N, rad = P::radix(ST), L = P::L(ST);
+    constexpr int NB = N / rad, BPL = NB / 64, S = P::S, TS = N / (rad * L);
+    const int lb = pad<LOG2N>(lane);
+    double2 v[BPL][rad];
+    stage_read<LOG2N, ST, 0>(buf, lb, v);
+#pragma unroll
+    for (int b = 0; b < BPL; ++b) {
+        const int j = lane + 64 * b, k = j & (L - 1);
+        // twiddles w^q, w = exp(-2 pi i k / (rad L)) = T[k N / (rad L)], by
+        // recurrence from one table read (no rad-1 twiddles live at once)
+        const double2 w1 = T[k * TS];
+        double2 wq = w1;
+        v[b][1] = cmul(v[b][1], w1);
+#pragma unroll
+        for (int q = 2; q < rad; ++q) {
+            wq = cmul(wq, w1);
+            v[b][q] = cmul(v[b][q], wq);
+        }
+        dft<rad>(v[b]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < BPL; ++b) {
+        const int j = lane + 64 * b, k = j & (L - 1);
+        const int o = (j - k) * rad + k;
+        if constexpr ((L >> S) << S == L) {
+            const int ob = pad<LOG2N>(o);
+#pragma unroll
+            for (int q = 0; q < rad; ++q) buf[ob + q * L + ((q * L) >> S)] = v[b][q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < rad; ++q) buf[pad<LOG2N>(o + q * L)] = v[b][q];
+        }
+    }
+    wave_sync();
+}
+template <int LOG2N, int ST>
+__device__ __forceinline__ void stages_from(double2 *buf, const double2 *__restrict__ T, int lane) {
+    if constexpr (ST < Plan<LOG2N>::NST) {
+        stage<LOG2N, ST>(buf, T, lane);
+        stages_from<LOG2N, ST + 1>(buf, T, lane);
+    }
+}
+
+// Full forward FFT of the row whose stage-0 inputs x[q] = z[lane + 64 q]
+// (q < R) are in registers; result in natural order in buf (padded).
+template <int LOG2N>
+__device__ __forceinline__ void fft_row(double2 (&x)[Plan<LOG2N>::R], double2 *buf,
+                                        const double2 *__restrict__ T, int lane) {
+    using P = Plan<LOG2N>;
+    constexpr int R = P::R;
+    dft<R>(x);
+    wave_sync();
+    // stage 0 output: o = lane R + q (L = 1, k = 0); pad(lane R + q) =
+    // pad(lane R) + q since q < R <= 2^S and 2^S is a multiple of R
+    const int ob = pad<LOG2N>(lane * R);
+#pragma unroll
+    for (int q = 0; q < R; ++q) buf[ob + q] = x[q];
+    wave_sync();
+    stages_from<LOG2N, 1>(buf, T, lane);
+}
+
+}  // namespace wfft
+}  // namespace ppf

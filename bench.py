@@ -154,14 +154,16 @@ def main():
     res_np = last.cpu().numpy()
     I = _lib.RESULT_INDEX
     nfev = res_np[:, I["nfeval"]]
+    npass = res_np[:, I["npass"]]
     status = res_np[:, I["status"]].astype(int)
     # algorithmic bytes per sub-integration
     xspec_bytes = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
     model_bytes = nchan * nbin * 8 + nchan * nharm * 16
-    solve_bytes_per_pass = nchan * nharm * 16 + nchan * 10 * 8
+    solve_bytes_per_pass = nchan * nharm * 16 + nchan * 32 * 16   # X + moments
     steps_subints = count * args.steps
-    mean_passes = float(nfev[first:first + count].mean()) if world > 1 else \
-        float(nfev.mean())
+    mine = slice(first, first + count) if world > 1 else slice(None)
+    mean_passes = float(npass[mine].mean())
+    mean_nfev = float(nfev[mine].mean())
     kern = {
         "xspec": dict(ms=stage_ms[1], unit=xspec_bytes,
                       bytes=steps_subints * xspec_bytes +
@@ -214,6 +216,7 @@ def main():
                            fit="phase+DM", parallelism="dp%d" % world),
                roofline=roof, stages=stages,
                mean_passes_per_fit=round(mean_passes, 3),
+               mean_evals_per_fit=round(mean_nfev, 3),
                fits_converged_frac=round(float(np.mean(
                    (status & 0xff) == 2)), 5))
     # sanity: fitted DM / phase agree with the injected truths

@@ -70,14 +70,15 @@ typedef struct ppf_result {
     double fun;            /* objective at the fit (chi2 - Sd)              */
     double Sd;             /* data power term                               */
     double phi_guess;      /* initial phase actually used                   */
-    double nfeval;         /* objective evaluations (passes over the data)  */
+    double nfeval;         /* objective evaluations (scipy nfev)            */
     double status;         /* ppf_status bits                               */
     double niter;          /* trust-region iterations                       */
     double dof;
     double nchanx;         /* channels used                                 */
     double x_fit_phi;      /* phi at nu_fit (before output transform)      */
     double x_fit_tau;      /* tau parameter at nu_fit                       */
-    double reserved[3];
+    double npass;          /* streaming passes over the cross spectrum      */
+    double reserved[2];
 } ppf_result;
 
 /* Batched wideband fit: replaces pptoaslib.fit_portrait_full

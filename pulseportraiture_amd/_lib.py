@@ -25,7 +25,8 @@ RESULT_FIELDS = (
     [("params", 5), ("param_errs", 5), ("nu_out", 3), ("nu_fit", 3)] +
     [(n, 1) for n in ("chi2", "red_chi2", "snr", "fun", "Sd", "phi_guess",
                       "nfeval", "status", "niter", "dof", "nchanx",
-                      "x_fit_phi", "x_fit_tau")] + [("reserved", 3)])
+                      "x_fit_phi", "x_fit_tau", "npass")] +
+    [("reserved", 2)])
 RESULT_DOUBLES = sum(n for _, n in RESULT_FIELDS)
 assert RESULT_DOUBLES == 32
 

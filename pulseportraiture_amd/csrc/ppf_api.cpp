@@ -74,7 +74,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gR, gM, gw, Msum, state, partials, active, total;
+    size_t M, X, chan, stats, x0, gR, gM, gw, Msum, state, partials, active, mom, dphi, total;
     int nblk, cb;
 };
 
@@ -95,6 +95,8 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.state = o; o += align256(ppf::tr_state_bytes() * nsub);
     L.partials = o; o += align256(sizeof(double) * nsub * (size_t)ppf::pass_blocks(d->nchan) * 21);
     L.active = o; o += 256;
+    L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
+    L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
     if (d->guess) {
         L.gR = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
         L.gM = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
@@ -291,18 +293,30 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         e = hipHostMalloc((void **)&ctx->host_active, sizeof(unsigned));
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
     }
+    const char *senv = getenv("PPF_SOLVER");
+    sa.moments = (senv && !strcmp(senv, "pass")) ? 0 : 1;
+    sa.mom = (double2 *)(ws + L.mom);
+    sa.dphi = (double *)(ws + L.dphi);
+    if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
-    // trust-region iterations: each = one streaming pass + one step.  Groups
-    // of iterations are queued without host synchronisation; the count of
-    // still-iterating sub-ints is read back between groups.
+    // trust-region iterations.  Scattering fits: each iteration = one
+    // streaming pass (k_pass) + one step (k_tr_step).  Other fits: k_moments
+    // (re)centres the moment sets of the sub-ints that asked, k_tr_mom runs
+    // iterations until the fit stops or leaves the expansion radius.  Groups
+    // of rounds are queued without host synchronisation; the count of
+    // sub-ints still needing work is read back between groups.
     const int maxiter = d->max_iter > 0 ? d->max_iter : 200 * 5;
     int iter = 0;
-    for (int group = 6;; group = 4) {
+    for (int group = sa.moments ? 3 : 6;; group = sa.moments ? 2 : 4) {
         for (int g = 0; g < group; ++g) {
             if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
+            if (sa.moments && (e = ppf::launch_moments(sa, st)) != hipSuccess)
+                return hip_fail(ctx, e, "k_moments");
             if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");
             if ((e = ppf::launch_tr_step(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_step");
+            if (sa.moments && (e = ppf::launch_tr_mom(sa, st)) != hipSuccess)
+                return hip_fail(ctx, e, "k_tr_mom");
         }
         iter += group;
         if ((e = hipMemcpyAsync(ctx->host_active, sa.active, sizeof(unsigned), hipMemcpyDeviceToHost,

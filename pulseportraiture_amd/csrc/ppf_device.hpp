@@ -56,6 +56,21 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
+// operations are processed in issue order; this keeps the compiler from
+// moving them across the exchange point)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Sum K values per thread over the whole block; result valid in every thread.
 // scratch must hold kWaves*K doubles.  Contains two __syncthreads().
 template <int K>

@@ -65,6 +65,10 @@ struct SolveArgs {
     TRState *state;              // [nsub]
     double *partials;            // [nsub][pass_blocks(nchan)][21]
     unsigned *active;            // sub-ints still iterating (k_tr_step)
+    // moment-expansion solver for fits without scattering (ppf_moments)
+    int moments;                 // 1: enabled
+    double2 *mom;                // [nsub][2][nchan][kMoments]
+    double *dphi;                // [nsub][nchan][2]: d phi_n / d(DM, GM)
 };
 
 struct RotateArgs {
@@ -115,6 +119,9 @@ hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel
 hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st);
 hipError_t launch_pass(const SolveArgs &a, hipStream_t st);
 hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st);
+hipError_t launch_moments(const SolveArgs &a, hipStream_t st);
+hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st);
+constexpr int kMoments = 32;     // Taylor moments per channel
 hipError_t launch_postfit(const SolveArgs &a, hipStream_t st);
 size_t tr_state_bytes();
 int pass_blocks(int nchan);

@@ -129,6 +129,10 @@ struct TRState {
     int slot_cur, slot_eval, flagmask, nchanx;
     int scat, hb, g_sum, g_tau;
     int g_alpha, pad0, pad1, pad2;
+    // moment mode (no scattering): two moment sets centred at mc[q]
+    int mmode, need_mom, mtarget, macc;
+    int mvalid[2], meval, nmom;
+    double mc[2][3];
 };
 
 __device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j
@@ -214,6 +218,37 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
             S.phase = PH_INIT;
         }
     }
+    // moment mode: phase-only channel model (no scattering), the objective
+    // and its derivatives from per-channel Taylor moments (ppf_moments)
+    const int mmode = (a.moments && !scat && nf > 0 && cnt > 0.0) ? 1 : 0;
+    if (lane == 0) {
+        S.mmode = mmode;
+        S.need_mom = mmode;
+        S.mtarget = 0;
+        S.macc = 0;
+        S.meval = 0;
+        S.nmom = 0;
+        S.mvalid[0] = mmode;
+        S.mvalid[1] = 0;
+        for (int i = 0; i < 3; ++i) { S.mc[0][i] = x[i]; S.mc[1][i] = x[i]; }
+    }
+    if (mmode) {
+        const double P = a.P[s];
+        const double nuDM2 = pow(nu_fit[0], -2.0), nuGM4 = pow(nu_fit[1], -4.0);
+        double *dp = a.dphi + (int64_t)s * a.nchan * 2;
+        double *st = a.stats + (int64_t)s * 2 * a.nchan * 10;
+        for (int n = lane; n < a.nchan; n += 64) {
+            const double nu = fr[n];
+            dp[2 * n + 0] = kDconst * (pow(nu, -2.0) - nuDM2) / P;
+            dp[2 * n + 1] = kDconst * kDconst * (pow(nu, -4.0) - nuGM4) / P;
+            const bool use = !mask || mask[n];
+            for (int q = 0; q < 2; ++q) {
+                double *d = st + ((int64_t)q * a.nchan + n) * 10;
+                for (int j = 0; j < 10; ++j) d[j] = 0.0;
+                d[6] = use ? chan[n * 4 + 3] : 0.0;
+            }
+        }
+    }
 }
 
 // ===========================================================================
@@ -229,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
     const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
     const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const TRState &S = a.state[s];
-    if (S.phase == PH_DONE || S.scat != (SCAT ? 1 : 0)) return;
+    if (S.phase == PH_DONE || S.scat != (SCAT ? 1 : 0) || S.mmode) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nharm = (a.nbin >> 1) + 1;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
@@ -383,6 +418,77 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
 }
 
 // ===========================================================================
+// one iteration of scipy _minimize_trust_region (scipy/optimize/_trustregion.py)
+// with CGSteihaugSubproblem (_trustregion_ncg.py): consume the evaluation o
+// (f, g[5], H[15]) of S.th, accept/reject, then propose the next point.
+// gtol = -1 (pptoaslib.py:1047-1048), eta 0.15, initial radius 1, max radius
+// 1000, maxiter 200 * len(x0).  Returns 1 when a new proposal is pending.
+// ===========================================================================
+__device__ int tr_update(TRState &S, const double *o, int max_iter) {
+    const int phase = S.phase;
+    const int flagmask = S.flagmask;
+    int idx[5], nf = 0;
+    for (int i = 0; i < 5; ++i)
+        if (flagmask >> i & 1) idx[nf++] = i;
+    const int maxiter = max_iter > 0 ? max_iter : 200 * 5;
+    TRModel m;
+    bool done = false;
+    int cmd = 0;
+    if (phase == PH_INIT) {
+        S.nfev = 1;
+        S.f = o[0];
+        for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+        for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+        if (!(o[0] == o[0])) { S.status = PPF_ST_NONFINITE; done = true; }
+        S.macc = S.meval;
+    } else {
+        S.nfev += 1;
+        const double fp = o[0];
+        const double actual = S.f - fp, pred = S.f - S.pred;
+        const double rho = actual / pred;
+        if (rho < 0.25) S.radius *= 0.25;
+        else if (rho > 0.75 && S.hb) S.radius = fmin(2.0 * S.radius, 1000.0);
+        if (rho > 0.15) {
+            for (int i = 0; i < 5; ++i) S.x[i] = S.th[i];
+            S.f = fp;
+            for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+            for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+            S.slot_cur = S.slot_eval;
+            S.macc = S.meval;
+        }
+        S.k += 1;
+        if (!(fp == fp)) { S.status = PPF_ST_NONFINITE; done = true; }
+        if (S.k >= maxiter) { S.status = PPF_ST_MAXITER; done = true; }
+    }
+    if (!done) {
+        m.f = S.f;
+        for (int q = 0; q < nf; ++q) {
+            m.g[q] = S.g[idx[q]];
+            for (int r = 0; r < nf; ++r) {
+                int i = min(idx[q], idx[r]), j = max(idx[q], idx[r]);
+                m.H[q][r] = S.H[uidx(i, j)];
+            }
+        }
+        double p[5];
+        const double jm = sqrt(dotn(m.g, m.g, nf));
+        const bool hb = cg_steihaug(m, jm, S.radius, p, nf);
+        const double pv = model_value(m, p, nf);
+        if (m.f - pv <= 0.0) {
+            done = true;                 // warnflag 2: no predicted improvement
+        } else {
+            for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
+            for (int q = 0; q < nf; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
+            S.pred = pv;
+            S.hb = hb ? 1 : 0;
+            S.slot_eval = S.slot_cur ^ 1;
+            cmd = 1;
+        }
+    }
+    S.phase = done ? PH_DONE : PH_PROPOSAL;
+    return cmd;
+}
+
+// ===========================================================================
 // k_tr_step: one wave per sub-integration; scipy _minimize_trust_region
 // (scipy/optimize/_trustregion.py) with CGSteihaugSubproblem
 // (_trustregion_ncg.py), gtol = -1 (pptoaslib.py:1047-1048), eta 0.15,
@@ -395,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     if (s >= a.nsub) return;
     TRState &S = a.state[s];
     const int phase = S.phase;
-    if (phase == PH_DONE) return;
+    if (phase == PH_DONE || S.mmode) return;
     const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
     double o[21];
 #pragma unroll
@@ -409,63 +515,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     for (int i = 0; i < 21; ++i) o[i] = wave_sum(o[i]);
     int cmd = 0;
     if (lane == 0) {
-        const int flagmask = S.flagmask;
-        int idx[5], nf = 0;
-        for (int i = 0; i < 5; ++i)
-            if (flagmask >> i & 1) idx[nf++] = i;
-        const int maxiter = a.max_iter > 0 ? a.max_iter : 200 * 5;
-        TRModel m;
-        bool done = false;
-        if (phase == PH_INIT) {
-            S.nfev = 1;
-            S.f = o[0];
-            for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
-            for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
-            if (!(o[0] == o[0])) { S.status = PPF_ST_NONFINITE; done = true; }
-        } else {
-            S.nfev += 1;
-            const double fp = o[0];
-            const double actual = S.f - fp, pred = S.f - S.pred;
-            const double rho = actual / pred;
-            if (rho < 0.25) S.radius *= 0.25;
-            else if (rho > 0.75 && S.hb) S.radius = fmin(2.0 * S.radius, 1000.0);
-            if (rho > 0.15) {
-                for (int i = 0; i < 5; ++i) S.x[i] = S.th[i];
-                S.f = fp;
-                for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
-                for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
-                S.slot_cur = S.slot_eval;
-            }
-            S.k += 1;
-            if (!(fp == fp)) { S.status = PPF_ST_NONFINITE; done = true; }
-            if (S.k >= maxiter) { S.status = PPF_ST_MAXITER; done = true; }
-        }
-        if (!done) {
-            m.f = S.f;
-            for (int q = 0; q < nf; ++q) {
-                m.g[q] = S.g[idx[q]];
-                for (int r = 0; r < nf; ++r) {
-                    int i = min(idx[q], idx[r]), j = max(idx[q], idx[r]);
-                    m.H[q][r] = S.H[uidx(i, j)];
-                }
-            }
-            double p[5];
-            const double jm = sqrt(dotn(m.g, m.g, nf));
-            const bool hb = cg_steihaug(m, jm, S.radius, p, nf);
-            const double pv = model_value(m, p, nf);
-            if (m.f - pv <= 0.0) {
-                done = true;                 // warnflag 2: no predicted improvement
-            } else {
-                for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
-                for (int q = 0; q < nf; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
-                S.pred = pv;
-                S.hb = hb ? 1 : 0;
-                S.slot_eval = S.slot_cur ^ 1;
-                cmd = 1;
-            }
-        }
-        if (done) S.phase = PH_DONE;
-        else S.phase = PH_PROPOSAL;
+        cmd = tr_update(S, o, a.max_iter);
         for (int i = 0; i < 5; ++i) thb[wave][i] = S.th[i];
         thb[wave][5] = (double)cmd;
     }
@@ -483,6 +533,225 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
                    a.nchan, tl, t4, S.nu_fit[2], a.log10_tau, gs, gt, ga);
         if (lane == 0) { S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga; }
     }
+}
+
+// ===========================================================================
+// Moment-expansion evaluation (fits without scattering).
+//
+// With tau = 0 every channel enters only through its phase phi_n(theta) =
+// phi + DM dphi1_n + GM dphi2_n, and C_n(phi_n) = Re sum_k X_nk e^{2 pi i k
+// phi_n}.  Around a centre phi_c (Y_k = X_k e^{2 pi i k phi_c}), with h = N/2,
+// u_k = (k - h)/h in [-1, 1] and x = 2 pi h Delta:
+//   sum_k Y_k e^{2 pi i k Delta} = e^{i x} sum_m (i x)^m / m! mu_m,
+//   mu_m = sum_k Y_k u_k^m,  and k = h (1 + u) gives the k- and k^2-weighted
+// sums (C', C'') from mu_m + mu_{m+1} and mu_m + 2 mu_{m+1} + mu_{m+2}.
+// kMoments = 32 moments and |x| <= 2.5 bound the truncation of the
+// second-derivative series by 2.5^30 / 30! < 4e-21 of sum_k |Y_k|, so every
+// trust-region evaluation inside that radius costs O(nchan) instead of a pass
+// over the cross spectrum; a point outside it re-centres (k_moments).
+// ===========================================================================
+constexpr double kXMax = 2.5;
+constexpr int kMomChans = 64;                    // channels per k_moments workgroup
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// k_moments: mu[s][q][n][m] for the sub-ints that asked for a (re)centre.
+// MFMA f64 16x16x4: A = Y (16 channels x 4 harmonics; one wave = 16
+// channels), B = u^m (4 harmonics x 16 moments), two B tiles (m < 16, m >=
+// 16) and separate real / imaginary A.  The harmonic sum is the MFMA K loop.
+__global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
+    const int nblk = (a.nchan + kMomChans - 1) / kMomChans;
+    const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    const TRState &S = a.state[s];
+    if (!S.mmode || !S.need_mom) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = S.mtarget;
+    const double c0 = S.mc[q][0], c1 = S.mc[q][1], c2 = S.mc[q][2];
+    const int nharm = (a.nbin >> 1) + 1;
+    const double h = 0.5 * (double)(nharm - 1), ih = 1.0 / h;
+    const int ci = lane & 15, kk = lane >> 4;
+    const int nbase = blk * kMomChans + wave * 16;
+    const int n = nbase + ci;
+    const bool valid = n < a.nchan && (!a.mask || a.mask[(int64_t)s * a.nchan + n]);
+    double phin = 0.0;
+    if (valid) {
+        const double *dp = a.dphi + ((int64_t)s * a.nchan + n) * 2;
+        phin = c0 + c1 * dp[0] + c2 * dp[1];
+    }
+    const double2 *Xr = a.X + ((int64_t)s * a.nchan + (valid ? n : 0)) * nharm;
+    const double2 W4 = cexp2pi(4.0 * phin);
+    f64x4 dre0 = {0.0, 0.0, 0.0, 0.0}, dre1 = dre0, dim0 = dre0, dim1 = dre0;
+    double2 E = cmk(1.0, 0.0);
+    // 8 K-steps (32 harmonics) per iteration: all 8 loads in flight first
+    constexpr int KU = 8;
+    for (int kb = 0; kb < nharm; kb += 4 * KU) {
+        double2 xv[KU];
+#pragma unroll
+        for (int t = 0; t < KU; ++t) {
+            const int k = kb + 4 * t + kk;
+            xv[t] = (valid && k < nharm) ? Xr[k] : cmk(0.0, 0.0);
+        }
+#pragma unroll
+        for (int t = 0; t < KU; ++t) {
+            const int k = kb + 4 * t + kk;
+            // phasor by recurrence, re-seeded exactly every 64 harmonics
+            E = (((4 * t) & 63) == 0 && (kb & 63) == 0) ? cexp2pi((double)k * phin) : cmul(E, W4);
+            const double2 y = cmul(xv[t], E);
+            const double u = ((double)k - h) * ih;
+            const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4, u16 = u8 * u8;
+            const double uj = ((ci & 1) ? u : 1.0) * ((ci & 2) ? u2 : 1.0) *
+                              ((ci & 4) ? u4 : 1.0) * ((ci & 8) ? u8 : 1.0);
+            const double ujh = uj * u16;
+            dre0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, uj, dre0, 0, 0, 0);
+            dim0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, uj, dim0, 0, 0, 0);
+            dre1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, ujh, dre1, 0, 0, 0);
+            dim1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, ujh, dim1, 0, 0, 0);
+        }
+    }
+    // D[row][col]: col = lane & 15 = moment, row = (lane >> 4) + 4 r = channel
+    double2 *M = a.mom + ((int64_t)s * 2 + q) * a.nchan * kMoments;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ch = nbase + kk + 4 * r;
+        if (ch < a.nchan) {
+            M[(int64_t)ch * kMoments + ci] = cmk(dre0[r], dim0[r]);
+            M[(int64_t)ch * kMoments + 16 + ci] = cmk(dre1[r], dim1[r]);
+        }
+    }
+}
+
+// rotate by i^P (compile time) and scale: r * i^P * z
+template <int P>
+__device__ __forceinline__ double2 rot_scale(double2 z, double r) {
+    if constexpr ((P & 3) == 0) return cmk(r * z.x, r * z.y);
+    else if constexpr ((P & 3) == 1) return cmk(-r * z.y, r * z.x);
+    else if constexpr ((P & 3) == 2) return cmk(-r * z.x, -r * z.y);
+    else return cmk(r * z.y, -r * z.x);
+}
+// G_j += i^(m-j) x^(m-j)/(m-j)! mu_m for j = 0, 1, 2; r0, r1, r2 hold
+// x^m/m!, x^(m-1)/(m-1)!, x^(m-2)/(m-2)! (sliding window, no array)
+template <int M>
+__device__ __forceinline__ void taylor_acc(const double2 *mu, double x, double r0, double r1,
+                                           double r2, double2 &G0, double2 &G1, double2 &G2) {
+    if constexpr (M < kMoments) {
+        const double2 v = mu[M];
+        G0 = cadd(G0, rot_scale<M>(v, r0));
+        if constexpr (M >= 1) G1 = cadd(G1, rot_scale<M - 1>(v, r1));
+        if constexpr (M >= 2) G2 = cadd(G2, rot_scale<M - 2>(v, r2));
+        taylor_acc<M + 1>(mu, x, r0 * x * (1.0 / (double)(M + 1)), r0, r1, G0, G1, G2);
+    }
+}
+
+// k_tr_mom: one wave per moment-mode sub-integration; runs trust-region
+// iterations back to back, every evaluation from the moments, until the fit
+// stops or a point leaves the expansion radius of both moment sets (then it
+// asks k_moments for a new centre and exits).
+__global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
+    __shared__ TRState sts[kWaves];
+    __shared__ int cmdb[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int s = blockIdx.x * kWaves + wave;
+    if (s >= a.nsub) return;
+    TRState &G = a.state[s];
+    if (!G.mmode || G.phase == PH_DONE) return;
+    TRState &L = sts[wave];
+    static_assert(sizeof(TRState) % 8 == 0, "TRState copy");
+    constexpr int NW = (int)(sizeof(TRState) / 8);
+    for (int i = lane; i < NW; i += 64)
+        reinterpret_cast<double *>(&L)[i] = reinterpret_cast<const double *>(&G)[i];
+    wave_lds_sync();
+    const int nharm = (a.nbin >> 1) + 1;
+    const double h = 0.5 * (double)(nharm - 1);
+    const double *dp = a.dphi + (int64_t)s * a.nchan * 2;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *chan = a.chan + (int64_t)s * a.nchan * 4;
+    const double2 *MOM = a.mom + (int64_t)s * 2 * a.nchan * kMoments;
+    double *stats = a.stats + (int64_t)s * 2 * a.nchan * 10;
+    const int flagmask = L.flagmask;
+    if (lane == 0) L.need_mom = 0;
+    const int cap = (a.max_iter > 0 ? a.max_iter : 1000) + 4;
+    for (int it = 0; it < cap; ++it) {
+        wave_lds_sync();
+        const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
+        // moment set whose centre is within the expansion radius for every channel
+        int qsel = -1;
+        for (int t = 0; t < 2 && qsel < 0; ++t) {
+            const int cand = t == 0 ? L.macc : 1 - L.macc;
+            if (!L.mvalid[cand]) continue;
+            const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
+            double xm = 0.0;
+            for (int n = lane; n < a.nchan; n += 64) {
+                if (mask && !mask[n]) continue;
+                xm = fmax(xm, fabs(e0 + e1 * dp[2 * n] + e2 * dp[2 * n + 1]));
+            }
+            xm = wave_max(xm);
+            if (kTwoPi * h * xm <= kXMax) qsel = cand;
+        }
+        if (qsel < 0) {
+            if (lane == 0) {
+                const int tgt = L.mvalid[L.macc] ? 1 - L.macc : L.macc;
+                L.mtarget = tgt;
+                L.mc[tgt][0] = t0; L.mc[tgt][1] = t1; L.mc[tgt][2] = t2;
+                L.mvalid[tgt] = 1;
+                L.need_mom = 1;
+                L.nmom += 1;
+                atomicAdd(a.active, 1u);
+            }
+            break;
+        }
+        const double e0 = t0 - L.mc[qsel][0], e1 = t1 - L.mc[qsel][1], e2 = t2 - L.mc[qsel][2];
+        const double2 *Mq = MOM + (int64_t)qsel * a.nchan * kMoments;
+        double *st = stats + (int64_t)L.slot_eval * a.nchan * 10;
+        double acc[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) acc[i] = 0.0;
+        for (int n = lane; n < a.nchan; n += 64) {
+            if (mask && !mask[n]) continue;
+            const double d1 = dp[2 * n], d2 = dp[2 * n + 1];
+            const double del = e0 + e1 * d1 + e2 * d2;
+            const double x = kTwoPi * h * del;
+            double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
+            taylor_acc<0>(Mq + (int64_t)n * kMoments, x, 1.0, 0.0, 0.0, G0, G1, G2);
+            const double2 eix = cexp2pi(h * del);
+            const double2 F = cmul(eix, G0);
+            const double2 K1 = cscale(cmul(eix, cadd(G0, G1)), h);
+            const double2 K2 = cscale(cmul(eix, cadd(cadd(G0, G2), cscale(G1, 2.0))), h * h);
+            const double C = F.x, Cp = -kTwoPi * K1.y, Cpp = -kTwoPi * kTwoPi * K2.x;
+            double *sn = st + (int64_t)n * 10;
+            sn[0] = C; sn[1] = Cp; sn[2] = Cpp;
+            const double iS = 1.0 / chan[n * 4 + 3];
+            const double dph[3] = {1.0, d1, d2};
+            const double hn = -2.0 * (C * Cpp + Cp * Cp) * iS;
+            // acc: f, g(phi, DM, GM), H upper triangle 00 01 02 11 12 22
+            acc[0] += -C * C * iS;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (flagmask >> i & 1) acc[1 + i] += -2.0 * C * Cp * dph[i] * iS;
+            constexpr int hi[6] = {0, 0, 0, 1, 1, 2}, hj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+            for (int e = 0; e < 6; ++e)
+                if ((flagmask >> hi[e] & 1) && (flagmask >> hj[e] & 1))
+                    acc[4 + e] += hn * dph[hi[e]] * dph[hj[e]];
+        }
+        double o[21];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) o[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = wave_sum(acc[i]);
+        {
+            constexpr int hi[6] = {0, 0, 0, 1, 1, 2}, hj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+            for (int e = 0; e < 6; ++e) o[6 + uidx(hi[e], hj[e])] = wave_sum(acc[4 + e]);
+        }
+        if (lane == 0) {
+            L.meval = qsel;
+            cmdb[wave] = tr_update(L, o, a.max_iter);
+        }
+        wave_lds_sync();
+        if (!cmdb[wave]) break;
+    }
+    wave_lds_sync();
+    for (int i = lane; i < NW; i += 64)
+        reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&L)[i];
 }
 
 // nu_zero-case accumulation slots
@@ -879,7 +1148,10 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
         res->nchanx = (double)nchanx;
         res->x_fit_phi = x[0];
         res->x_fit_tau = x[3];
-        res->reserved[0] = res->reserved[1] = res->reserved[2] = 0.0;
+        // full passes over X: one per evaluation (k_pass) or one per moment
+        // (re)centre (k_moments)
+        res->npass = S.mmode ? (double)S.nmom + 1.0 : (double)nfev;
+        res->reserved[0] = res->reserved[1] = 0.0;
     }
 }
 
@@ -919,6 +1191,18 @@ hipError_t launch_pass(const SolveArgs &a, hipStream_t st) {
 
 hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(k_tr_step, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
+                       st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_moments(const SolveArgs &a, hipStream_t st) {
+    const int nblk = (a.nchan + kMomChans - 1) / kMomChans;
+    hipLaunchKernelGGL(k_moments, dim3((unsigned)((int64_t)a.nsub * nblk)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_tr_mom, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
                        st, a);
     return hipGetLastError();
 }

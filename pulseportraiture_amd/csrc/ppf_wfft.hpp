@@ -141,14 +141,7 @@ __device__ __forceinline__ int slot_lane(int lane_base /* pad(lane) */) {
     return lane_base + C + (C >> Plan<LOG2N>::S);
 }
 
-// wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
-// operations are processed in issue order; this keeps the compiler from
-// moving them across the exchange point)
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
 // One Stockham stage ST >= 1: read from buf, twiddle, DFT, write to buf.
 // Reads j + q NB (j = lane + 64 b): pad(lane) + const.  Writes o + q L with

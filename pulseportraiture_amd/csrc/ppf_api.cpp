@@ -74,8 +74,8 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gR, gM, gw, Msum, state, partials, active, mom, dphi, total;
-    int nblk, cb;
+    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, Mpow, needx, Bt, total;
+    int nblk, cb, cbd, nblkd;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -86,6 +86,8 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
+    L.cbd = d->nchan < 64 ? d->nchan : 64;            // k_dsum channel block
+    L.nblkd = (d->nchan + L.cbd - 1) / L.cbd;
     size_t o = 0;
     L.M = o;     o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
     L.X = o;     o += align256(sizeof(double2) * nsub * nchan * nharm);
@@ -97,10 +99,12 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.active = o; o += 256;
     L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
     L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
+    L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
+    L.needx = o; o += align256(nsub);
+    L.Bt = o;    o += align256(sizeof(double) * (nharm - 1) / 2 * 16);
     if (d->guess) {
-        L.gR = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
-        L.gM = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * nharm);
-        L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblk * 2);
+        L.gP = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * (size_t)d->nbin);
+        L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * 2);
         L.Msum = o; o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nharm);
     }
     L.total = o;
@@ -236,6 +240,17 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ppf::RfftArgs ra{d->nbin, ilog2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_rfft_rows");
+    double *Mpow = (double *)(ws + L.Mpow);
+    if ((e = ppf::launch_model_pow(Mft, d->nchan, nharm, d->nmodel, Mpow, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_model_pow");
+    // moment-mode sub-ints (no scattering) never need the cross spectrum in
+    // HBM: k_xmom re-FFTs their rows; k_classify marks the others
+    const char *senv = getenv("PPF_SOLVER");
+    const int use_moments = (senv && !strcmp(senv, "pass")) ? 0 : 1;
+    uint8_t *needx = (uint8_t *)(ws + L.needx);
+    if ((e = ppf::launch_classify(d->nsub, d->fit_flags, d->init, d->log10_tau, use_moments, needx,
+                                  st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_classify");
     mark(1);
 
     ppf::XspecArgs xa{};
@@ -245,12 +260,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.data = d->data; xa.Mft = Mft; xa.model_index = d->model_index; xa.mask = d->chan_mask;
     xa.errs = d->errs; xa.freqs = d->freqs; xa.P = d->P; xa.T = T; xa.T2 = T2;
     xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);
-    xa.guess = d->guess; xa.guess_weights = d->guess_weights; xa.guess_DM = d->guess_DM;
-    xa.gR = d->guess ? (double2 *)(ws + L.gR) : nullptr;
-    xa.gM = d->guess ? (double2 *)(ws + L.gM) : nullptr;
-    xa.gw = d->guess ? (double *)(ws + L.gw) : nullptr;
+    xa.Mpow = Mpow;
     const char *xenv = getenv("PPF_XSPEC");
     const bool wave = ppf::xspec_wave_supported(xa.log2N, xa.cb) && !(xenv && !strcmp(xenv, "block"));
+    // fused moment pass (k_xmom) only on the wave-FFT shapes; elsewhere the
+    // moments are taken from X (k_moments)
+    const bool fused = wave && use_moments;
+    xa.needx = fused ? needx : nullptr;
     if (wave) {
         if ((e = ppf::launch_xspec_wave(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec_w");
     } else {
@@ -259,18 +275,25 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     mark(2);
 
     if (d->guess) {
+        // guess profile: time-domain dedispersion (k_dsum), then FFTFIT
+        // against the mean model (k_guess)
+        ppf::DsumArgs da{};
+        da.nsub = d->nsub; da.nchan = d->nchan; da.nbin = d->nbin; da.dtype = d->data_dtype;
+        da.cbd = L.cbd; da.nblkd = L.nblkd; da.data = d->data; da.mask = d->chan_mask;
+        da.freqs = d->freqs; da.P = d->P; da.guess_DM = d->guess_DM;
+        da.guess_weights = d->guess_weights;
+        da.gP = (double *)(ws + L.gP); da.gw = (double *)(ws + L.gw);
+        if ((e = ppf::launch_dsum(da, st)) != hipSuccess) return hip_fail(ctx, e, "k_dsum");
+        double2 *msum = (double2 *)(ws + L.Msum);
+        if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
+            return hip_fail(ctx, e, "k_model_sum");
         ppf::GuessArgs ga{};
-        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.kc = kc; ga.nblk = L.nblk;
-        ga.Ns = d->guess_Ns; ga.mask = d->chan_mask; ga.freqs = d->freqs; ga.P = d->P;
-        ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau; ga.nu_fits = d->nu_fits; ga.gR = xa.gR; ga.gM = xa.gM;
-        ga.gw = xa.gw; ga.x0 = (double *)(ws + L.x0);
-        if (wave) {   // mean model spectrum from the all-channel sum (k_model_sum)
-            double2 *msum = (double2 *)(ws + L.Msum);
-            ga.Msum = msum;
-            ga.Mft = Mft; ga.model_index = d->model_index;
-            if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
-                return hip_fail(ctx, e, "k_model_sum");
-        }
+        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = ilog2(d->nbin / 2);
+        ga.kc = kc; ga.nblkd = L.nblkd; ga.Ns = d->guess_Ns; ga.mask = d->chan_mask;
+        ga.freqs = d->freqs; ga.P = d->P; ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau;
+        ga.nu_fits = d->nu_fits; ga.gP = da.gP; ga.gw = da.gw; ga.T = T; ga.T2 = T2;
+        ga.x0 = (double *)(ws + L.x0); ga.Msum = msum; ga.Mft = Mft;
+        ga.model_index = d->model_index;
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
     }
     mark(3);
@@ -293,12 +316,21 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         e = hipHostMalloc((void **)&ctx->host_active, sizeof(unsigned));
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
     }
-    const char *senv = getenv("PPF_SOLVER");
-    sa.moments = (senv && !strcmp(senv, "pass")) ? 0 : 1;
+    sa.moments = use_moments;
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
+    ppf::XmomArgs ma{};
+    ma.nsub = d->nsub; ma.nchan = d->nchan; ma.nbin = d->nbin; ma.log2N = xa.log2N;
+    ma.nblk = L.nblk; ma.cb = L.cb; ma.dtype = d->data_dtype; ma.xcd_swizzle = xa.xcd_swizzle;
+    ma.data = d->data; ma.Mft = Mft; ma.model_index = d->model_index; ma.mask = d->chan_mask;
+    ma.chan = xa.chan; ma.dphi = sa.dphi; ma.T = T; ma.T2 = T2; ma.state = sa.state;
+    ma.mom = (double *)sa.mom;
+    ma.Bt = (const double *)(ws + L.Bt);
+    ma.kc = kc; ma.errs = d->errs; ma.Mpow = Mpow;
+    if (fused && (e = ppf::launch_btab(d->nbin / 2, (double *)(ws + L.Bt), st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_btab");
     // trust-region iterations.  Scattering fits: each iteration = one
     // streaming pass (k_pass) + one step (k_tr_step).  Other fits: k_moments
     // (re)centres the moment sets of the sub-ints that asked, k_tr_mom runs
@@ -310,8 +342,10 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     for (int group = sa.moments ? 3 : 6;; group = sa.moments ? 2 : 4) {
         for (int g = 0; g < group; ++g) {
             if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
-            if (sa.moments && (e = ppf::launch_moments(sa, st)) != hipSuccess)
-                return hip_fail(ctx, e, "k_moments");
+            if (sa.moments) {
+                e = fused ? ppf::launch_xmom(ma, st) : ppf::launch_moments(sa, st);
+                if (e != hipSuccess) return hip_fail(ctx, e, fused ? "k_xmom" : "k_moments");
+            }
             if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");
             if ((e = ppf::launch_tr_step(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_step");

@@ -25,21 +25,51 @@ struct XspecArgs {
     const double2 *T, *T2;
     double2 *X;                  // [nsub][nchan][N+1]
     double *chan;                // [nsub][nchan][4]
-    int guess;
-    const double *guess_weights, *guess_DM;
-    double2 *gR, *gM;            // [nsub][nblk][N+1]
-    double *gw;                  // [nsub][nblk][2]
+    // wave path: model row power sum_{k>=1} |M_nk|^2 ([nmodel][nchan]) and
+    // the per-sub-int "write X" flag (null: every sub-int).  Sub-ints whose
+    // fit runs on moments (k_xmom) are skipped.
+    const double *Mpow;
+    const uint8_t *needx;        // [nsub]
+};
+
+// k_dsum: GetTOAs guess profile, time-domain dedispersion (pptoas.py:461-464)
+struct DsumArgs {
+    int nsub, nchan, nbin, dtype, cbd, nblkd;
+    const void *data;
+    const uint8_t *mask;
+    const double *freqs, *P, *guess_DM, *guess_weights;
+    double *gP;                  // [nsub][nblkd][nbin] partial profiles
+    double *gw;                  // [nsub][nblkd][2] (sum w, count)
+};
+
+// k_xmom: fused re-FFT + cross spectrum + Taylor moments (no X in HBM)
+struct XmomArgs {
+    int nsub, nchan, nbin, log2N, nblk, cb, dtype, xcd_swizzle;
+    const void *data;
+    const double2 *Mft;
+    const int32_t *model_index;
+    const uint8_t *mask;
+    double *chan;                // [nsub][nchan][4] (written: noise, Sd, S)
+    const double *dphi;          // [nsub][nchan][2]
+    const double2 *T, *T2;
+    const void *state;           // TRState[nsub]
+    double *mom;                 // [nsub][2][nchan][kMoments] (double2)
+    const double *Bt;            // [N/2][16] folded-moment B tile (k_btab)
+    int kc;                      // get_noise_PS cut
+    const double *errs;          // [nsub][nchan] or null
+    const double *Mpow;          // [nmodel][nchan]
 };
 
 struct GuessArgs {
-    int nsub, nchan, nbin, kc, nblk, Ns;
+    int nsub, nchan, nbin, log2N, kc, nblkd, Ns;
     const uint8_t *mask;
     const double *freqs, *P, *guess_DM, *guess_tau, *nu_fits;
-    const double2 *gR, *gM;
-    const double *gw;
+    const double *gP;            // [nsub][nblkd][nbin] (k_dsum)
+    const double *gw;            // [nsub][nblkd][2]
+    const double2 *T, *T2;
     double *x0;                  // [nsub][8]
-    // wave xspec path: mean model = (Msum - masked rows) / count
-    const double2 *Msum;         // [nmodel][N+1] or null (use gM partials)
+    // mean model = (Msum - masked rows) / count
+    const double2 *Msum;         // [nmodel][N+1]
     const double2 *Mft;
     const int32_t *model_index;
 };
@@ -112,8 +142,15 @@ hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st);
+hipError_t launch_dsum(const DsumArgs &a, hipStream_t st);
 bool xspec_wave_supported(int log2N, int cb);
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);
+hipError_t launch_xmom(const XmomArgs &a, hipStream_t st);
+hipError_t launch_btab(int N, double *Bt, hipStream_t st);
+hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
+                           int moments, uint8_t *needx, hipStream_t st);
+hipError_t launch_model_pow(const double2 *Mft, int nchan, int nharm, int nmodel, double *out,
+                            hipStream_t st);
 hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out,
                             hipStream_t st);
 hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st);

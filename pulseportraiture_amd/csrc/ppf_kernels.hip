@@ -97,25 +97,8 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
     const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double *fr = a.freqs + (int64_t)s * a.nchan;
     const double sqrt_half_nbin = sqrt((double)(2 * N) / 2.0);
     const RowT *rows = reinterpret_cast<const RowT *>(a.data);
-
-    // guess stage: dedispersion phase of each channel, relative to the mean
-    // frequency of the usable channels (pptoas.py:439,462-464)
-    double Dg = 0.0, nu_mean_m2 = 0.0;
-    if (a.guess) {
-        double v[2] = {0.0, 0.0};
-        for (int n = tid; n < a.nchan; n += kBlock)
-            if (!mask || mask[n]) { v[0] += fr[n]; v[1] += 1.0; }
-        block_sum<2>(v, red);
-        Dg = kDconst * a.guess_DM[s] / a.P[s];
-        nu_mean_m2 = pow(v[0] / v[1], -2.0);
-    }
-    double2 R[KM], Mb[KM];
-#pragma unroll
-    for (int i = 0; i < KM; ++i) { R[i] = cmk(0, 0); Mb[i] = cmk(0, 0); }
-    double wsum = 0.0, wcnt = 0.0;
 
     auto skip_masked = [&](int n) {
         while (n < c1 && mask && !mask[n]) {
@@ -144,16 +127,6 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         }
         const int nn = skip_masked(n + 1);
         if (nn < c1) prefetch(nn);              // next row in flight during this FFT
-        // guess phasors first: the sincos temporaries are dead before the
-        // FFT / spectrum registers go live
-        double2 Eg = cmk(1, 0), Wg = cmk(1, 0);
-        double wn = 0.0;
-        if (a.guess) {
-            const double phg = Dg * (pow(fr[n], -2.0) - nu_mean_m2);
-            Eg = cexp2pi((double)tid * phg);
-            Wg = cexp2pi((double)kBlock * phg);
-            wn = a.guess_weights[crow];
-        }
         const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
         double2 Mv[KM];
 #pragma unroll
@@ -163,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         }
         __syncthreads();
         lds_fft_t<LOG2N, false>(buf, T);
-        // pass 1 over my harmonics: power sums and the guess accumulation
+        // pass 1 over my harmonics: power sums
         double acc[2] = {0.0, 0.0};
 #pragma unroll
         for (int i = 0; i < KM; ++i) {
@@ -173,10 +146,6 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
                 const double p2 = cabs2(D);
                 if (k >= a.kc) acc[0] += p2;
                 if (k >= 1) acc[1] += p2;
-                if (a.guess) {
-                    R[i] = cadd(R[i], cscale(cmul(D, Eg), wn));
-                    Eg = cmul(Eg, Wg);
-                }
             }
         }
         block_sum<2>(acc, red);                 // buf is not modified here
@@ -198,7 +167,6 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
                     mpow[0] += cabs2(M);
                     Xrow[k] = cscale(cmulc(rfft_bin(buf, N, T2, k), M), inv_e2);
                 }
-                if (a.guess) Mb[i] = cadd(Mb[i], M);
             }
         }
         block_sum<1>(mpow, red);
@@ -209,21 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
             chan[2] = acc[1] * inv_e2;     // Sd_n
             chan[3] = mpow[0] * inv_e2;    // S_n at tau = 0
         }
-        wsum += wn;
-        wcnt += 1.0;
         n = nn;
-    }
-    if (a.guess) {
-        const int64_t base = ((int64_t)s * a.nblk + cb) * NH;
-#pragma unroll
-        for (int i = 0; i < KM; ++i) {
-            const int k = tid + i * kBlock;
-            if (k <= N) { a.gR[base + k] = R[i]; a.gM[base + k] = Mb[i]; }
-        }
-        if (tid == 0) {
-            a.gw[((int64_t)s * a.nblk + cb) * 2 + 0] = wsum;
-            a.gw[((int64_t)s * a.nblk + cb) * 2 + 1] = wcnt;
-        }
     }
 }
 
@@ -313,44 +267,115 @@ __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int 
 }
 
 // ===========================================================================
+// k_dsum: the GetTOAs guess profile (pptoas.py:461-464): the portrait
+// rotated by the guess DM relative to the mean usable frequency and
+// averaged with the channel weights, rot_prof(t) = sum_n w_n x_n(t + tau_n) /
+// sum_n w_n, tau_n = nbin Dconst DM/P (nu_n^-2 - nu_mean^-2).  The shift is
+// applied in the time domain by linear interpolation between bins (the
+// reference rotates each channel in the Fourier domain): this profile only
+// seeds the phase of the trust-region fit, whose converged result does not
+// depend on it, and the pass then streams the data once at HBM rate with no
+// per-channel FFT.  Grid: (sub-int, block of cbd channels); thread t owns
+// bins t + 256 j; output: the block's partial sum (fixed channel order).
+// ===========================================================================
+template <int DT, int JB>
+__global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
+    using ElT = typename std::conditional<DT == 0, float, double>::type;
+    __shared__ double red[kWaves * 4];
+    const int tid = threadIdx.x;
+    const int s = blockIdx.x / a.nblkd, blk = blockIdx.x % a.nblkd;
+    const int nbin = a.nbin, bmask = nbin - 1;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    double v[2] = {0.0, 0.0};
+    for (int n = tid; n < a.nchan; n += kBlock)
+        if (!mask || mask[n]) { v[0] += fr[n]; v[1] += 1.0; }
+    block_sum<2>(v, red);
+    const double Dg = kDconst * a.guess_DM[s] / a.P[s];
+    const double nu_mean_m2 = pow(v[0] / v[1], -2.0);
+    const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
+    const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)s * a.nchan * nbin;
+    double wsum = 0.0, wcnt = 0.0;
+    for (int t0 = 0; t0 < nbin; t0 += JB * kBlock) {
+        double p[JB];
+#pragma unroll
+        for (int j = 0; j < JB; ++j) p[j] = 0.0;
+        for (int n = c0; n < c1; ++n) {
+            if (mask && !mask[n]) continue;
+            const double w = a.guess_weights[(int64_t)s * a.nchan + n];
+            const double tau = (double)nbin * Dg * (pow(fr[n], -2.0) - nu_mean_m2);
+            const double fl = floor(tau);
+            const double f = tau - fl;
+            const int i0 = (int)(fl - (double)nbin * floor(fl / (double)nbin));   // mod nbin
+            const double wa = w * (1.0 - f), wb = w * f;
+            const ElT *x = rows + (int64_t)n * nbin;
+#pragma unroll
+            for (int j = 0; j < JB; ++j) {
+                const int t = t0 + tid + j * kBlock;
+                if (t < nbin) {
+                    const int ia = (t + i0) & bmask;
+                    p[j] = fma(wa, (double)x[ia], fma(wb, (double)x[(ia + 1) & bmask], p[j]));
+                }
+            }
+            if (t0 == 0) { wsum += w; wcnt += 1.0; }
+        }
+        double *out = a.gP + ((int64_t)s * a.nblkd + blk) * nbin;
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+            const int t = t0 + tid + j * kBlock;
+            if (t < nbin) out[t] = p[j];
+        }
+    }
+    if (tid == 0) {
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 0] = wsum;
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 1] = wcnt;
+    }
+}
+
+// ===========================================================================
 // k_guess: GetTOAs initial phase (pptoas.py:461-499): FFTFIT of the weighted,
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
 // ===========================================================================
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];   // xm[N+1] | sh[Ns+8]
+    // lds: z[N] (packed profile, FFT in place) | xm[N+1] | sh[Ns+8]
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const int N = a.nbin >> 1, nharm = N + 1, s = blockIdx.x, tid = threadIdx.x;
-    double *sh = reinterpret_cast<double *>(lds + nharm + 1);
-    double ws[2] = {0.0, 0.0};
+    double2 *z = lds, *xm = lds + N;
+    double *sh = reinterpret_cast<double *>(xm + nharm + 1);
     if (tid == 0) {
-        for (int b = 0; b < a.nblk; ++b) {
-            ws[0] += a.gw[((int64_t)s * a.nblk + b) * 2 + 0];
-            ws[1] += a.gw[((int64_t)s * a.nblk + b) * 2 + 1];
+        double w0 = 0.0, w1 = 0.0;
+        for (int b = 0; b < a.nblkd; ++b) {
+            w0 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 0];
+            w1 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 1];
         }
-        sh[0] = ws[0]; sh[1] = ws[1];
+        sh[0] = w0; sh[1] = w1;
+    }
+    // weighted dedispersed profile: sum of the k_dsum block partials (fixed
+    // order), packed z_j = p_2j + i p_2j+1 for the real FFT
+    for (int j = tid; j < N; j += kBlock) {
+        double pe = 0.0, po = 0.0;
+        for (int b = 0; b < a.nblkd; ++b) {
+            const double *pp = a.gP + ((int64_t)s * a.nblkd + b) * a.nbin;
+            pe += pp[2 * j];
+            po += pp[2 * j + 1];
+        }
+        z[j] = cmk(pe, po);
     }
     __syncthreads();
     const double wsum = sh[0], cnt = sh[1];
-    __syncthreads();
+    lds_fft(z, a.log2N, a.T, false);
     double pw[1] = {0.0};
     for (int k = tid; k <= N; k += kBlock) {
-        double2 R = cmk(0, 0), M = cmk(0, 0);
-        for (int b = 0; b < a.nblk; ++b) {
-            int64_t o = ((int64_t)s * a.nblk + b) * nharm + k;
-            R = cadd(R, a.gR[o]);
-            if (!a.Msum) M = cadd(M, a.gM[o]);
-        }
-        if (a.Msum) {
-            const int mi = a.model_index ? a.model_index[s] : 0;
-            const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
-            const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-            M = a.Msum[(int64_t)mi * nharm + k];
-            if (mask)
-                for (int n = 0; n < a.nchan; ++n)
-                    if (!mask[n]) M = csub(M, Mm[(int64_t)n * nharm + k]);
-        }
-        R = cscale(R, 1.0 / wsum);
+        double2 R = cscale(rfft_bin(z, N, a.T2, k), 1.0 / wsum);
+        const int mi = a.model_index ? a.model_index[s] : 0;
+        const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
+        const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+        double2 M = a.Msum[(int64_t)mi * nharm + k];
+        if (mask)
+            for (int n = 0; n < a.nchan; ++n)
+                if (!mask[n]) M = csub(M, Mm[(int64_t)n * nharm + k]);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
             double u = kTwoPi * (double)k * a.guess_tau[s];
@@ -359,12 +384,12 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
         }
         if (k == N) R.y = 0.0;   // irfft drops the imaginary Nyquist part
         if (k >= a.kc) pw[0] += cabs2(R);
-        lds[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(R, M);
+        xm[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(R, M);
     }
     block_sum<1>(pw, red);
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
     const double err = sig * sqrt((double)a.nbin / 2.0);
-    const double phase = brute_fmin(lds, nharm, 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
+    const double phase = brute_fmin(xm, nharm, 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
                                     nullptr);
     if (tid == 0) {
         // nu_mean of the usable channels
@@ -600,8 +625,25 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
     }
     return hipGetLastError();
 }
+hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblkd)), b(kBlock);
+    const int jb = a.nbin >= 2048 ? 8 : (a.nbin + kBlock - 1) / kBlock;
+    if (a.dtype == 0) {
+        if (jb >= 8) hipLaunchKernelGGL((k_dsum<0, 8>), g, b, 0, st, a);
+        else if (jb >= 4) hipLaunchKernelGGL((k_dsum<0, 4>), g, b, 0, st, a);
+        else if (jb >= 2) hipLaunchKernelGGL((k_dsum<0, 2>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_dsum<0, 1>), g, b, 0, st, a);
+    } else {
+        if (jb >= 8) hipLaunchKernelGGL((k_dsum<1, 8>), g, b, 0, st, a);
+        else if (jb >= 4) hipLaunchKernelGGL((k_dsum<1, 4>), g, b, 0, st, a);
+        else if (jb >= 2) hipLaunchKernelGGL((k_dsum<1, 2>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_dsum<1, 1>), g, b, 0, st, a);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2 + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
+    size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
     hipLaunchKernelGGL(k_guess, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }

@@ -21,6 +21,7 @@
 // of a channel row in flight.
 #include "ppf_device.hpp"
 #include "ppf_internal.hpp"
+#include "ppf_state.hpp"
 
 namespace ppf {
 
@@ -114,31 +115,6 @@ __device__ __forceinline__ Fac make_fac(double nu, const FitGeom &g, double alph
     return f;
 }
 
-// ===========================================================================
-// per-sub-integration solver state (workspace)
-// ===========================================================================
-enum { PH_INIT = 0, PH_PROPOSAL = 1, PH_DONE = 2 };
-
-struct TRState {
-    double x[5];          // accepted point
-    double th[5];         // point the next pass evaluates
-    double f, g[5], H[15];  // model at x (H upper triangle, all 5 params)
-    double radius, pred;
-    double nu_fit[3], nu_mean, Sd, dof, phi_guess;
-    int k, status, nfev, phase;
-    int slot_cur, slot_eval, flagmask, nchanx;
-    int scat, hb, g_sum, g_tau;
-    int g_alpha, pad0, pad1, pad2;
-    // moment mode (no scattering): two moment sets centred at mc[q]
-    int mmode, need_mom, mtarget, macc;
-    int mvalid[2], meval, nmom;
-    double mc[2][3];
-};
-
-__device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j
-    return i * 5 - (i * (i - 1)) / 2 + (j - i);
-}
-
 // reference gates (taus.sum(), dtau.sum(), dalpha.sum()) at (tau_lin, alpha)
 // over the usable channels; wave-level (all 64 lanes of the calling wave).
 __device__ void wave_gates(const double *fr, const uint8_t *mask, int nchan, double tau_lin,
@@ -159,6 +135,19 @@ __device__ void wave_gates(const double *fr, const uint8_t *mask, int nchan, dou
     g_alpha = s2 != 0.0;
 }
 
+// k_classify: which sub-ints need the cross spectrum X in HBM (scattering
+// fits, which k_pass streams; or every fit when the moment solver is off).
+// Same test as k_tr_init's `scat`.
+__global__ void k_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
+                           int moments, uint8_t *needx) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nsub) return;
+    const double x3 = init[(int64_t)s * 5 + 3];
+    const double tau0 = log10_tau ? pow(10.0, x3) : x3;
+    const bool scat = fit_flags[(int64_t)s * 5 + 3] || fit_flags[(int64_t)s * 5 + 4] || tau0 != 0.0;
+    needx[s] = (!moments || scat) ? 1 : 0;
+}
+
 // ===========================================================================
 // k_tr_init: one wave per sub-integration (4 per workgroup)
 // ===========================================================================
@@ -168,11 +157,11 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
     if (s >= a.nsub) return;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double *chan = a.chan + (int64_t)s * a.nchan * 4;
-    double sf = 0.0, cnt = 0.0, sd = 0.0;
+    // (runs before the spectrum kernels: nothing here reads chan[])
+    double sf = 0.0, cnt = 0.0;
     for (int n = lane; n < a.nchan; n += 64)
-        if (!mask || mask[n]) { sf += fr[n]; cnt += 1.0; sd += chan[n * 4 + 2]; }
-    sf = wave_sum(sf); cnt = wave_sum(cnt); sd = wave_sum(sd);
+        if (!mask || mask[n]) { sf += fr[n]; cnt += 1.0; }
+    sf = wave_sum(sf); cnt = wave_sum(cnt);
     TRState &S = a.state[s];
     int flagmask = 0, nf = 0;
     for (int i = 0; i < 5; ++i)
@@ -198,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         S.pred = 0.0;
         for (int i = 0; i < 3; ++i) S.nu_fit[i] = nu_fit[i];
         S.nu_mean = nu_mean;
-        S.Sd = sd;
+        S.Sd = 0.0;                     // summed from chan[] in k_postfit
         S.dof = cnt * (double)a.nbin - (double)(nf + (int)cnt);
         S.phi_guess = x[0];
         S.k = 0;
@@ -241,11 +230,10 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
             const double nu = fr[n];
             dp[2 * n + 0] = kDconst * (pow(nu, -2.0) - nuDM2) / P;
             dp[2 * n + 1] = kDconst * kDconst * (pow(nu, -4.0) - nuGM4) / P;
-            const bool use = !mask || mask[n];
+            // S_n (slot 6) is stored with C, C', C'' by k_tr_mom
             for (int q = 0; q < 2; ++q) {
                 double *d = st + ((int64_t)q * a.nchan + n) * 10;
                 for (int j = 0; j < 10; ++j) d[j] = 0.0;
-                d[6] = use ? chan[n * 4 + 3] : 0.0;
             }
         }
     }
@@ -717,8 +705,9 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
             const double2 K2 = cscale(cmul(eix, cadd(cadd(G0, G2), cscale(G1, 2.0))), h * h);
             const double C = F.x, Cp = -kTwoPi * K1.y, Cpp = -kTwoPi * kTwoPi * K2.x;
             double *sn = st + (int64_t)n * 10;
-            sn[0] = C; sn[1] = Cp; sn[2] = Cpp;
-            const double iS = 1.0 / chan[n * 4 + 3];
+            const double Sn = chan[n * 4 + 3];
+            sn[0] = C; sn[1] = Cp; sn[2] = Cpp; sn[6] = Sn;
+            const double iS = 1.0 / Sn;
             const double dph[3] = {1.0, d1, d2};
             const double hn = -2.0 * (C * Cpp + Cp * Cp) * iS;
             // acc: f, g(phi, DM, GM), H upper triangle 00 01 02 11 12 22
@@ -792,7 +781,18 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
     const double fun = S.f;
     const int status = S.status, nfev = S.nfev, k = S.k;
     const bool scat = S.scat != 0;
-    const double nu_mean = S.nu_mean, Sd = S.Sd, dof = S.dof, phi_guess = S.phi_guess;
+    const double nu_mean = S.nu_mean, dof = S.dof, phi_guess = S.phi_guess;
+    // Sd = sum_n |D_n|^2 / sigma~_n^2 over the usable channels
+    // (pptoaslib.py:1031), from the spectrum kernels' chan[]
+    double sdv[1] = {0.0};
+    {
+        const double *chan = a.chan + (int64_t)s * a.nchan * 4;
+        const uint8_t *mk = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+        for (int n = tid; n < a.nchan; n += kBlock)
+            if (!mk || mk[n]) sdv[0] += chan[n * 4 + 2];
+    }
+    block_sum<1>(sdv, red);
+    const double Sd = sdv[0];
     const int nchanx = S.nchanx;
     FitGeom g;
     g.P = a.P[s];
@@ -1161,6 +1161,13 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
 static int pass_unroll(int nharm) {
     int j = (nharm + 63) / 64;
     return j >= 17 ? 17 : j >= 9 ? 9 : j >= 5 ? 5 : j >= 3 ? 3 : j >= 2 ? 2 : 1;
+}
+
+hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
+                           int moments, uint8_t *needx, hipStream_t st) {
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)((nsub + 255) / 256)), dim3(256), 0, st, nsub,
+                       fit_flags, init, log10_tau, moments, needx);
+    return hipGetLastError();
 }
 
 hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st) {

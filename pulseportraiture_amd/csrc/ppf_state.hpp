@@ -1,0 +1,33 @@
+// ppf_state.hpp -- per-sub-integration solver state shared by the solver
+// (ppf_solve.hip) and the fused moment kernel (ppf_xspec.hip).
+#pragma once
+#include "ppf_device.hpp"
+
+namespace ppf {
+
+// ===========================================================================
+// per-sub-integration solver state (workspace)
+// ===========================================================================
+enum { PH_INIT = 0, PH_PROPOSAL = 1, PH_DONE = 2 };
+
+struct TRState {
+    double x[5];          // accepted point
+    double th[5];         // point the next pass evaluates
+    double f, g[5], H[15];  // model at x (H upper triangle, all 5 params)
+    double radius, pred;
+    double nu_fit[3], nu_mean, Sd, dof, phi_guess;
+    int k, status, nfev, phase;
+    int slot_cur, slot_eval, flagmask, nchanx;
+    int scat, hb, g_sum, g_tau;
+    int g_alpha, pad0, pad1, pad2;
+    // moment mode (no scattering): two moment sets centred at mc[q]
+    int mmode, need_mom, mtarget, macc;
+    int mvalid[2], meval, nmom;
+    double mc[2][3];
+};
+
+__device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j
+    return i * 5 - (i * (i - 1)) / 2 + (j - i);
+}
+
+}  // namespace ppf

@@ -1,31 +1,46 @@
-// ppf_xspec.hip -- wave-per-row cross-spectrum kernel (128 <= nbin/2 <= 1024).
+// ppf_xspec.hip -- wave-per-row spectrum kernels (128 <= nbin/2 <= 1024).
 //
-// k_xspec_w<LOG2N, DT, GUESS>: workgroup = 8 waves = one (sub-integration,
-// block of CB channels); each wave takes CB/8 consecutive channel rows and,
-// per row, with no workgroup barrier:
-//   global f32/f64 row (prefetched one row ahead)  -> registers
-//   wave FFT of the N = nbin/2 complex points (ppf_wfft.hpp)
-//   real-FFT post-pass on (k, N-k) pairs -> D_k, D_{N-k}
-//   get_noise_PS noise (pplib.py:2312-2332), Sd_n, S_n(tau=0)
-//   X_k = D_k conj(M_k) / sigma~_n^2 (pptoaslib.py:1014-1031), k = 0 zeroed
-//   [GUESS] accumulate w_n D_k exp(2 pi i k phi_n) for the dedispersed mean
-//           profile of GetTOAs' initial phase (pptoas.py:461-499)
-// The mean model spectrum of the guess is model-only: k_model_sum forms
-// sum_n M_nk once per call and k_guess subtracts the masked channels.
+// Both kernels give one channel row to one wave: the row is loaded from HBM
+// (f32 or f64, prefetched one row ahead), transformed by the wave-private
+// register/LDS FFT of ppf_wfft.hpp (no workgroup barrier inside a row) and
+// finished by the real-FFT post-pass on (k, N-k) pairs.
 //
-// The 8 waves of a workgroup take the block's channels in rounds (round r:
-// channel base + 8 r + wave); in GUESS mode each round's 8 contributions are
-// summed into a block accumulator in LDS in wave order (deterministic).
-// LDS: 8 padded wave buffers (17/16 N x 16 B) [+ the N+1 accumulator] =
-// 136 [152] KiB at N = 1024: one workgroup (8 waves, 2 per SIMD) per CU.
+// k_xspec_w<LOG2N, DT>: the cross spectrum for the sub-ints whose fit
+//   streams it (scattering fits, k_pass):
+//     get_noise_PS noise (pplib.py:2312-2332), Sd_n, S_n(tau = 0)
+//     X_k = D_k conj(M_k) / sigma~_n^2 (pptoaslib.py:1014-1031), k = 0 zeroed
+//   Sub-ints fitted from moments (TRState.mmode) are skipped: k_xmom_w
+//   produces everything they need without X.
+//
+// k_xmom_w<LOG2N, DT, XW>: the fused moment pass (fits without scattering).
+//   The cross spectrum never reaches HBM: for every sub-int that asks for a
+//   moment set (need_mom, centre mc[mtarget]) the workgroup re-reads its
+//   block of channel rows and per row forms the noise, Sd_n, S_n (chan[]) and
+//     Y_k = D_k conj(M_k) e^{2 pi i k phi_c,n}   (phi_c,n = c0 + c1 dphi1_n
+//                                                  + c2 dphi2_n)
+//   The moments mu_m = sum_{k=1..N} Y_k u_k^m / sigma~_n^2, u_k = (k - N/2)
+//   / (N/2), fold the harmonic pairs (k, N-k), u_{N-k} = -u_k:
+//     mu_2j   = sum_{k<N/2} (Y_k + Y_{N-k})       (u_k^2)^j  + [j=0] Y_{N/2}
+//     mu_2j+1 = sum_{k<N/2} (Y_k - Y_{N-k}) u_k   (u_k^2)^j
+//   so both halves share one B tile (v_k^j, v = u^2, j < 16) and the MFMA
+//   K loop runs over N/2 harmonics.  A = 16 rows of v_mfma_f64_16x16x4f64
+//   from the XW wave buffers: XW = 8 -> 8 channels x {Re, Im}, one MFMA per
+//   half; XW = 4 -> 4 channels x {even, odd} x {Re, Im}, one MFMA.  Each
+//   wave takes 1/XW of the folded harmonics; the partial tiles are summed in
+//   wave order through LDS (deterministic) and scaled by 1/sigma~_n^2.
+//   Output: mu[s][q][n][m] (k_tr_mom consumes it).  HBM traffic per sub-int:
+//   the data rows (nchan nbin s_in B) + the moments (nchan 32 16 B).
+#include <cstdlib>
 #include <type_traits>
 
 #include "ppf_internal.hpp"
+#include "ppf_state.hpp"
 #include "ppf_wfft.hpp"
 
 namespace ppf {
 
-constexpr int kXW = 8;                 // waves per workgroup
+constexpr int kXW = 8;                 // waves per k_xspec_w workgroup
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef PPF_SCHED_CUT
 #define PPF_SCHED_CUT 1
 #endif
@@ -34,8 +49,47 @@ constexpr int kXW = 8;                 // waves per workgroup
 #else
 #define SCHED_CUT()
 #endif
+#ifndef PPF_XM_CUT
+#define PPF_XM_CUT 0
+#endif
+#if PPF_XM_CUT
+#define XM_CUT() __builtin_amdgcn_sched_barrier(0)
+#else
+#define XM_CUT()
+#endif
 
-template <int LOG2N, int DT, bool GUESS>
+// XCD-aware block -> (sub-int, channel block): blocks b and b+8 share an
+// XCD, so each XCD keeps only its channel blocks' model rows in its L2
+__device__ __forceinline__ void block_map(int xcd_swizzle, int nblk, int &s, int &cb) {
+    if (xcd_swizzle) {
+        const int per = nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
+        cb = x * per + r % per;
+        s = r / per;
+    } else {
+        s = blockIdx.x / nblk;
+        cb = blockIdx.x % nblk;
+    }
+}
+
+// real-FFT post-pass of the pair (k, N-k), k = lane + 64 i, from the wave's
+// LDS spectrum; w = exp(-i pi k / N)
+template <int LOG2N>
+__device__ __forceinline__ void rfft_pair(const double2 *buf, int k, double2 w, double2 &Dlo,
+                                          double2 &Dhi) {
+    constexpr int N = 1 << LOG2N;
+    const double2 zk = buf[wfft::pad<LOG2N>(k)];
+    const double2 zn = buf[k == 0 ? 0 : wfft::pad<LOG2N>(N - k)];
+    const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+    const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
+    const double2 wo = cmul(w, o);
+    Dlo = cmk(e.x + wo.y, e.y - wo.x);
+    Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
+}
+
+// ===========================================================================
+// k_xspec_w: cross spectrum X of the sub-ints that stream it
+// ===========================================================================
+template <int LOG2N, int DT>
 __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
@@ -43,44 +97,22 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     constexpr int SL = wfft::buf_slots<LOG2N>();      // padded wave buffer
     using RowT = typename std::conditional<DT == 0, float2, double2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double2 *buf = lds + wave * SL;
-    double2 *racc = lds + kXW * SL;                   // [N+1] block guess accumulator
-    double *tail = reinterpret_cast<double *>(racc + NH);   // [kXW][2]
 
     int s, cb;
-    if (a.xcd_swizzle) {
-        const int per = a.nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
-        cb = x * per + r % per;
-        s = r / per;
-    } else {
-        s = blockIdx.x / a.nblk;
-        cb = blockIdx.x % a.nblk;
-    }
+    block_map(a.xcd_swizzle, a.nblk, s, cb);
+    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int
     // rounds: in round r wave w takes channel cb*CB + r*kXW + w
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
     const int nround = (a.cb + kXW - 1) / kXW;
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double *fr = a.freqs + (int64_t)s * a.nchan;
     const double sqrtN = sqrt((double)N);
     const RowT *rows = reinterpret_cast<const RowT *>(a.data);
     // rfft post-pass twiddles w_k = exp(-i pi k / N), k = lane + 64 i, by
     // recurrence from w_lane (T2) with step exp(-i pi 64 / N) = T2[64]
     const double2 w_seed = a.T2[lane], w_step = a.T2[64];
-
-    double Dg = 0.0, nu_mean_m2 = 0.0, wsum = 0.0, wcnt = 0.0;
-    if constexpr (GUESS) {
-        double v0 = 0.0, v1 = 0.0;
-        for (int n = lane; n < a.nchan; n += 64)
-            if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
-        v0 = wave_sum(v0);
-        v1 = wave_sum(v1);
-        Dg = kDconst * a.guess_DM[s] / a.P[s];
-        const double nm = v0 / v1;
-        nu_mean_m2 = 1.0 / (nm * nm);
-        for (int k = tid; k < NH; k += 64 * kXW) racc[k] = cmk(0.0, 0.0);
-    }
 
     auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
     RowT zr[R];
@@ -97,165 +129,290 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
             if (lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
             if (usable(n + kXW)) fetch(n + kXW);
         }
+        if (!live) continue;
+        const int64_t crow = (int64_t)s * a.nchan + n;
+        double2 x[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+        if (usable(n + kXW)) fetch(n + kXW);       // next row in flight during this FFT
+        wfft::fft_row<LOG2N>(x, buf, a.T, lane);
+
+        // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
+        double pn = 0.0, pd = 0.0;
+        {
+            double2 w = w_seed;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int klo = lane + 64 * i, khi = N - klo;
+                double2 Dlo, Dhi;
+                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                w = cmul(w, w_step);
+                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                if (klo >= a.kc) pn += p0;
+                if (khi >= a.kc) pn += p1;
+                if (klo >= 1) pd += p0;
+                pd += p1;
+                SCHED_CUT();
+            }
+        }
+        double2 Dm = cmk(0.0, 0.0);
+        if (lane == 0) {
+            const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
+            Dm = cmk(zm.x, -zm.y);
+            const double p = cabs2(Dm);
+            if (N / 2 >= a.kc) pn += p;
+            pd += p;
+        }
+        pn = wave_sum(pn);
+        pd = wave_sum(pd);
+        double errs_FT;
+        if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+        else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+
+        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+        double2 *Xrow = a.X + crow * NH;
+        {
+            double2 w = w_seed;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int klo = lane + 64 * i, khi = N - klo;
+                double2 Dlo, Dhi;
+                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                w = cmul(w, w_step);
+                const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
+                Xrow[klo] = (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
+                Xrow[khi] = cscale(cmulc(Dhi, Mhi), inv_e2);
+                SCHED_CUT();
+            }
+        }
+        if (lane == 0) {
+            Xrow[N / 2] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
+            double *chan = a.chan + crow * 4;
+            chan[0] = errs_FT;
+            chan[1] = inv_e2;
+            chan[2] = pd * inv_e2;                                  // Sd_n
+            chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+        }
+        wfft::wave_sync();
+    }
+}
+
+// ===========================================================================
+// k_xmom_w: fused moment pass (see the file header)
+// ===========================================================================
+template <int LOG2N, int XW>
+__host__ __device__ constexpr int xmom_slw() {
+    // >= 256 slots (the partial tile) + two side slots; consecutive wave
+    // buffers start 8 (XW = 8) or 16 (XW = 4) banks apart for the A reads
+    return (wfft::buf_slots<LOG2N>() < 272 ? 272 : wfft::buf_slots<LOG2N>()) + (XW == 8 ? 2 : 4);
+}
+
+template <int LOG2N, int DT, int XW>
+__global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2))) void k_xmom_w(XmomArgs a) {
+    using P = wfft::Plan<LOG2N>;
+    constexpr int N = P::N, R = P::R, NH = N + 1;
+    constexpr int NP = N / 128;
+    constexpr int SLW = xmom_slw<LOG2N, XW>();
+    constexpr int SIDE = SLW - 1;      // Y_{N/2}
+    constexpr int SIDE2 = SLW - 2;     // 1/sigma~_n^2 of the row (.x)
+    constexpr int KPW = N / 2 / XW;    // folded harmonics (MFMA K) per wave
+    using RowT = typename std::conditional<DT == 0, float2, double2>::type;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double2 *buf = lds + wave * SLW;
+
+    int s, cb;
+    block_map(a.xcd_swizzle, a.nblk, s, cb);
+    const TRState &S = reinterpret_cast<const TRState *>(a.state)[s];
+    if (!S.mmode || !S.need_mom) return;                 // uniform per workgroup
+    const int q = S.mtarget;
+    const double c0 = S.mc[q][0], c1 = S.mc[q][1], c2 = S.mc[q][2];
+
+    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
+    const int nround = (a.cb + XW - 1) / XW;
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
+    const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    const double sqrtN = sqrt((double)N);
+    double *mom = a.mom + (((int64_t)s * 2 + q) * a.nchan) * kMoments * 2;
+
+    // MFMA operand roles (v_mfma_f64_16x16x4f64: A row = lane & 15, B col =
+    // lane & 15, K index = lane >> 4); B = v_k^col from the table Bt
+    const int arow = lane & 15, kk = lane >> 4;
+    const int ach = XW == 8 ? arow >> 1 : arow >> 2;
+    const int aset = XW == 8 ? 0 : (arow >> 1) & 1;
+    const double *abase = reinterpret_cast<const double *>(lds + ach * SLW) + (arow & 1);
+    constexpr double ih = 2.0 / (double)N;
+    const int k0 = wave * KPW;
+    const double *btab = a.Bt + (int64_t)(k0 + kk) * 16 + (lane & 15);
+
+    auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
+    RowT zr[R];
+    double nx_d0 = 0.0, nx_d1 = 0.0, nx_e = 0.0;         // next row's scalars
+    auto fetch = [&](int n) {
+        const int64_t row = (int64_t)s * a.nchan + n;
+        const RowT *src = rows + row * N;
+#pragma unroll
+        for (int qq = 0; qq < R; ++qq) zr[qq] = src[lane + 64 * qq];
+        nx_d0 = a.dphi[row * 2];
+        nx_d1 = a.dphi[row * 2 + 1];
+        if (a.errs) nx_e = a.errs[row];
+    };
+    int n = cbase + wave;
+    if (usable(n)) fetch(n);
+    for (int r = 0; r < nround; ++r, n += XW) {
+        const bool live = usable(n);
+        if (n < cend && !live) {
+            if (lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
+            if (usable(n + XW)) fetch(n + XW);
+        }
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
             double2 x[R];
 #pragma unroll
-            for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-            if (usable(n + kXW)) fetch(n + kXW);       // next row in flight during this FFT
+            for (int qq = 0; qq < R; ++qq) x[qq] = cmk((double)zr[qq].x, (double)zr[qq].y);
+            const double phc = c0 + c1 * nx_d0 + c2 * nx_d1, errs_in = nx_e;
+            if (usable(n + XW)) fetch(n + XW);
             wfft::fft_row<LOG2N>(x, buf, a.T, lane);
 
-            // real-FFT post-pass on pairs (k, N-k), k = lane + 64 i < N/2; lane
-            // 0 also owns k = N/2.  Pass 1: power sums (noise, Sd); pass 2
-            // recomputes D from the LDS spectrum.
-            auto dpair = [&](int i, double2 w, double2 &Dlo, double2 &Dhi) {
-                const int k = lane + 64 * i;
-                const double2 zk = buf[wfft::pad<LOG2N>(k)];
-                const double2 zn = buf[k == 0 ? 0 : wfft::pad<LOG2N>(N - k)];
-                const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
-                const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
-                const double2 wo = cmul(w, o);
-                Dlo = cmk(e.x + wo.y, e.y - wo.x);
-                Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
-            };
-            auto dmid = [&]() {
-                const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
-                return cmk(zm.x, -zm.y);
-            };
-            double pn = 0.0, pd = 0.0;
-            {
-                double2 w = w_seed;
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            __builtin_amdgcn_sched_barrier(0);
+            double2 E = cexp2pi((double)lane * phc);
+            __builtin_amdgcn_sched_barrier(0);
+            const double2 W = cexp2pi(64.0 * phc);
+            double2 Em = W;          // e^{2 pi i (N/2) phc} = W^(N/128)
 #pragma unroll
-                for (int i = 0; i < NP; ++i) {
-                    const int klo = lane + 64 * i, khi = N - klo;
-                    double2 Dlo, Dhi;
-                    dpair(i, w, Dlo, Dhi);
-                    w = cmul(w, w_step);
-                    const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
-                    if (klo >= a.kc) pn += p0;
-                    if (khi >= a.kc) pn += p1;
-                    if (klo >= 1) pd += p0;
-                    pd += p1;
-                    SCHED_CUT();
-                }
+            for (int t = 128; t < N; t <<= 1) Em = cmul(Em, Em);
+            const double2 EN = cmul(Em, Em);
+            __builtin_amdgcn_sched_barrier(0);
+            double2 Dm = cmk(0.0, 0.0);
+            if (lane == 0) {
+                const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
+                Dm = cmk(zm.x, -zm.y);
+            }
+            // in place: iteration i reads and rewrites only pad(k) and
+            // pad(N - k), k = lane + 64 i: S_k -> pad(k), (Y_k - Y_{N-k}) u_k
+            // -> pad(N - k) (k = 0: -> pad(N/2), read above as Dm).  The
+            // power sums of the noise / Sd ride along.
+            double pn = 0.0, pd = 0.0;
+            double2 w = w_seed;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const int klo = lane + 64 * i, khi = N - klo;
+                double2 Dlo, Dhi;
+                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                w = cmul(w, w_step);
+                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                if (klo >= a.kc) pn += p0;
+                if (khi >= a.kc) pn += p1;
+                if (klo >= 1) pd += p0;
+                pd += p1;
+                const double2 Ylo = klo == 0 ? cmk(0.0, 0.0) : cmul(cmulc(Dlo, Mrow[klo]), E);
+                const double2 Yhi = cmul(cmulc(Dhi, Mrow[khi]), cmul(EN, cconj(E)));
+                const double uk = (double)(klo - N / 2) * ih;
+                buf[wfft::pad<LOG2N>(klo)] = cadd(Ylo, Yhi);
+                buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
+                    cscale(csub(Ylo, Yhi), uk);
+                E = cmul(E, W);
+                XM_CUT();
             }
             if (lane == 0) {
-                const double p = cabs2(dmid());
+                const double p = cabs2(Dm);
                 if (N / 2 >= a.kc) pn += p;
                 pd += p;
+                buf[SIDE] = cmul(cmulc(Dm, Mrow[N / 2]), Em);
             }
             pn = wave_sum(pn);
             pd = wave_sum(pd);
-            double errs_FT;
-            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
-            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            const double errs_FT = a.errs ? errs_in * sqrtN
+                                          : sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-
-            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-            double2 *Xrow = a.X + crow * NH;
-            double wn = 0.0;
-            double2 E = cmk(1.0, 0.0), W = cmk(1.0, 0.0), EN = cmk(1.0, 0.0), Em = cmk(1.0, 0.0);
-            if constexpr (GUESS) {
-                // phasor seeds in a region of their own: the sincos
-                // temporaries must not interleave with the post-pass
-                __builtin_amdgcn_sched_barrier(0);
-                wn = a.guess_weights[crow];
-                const double fn = fr[n];
-                const double phg = Dg * (1.0 / (fn * fn) - nu_mean_m2);
-                E = cexp2pi((double)lane * phg);
-                __builtin_amdgcn_sched_barrier(0);
-                W = cexp2pi(64.0 * phg);
-                // exp(2 pi i N/2 phg) = W^(N/128), exp(2 pi i N phg) = W^(N/64)
-                Em = W;
-#pragma unroll
-                for (int t = 128; t < N; t <<= 1) Em = cmul(Em, Em);
-                EN = cmul(Em, Em);
-                wsum += wn;
-                wcnt += 1.0;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            // GUESS: the contribution w_n D_k exp(2 pi i k phi_n) overwrites the
-            // spectrum slot it was computed from (pad(k) for 0 < k < N, slot 0
-            // for k = N; k = 0 is not used by the guess).  No lane reads a slot
-            // another lane has already overwritten: iteration i reads only
-            // pad(lane + 64 i) and pad(N - lane - 64 i).
-            double mp = 0.0;
-            double2 Dm = cmk(0.0, 0.0);
-            if (lane == 0) Dm = dmid();
-            {
-                double2 w = w_seed;
-#pragma unroll
-                for (int i = 0; i < NP; ++i) {
-                    const int klo = lane + 64 * i, khi = N - klo;
-                    double2 Dlo, Dhi;
-                    dpair(i, w, Dlo, Dhi);
-                    w = cmul(w, w_step);
-                    const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
-                    if (klo >= 1) mp += cabs2(Mlo);
-                    mp += cabs2(Mhi);
-                    Xrow[klo] = (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
-                    Xrow[khi] = cscale(cmulc(Dhi, Mhi), inv_e2);
-                    if constexpr (GUESS) {
-                        // exp(2 pi i (N - k) phg) = EN conj(E_k)
-                        const double2 chi = cscale(cmul(Dhi, cmul(EN, cconj(E))), wn);
-                        if (klo != 0) {
-                            buf[wfft::pad<LOG2N>(klo)] = cscale(cmul(Dlo, E), wn);
-                            buf[wfft::pad<LOG2N>(khi)] = chi;
-                        } else {
-                            buf[0] = chi;
-                        }
-                        E = cmul(E, W);
-                    }
-                    SCHED_CUT();
-                }
-            }
             if (lane == 0) {
-                const double2 Mm = Mrow[N / 2];
-                mp += cabs2(Mm);
-                Xrow[N / 2] = cscale(cmulc(Dm, Mm), inv_e2);
-                if constexpr (GUESS) buf[wfft::pad<LOG2N>(N / 2)] = cscale(cmul(Dm, Em), wn);
-            }
-            mp = wave_sum(mp);
-            if (lane == 0) {
+                buf[SIDE2] = cmk(inv_e2, 0.0);
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
-                chan[2] = pd * inv_e2;        // Sd_n
-                chan[3] = mp * inv_e2;        // S_n at tau = 0
+                chan[2] = pd * inv_e2;                                  // Sd_n
+                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
             }
-            wfft::wave_sync();
-        } else if (GUESS) {
-            for (int k = lane; k < SL; k += 64) buf[k] = cmk(0.0, 0.0);
-        }
-        if constexpr (GUESS) {
-            // block accumulation of this round's rows in wave order
-            // (deterministic, independent of timing)
-            __syncthreads();
-            for (int k = tid + 1; k < NH; k += 64 * kXW) {
-                const int slot = (k == N) ? 0 : wfft::pad<LOG2N>(k);
-                double2 acc = racc[k];
-#pragma unroll
-                for (int w = 0; w < kXW; ++w) acc = cadd(acc, lds[w * SL + slot]);
-                racc[k] = acc;
-            }
-            __syncthreads();
-        }
-    }
-    if constexpr (GUESS) {
-        if (lane == 0) {
-            tail[2 * wave] = wsum;
-            tail[2 * wave + 1] = wcnt;
+        } else {
+            for (int k = lane; k < SLW; k += 64) buf[k] = cmk(0.0, 0.0);
         }
         __syncthreads();
-        const int64_t base = ((int64_t)s * a.nblk + cb) * NH;
-        for (int k = tid; k < NH; k += 64 * kXW) a.gR[base + k] = racc[k];
-        if (tid == 0) {
-            double ws = 0.0, wc = 0.0;
-            for (int w = 0; w < kXW; ++w) { ws += tail[2 * w]; wc += tail[2 * w + 1]; }
-            a.gw[((int64_t)s * a.nblk + cb) * 2 + 0] = ws;
-            a.gw[((int64_t)s * a.nblk + cb) * 2 + 1] = wc;
+
+        // folded moments of the XW rows over this wave's harmonic range
+        f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0;
+#pragma unroll 4
+        for (int t = 0; t < KPW / 4; ++t) {
+            const int k = k0 + 4 * t + kk;
+            const int se = wfft::pad<LOG2N>(k);
+            const int so = k == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(N - k);
+            const double bv = btab[t * 64];
+            if constexpr (XW == 8) {
+                d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * se], bv, d0, 0, 0, 0);
+                d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * so], bv, d1, 0, 0, 0);
+            } else {
+                d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * (aset ? so : se)], bv, d0, 0, 0,
+                                                          0);
+            }
         }
+        // output element tid: channel oc, moment om = 2 j + set, Re/Im ori;
+        // Y_{N/2} and 1/sigma~^2 of its channel read before the buffers
+        // take the partial tiles
+        const int oc = tid >> 6, om = (tid >> 1) & 31, ori = tid & 1;
+        double v = 0.0;
+        if (om == 0) v = reinterpret_cast<const double *>(lds + oc * SLW + SIDE)[ori];
+        const double ie = reinterpret_cast<const double *>(lds + oc * SLW + SIDE2)[0];
+        __syncthreads();
+        {
+            double *sc = reinterpret_cast<double *>(buf);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                sc[rr * 64 + lane] = d0[rr];
+                if constexpr (XW == 8) sc[256 + rr * 64 + lane] = d1[rr];
+            }
+        }
+        __syncthreads();
+        {
+            int idx;
+            if constexpr (XW == 8) {
+                const int row = 2 * oc + ori;
+                idx = (om & 1) * 256 + (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
+            } else {
+                const int row = 4 * oc + 2 * (om & 1) + ori;
+                idx = (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
+            }
+#pragma unroll
+            for (int w2 = 0; w2 < XW; ++w2) v += reinterpret_cast<const double *>(lds + w2 * SLW)[idx];
+            const int nc = cbase + r * XW + oc;
+            if (nc < cend) mom[((int64_t)nc * kMoments + om) * 2 + ori] = v * ie;
+        }
+        __syncthreads();
     }
+}
+
+// folded-moment B table: Bt[k][j] = (u_k^2)^j, u_k = (k - N/2)/(N/2), k < N/2
+__global__ void k_btab(int N, double *Bt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N / 2 * 16) return;
+    const int k = i >> 4, j = i & 15;
+    const double u = (double)(k - N / 2) * (2.0 / (double)N);
+    const double v = u * u, v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+    Bt[i] = ((j & 1) ? v : 1.0) * ((j & 2) ? v2 : 1.0) * ((j & 4) ? v4 : 1.0) * ((j & 8) ? v8 : 1.0);
+}
+
+// per model row: sum_{k>=1} |M_nk|^2 (the tau = 0 S_n numerator)
+__global__ void k_model_pow(const double2 *Mft, int nrows, int nharm, double *out) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (row >= nrows) return;
+    const double2 *M = Mft + (int64_t)row * nharm;
+    double acc = 0.0;
+    for (int k = lane + 1; k < nharm; k += 64) acc += cabs2(M[k]);
+    acc = wave_sum(acc);
+    if (lane == 0) out[row] = acc;
 }
 
 // sum_n M[model][n][k] over all channels, fixed order (mean model spectrum of
@@ -270,14 +427,14 @@ __global__ void k_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel
     out[(int64_t)m * nharm + k] = acc;
 }
 
+// ===========================================================================
+// launchers
+// ===========================================================================
 template <int L2, int DT>
 static void launch_w(const XspecArgs &a, hipStream_t st) {
-    constexpr int N = 1 << L2;
-    const size_t lds = ((size_t)kXW * wfft::buf_slots<L2>() + (a.guess ? N + 1 + kXW : 0)) *
-                       sizeof(double2);
+    const size_t lds = (size_t)kXW * wfft::buf_slots<L2>() * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kXW);
-    if (a.guess) hipLaunchKernelGGL((k_xspec_w<L2, DT, true>), g, b, lds, st, a);
-    else hipLaunchKernelGGL((k_xspec_w<L2, DT, false>), g, b, lds, st, a);
+    hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
 }
 
 bool xspec_wave_supported(int log2N, int cb) {
@@ -296,6 +453,47 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {
         case 21: launch_w<10, 1>(a, st); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+template <int L2, int DT, int XW>
+static void launch_xm(const XmomArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)XW * xmom_slw<L2, XW>() * sizeof(double2);
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * XW);
+    hipLaunchKernelGGL((k_xmom_w<L2, DT, XW>), g, b, lds, st, a);
+}
+template <int L2, int DT>
+static void launch_xm2(const XmomArgs &a, hipStream_t st) {
+    static const int xw = getenv("PPF_XMOM_WAVES") ? atoi(getenv("PPF_XMOM_WAVES")) : 8;
+    if (xw == 4) launch_xm<L2, DT, 4>(a, st);
+    else launch_xm<L2, DT, 8>(a, st);
+}
+
+hipError_t launch_btab(int N, double *Bt, hipStream_t st) {
+    hipLaunchKernelGGL(k_btab, dim3((unsigned)((N / 2 * 16 + 255) / 256)), dim3(256), 0, st, N, Bt);
+    return hipGetLastError();
+}
+
+hipError_t launch_xmom(const XmomArgs &a, hipStream_t st) {
+    switch (a.log2N * 2 + a.dtype) {
+        case 14: launch_xm2<7, 0>(a, st); break;
+        case 15: launch_xm2<7, 1>(a, st); break;
+        case 16: launch_xm2<8, 0>(a, st); break;
+        case 17: launch_xm2<8, 1>(a, st); break;
+        case 18: launch_xm2<9, 0>(a, st); break;
+        case 19: launch_xm2<9, 1>(a, st); break;
+        case 20: launch_xm2<10, 0>(a, st); break;
+        case 21: launch_xm2<10, 1>(a, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_model_pow(const double2 *Mft, int nchan, int nharm, int nmodel, double *out,
+                            hipStream_t st) {
+    const int nrows = nchan * nmodel;
+    hipLaunchKernelGGL(k_model_pow, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, Mft, nrows,
+                       nharm, out);
     return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
-    L.cbd = d->nchan < 64 ? d->nchan : 64;            // k_dsum channel block
+    L.cbd = d->nchan < 128 ? d->nchan : 128;          // k_dsum channel block
     L.nblkd = (d->nchan + L.cbd - 1) / L.cbd;
     size_t o = 0;
     L.M = o;     o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);

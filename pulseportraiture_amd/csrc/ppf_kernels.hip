@@ -333,6 +333,107 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
 }
 
 // ===========================================================================
+// k_dsum_w: k_dsum with one wave per channel row (256 <= nbin <= 2048).
+// Each wave streams its rows (channels c0 + wave + 4 i) with 16-B loads, one
+// row in flight ahead of the one being summed, stages the row in its own LDS
+// slice and accumulates the shifted, interpolated row into nbin/64 register
+// accumulators per lane (output bin t = lane + 64 j); no workgroup barrier in
+// the row loop.  The four waves' sums are added in wave order through LDS
+// (deterministic) and the block's partial profile is written once.
+// ===========================================================================
+template <int DT, int LOG2NB>
+__global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
+    using ElT = typename std::conditional<DT == 0, float, double>::type;
+    // native vector types: arrays of HIP_vector_type structs carried across
+    // the row loop are not promoted to VGPRs (they land in scratch)
+    typedef float vf4 __attribute__((ext_vector_type(4)));
+    typedef double vd2 __attribute__((ext_vector_type(2)));
+    using VecT = typename std::conditional<DT == 0, vf4, vd2>::type;
+    constexpr int NB = 1 << LOG2NB, J = NB / 64, VW = 16 / (int)sizeof(ElT);
+    constexpr int NL = NB / (64 * VW);                 // 16-B loads per lane per row
+    extern __shared__ __attribute__((aligned(16))) double dlds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    ElT *xs = reinterpret_cast<ElT *>(dlds) + wave * NB;
+    const int s = blockIdx.x / a.nblkd, blk = blockIdx.x % a.nblkd;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    const double *gwt = a.guess_weights + (int64_t)s * a.nchan;
+    double v0 = 0.0, v1 = 0.0;
+    for (int n = lane; n < a.nchan; n += 64)
+        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    const double Dg = (double)NB * kDconst * a.guess_DM[s] / a.P[s];
+    const double mu = v0 / v1, nu_mean_m2 = 1.0 / (mu * mu);
+    const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
+    const VecT *rows = reinterpret_cast<const VecT *>(a.data) + (int64_t)s * a.nchan * (NB / VW);
+    double acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = 0.0;
+    double wsum = 0.0, wcnt = 0.0;
+    int n = c0 + wave;
+    while (n < c1 && mask && !mask[n]) n += kWaves;
+    VecT pre[NL];
+    {
+        const VecT *src = rows + (int64_t)min(n, c1 - 1) * (NB / VW);
+#pragma unroll
+        for (int i = 0; i < NL; ++i) pre[i] = src[lane + 64 * i];
+    }
+    while (n < c1) {
+        wave_lds_sync();                      // the previous row's reads are issued
+#pragma unroll
+        for (int i = 0; i < NL; ++i) reinterpret_cast<VecT *>(xs)[lane + 64 * i] = pre[i];
+        int nn = n + kWaves;
+        while (nn < c1 && mask && !mask[nn]) nn += kWaves;
+        {
+            // next row in flight during this one (unconditional load: keeps
+            // pre[] in VGPRs)
+            const VecT *src = rows + (int64_t)(nn < c1 ? nn : n) * (NB / VW);
+#pragma unroll
+            for (int i = 0; i < NL; ++i) pre[i] = src[lane + 64 * i];
+        }
+        const double w = gwt[n], f0 = fr[n];
+        const double tau = Dg * (1.0 / (f0 * f0) - nu_mean_m2);
+        const double fl = floor(tau), f = tau - fl;
+        const int i0 = (int)(fl - (double)NB * floor(fl / (double)NB));   // mod nbin
+        const double wa = w * (1.0 - f), wb = w * f;
+        wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int ia = (lane + 64 * j + i0) & (NB - 1);
+            acc[j] = fma(wa, (double)xs[ia], fma(wb, (double)xs[(ia + 1) & (NB - 1)], acc[j]));
+        }
+        wsum += w;
+        wcnt += 1.0;
+        n = nn;
+    }
+    // fixed-order sum of the four waves' profiles (LDS reused as NB doubles)
+    __syncthreads();
+    double *part = dlds;
+    for (int w2 = 0; w2 < kWaves; ++w2) {
+        if (wave == w2) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int t = lane + 64 * j;
+                part[t] = w2 == 0 ? acc[j] : part[t] + acc[j];
+            }
+        }
+        __syncthreads();
+    }
+    double *out = a.gP + ((int64_t)s * a.nblkd + blk) * NB;
+    for (int t = threadIdx.x; t < NB; t += kBlock) out[t] = part[t];
+    __shared__ double wred[kWaves * 2];
+    if (lane == 0) { wred[wave * 2] = wsum; wred[wave * 2 + 1] = wcnt; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int w2 = 0; w2 < kWaves; ++w2) { s0 += wred[w2 * 2]; s1 += wred[w2 * 2 + 1]; }
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 0] = s0;
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 1] = s1;
+    }
+}
+
+// ===========================================================================
 // k_guess: GetTOAs initial phase (pptoas.py:461-499): FFTFIT of the weighted,
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
@@ -625,7 +726,32 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
     }
     return hipGetLastError();
 }
+bool dsum_wave_supported(int nbin) { return nbin >= 256 && nbin <= 2048; }
+
+template <int DT, int L2>
+static void launch_dsum_w(const DsumArgs &a, hipStream_t st) {
+    constexpr int NB = 1 << L2;
+    const size_t row = (size_t)kWaves * NB * (DT == 0 ? 4 : 8);
+    const size_t lds = row > (size_t)NB * 8 ? row : (size_t)NB * 8;
+    hipLaunchKernelGGL((k_dsum_w<DT, L2>), dim3((unsigned)((int64_t)a.nsub * a.nblkd)), dim3(kBlock),
+                       lds, st, a);
+}
+
 hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
+    if (dsum_wave_supported(a.nbin)) {
+        switch (__builtin_ctz((unsigned)a.nbin) * 2 + a.dtype) {
+            case 16: launch_dsum_w<0, 8>(a, st); break;
+            case 17: launch_dsum_w<1, 8>(a, st); break;
+            case 18: launch_dsum_w<0, 9>(a, st); break;
+            case 19: launch_dsum_w<1, 9>(a, st); break;
+            case 20: launch_dsum_w<0, 10>(a, st); break;
+            case 21: launch_dsum_w<1, 10>(a, st); break;
+            case 22: launch_dsum_w<0, 11>(a, st); break;
+            case 23: launch_dsum_w<1, 11>(a, st); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     dim3 g((unsigned)((int64_t)a.nsub * a.nblkd)), b(kBlock);
     const int jb = a.nbin >= 2048 ? 8 : (a.nbin + kBlock - 1) / kBlock;
     if (a.dtype == 0) {

@@ -41,6 +41,10 @@ namespace ppf {
 
 constexpr int kXW = 8;                 // waves per k_xspec_w workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+// row elements as native vectors: arrays of HIP_vector_type structs carried
+// across the row loop are not promoted to VGPRs
+typedef float vf2 __attribute__((ext_vector_type(2)));
+typedef double vd2 __attribute__((ext_vector_type(2)));
 #ifndef PPF_SCHED_CUT
 #define PPF_SCHED_CUT 1
 #endif
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
     constexpr int SL = wfft::buf_slots<LOG2N>();      // padded wave buffer
-    using RowT = typename std::conditional<DT == 0, float2, double2>::type;
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double2 *buf = lds + wave * SL;
@@ -217,7 +221,7 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2))) vo
     constexpr int SIDE = SLW - 1;      // Y_{N/2}
     constexpr int SIDE2 = SLW - 2;     // 1/sigma~_n^2 of the row (.x)
     constexpr int KPW = N / 2 / XW;    // folded harmonics (MFMA K) per wave
-    using RowT = typename std::conditional<DT == 0, float2, double2>::type;
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double2 *buf = lds + wave * SLW;

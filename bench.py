@@ -151,36 +151,36 @@ def main():
     hist = np.zeros((ncalls, 4))
     got = lib.ppf_stage_ms_history(ctx, ncalls, hist.ctypes.data)
     stage_ms = hist[:got].sum(axis=0)
+    khist = np.zeros((ncalls, 2))
+    kgot = lib.ppf_kernel_ms_history(ctx, ncalls, khist.ctypes.data)
+    kern_ms = khist[:kgot].sum(axis=0)
     res_np = last.cpu().numpy()
     I = _lib.RESULT_INDEX
     nfev = res_np[:, I["nfeval"]]
     npass = res_np[:, I["npass"]]
     status = res_np[:, I["status"]].astype(int)
-    # algorithmic bytes per sub-integration
-    xspec_bytes = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
-    model_bytes = nchan * nbin * 8 + nchan * nharm * 16
-    solve_bytes_per_pass = nchan * nharm * 16 + nchan * 32 * 16   # X + moments
     steps_subints = count * args.steps
     mine = slice(first, first + count) if world > 1 else slice(None)
     mean_passes = float(npass[mine].mean())
     mean_nfev = float(nfev[mine].mean())
+    # ALGORITHMIC bytes per sub-integration:
+    #  k_xmom_g (first, full moment pass): read the f32 rows, the channel
+    #   derivatives dphi (2 f64); write 32 complex moments, the 4 channel
+    #   scalars and the centre residual per channel.  The model spectra
+    #   (nchan nharm 16 B) are read once per launch.
+    #  k_dsum_w: read the f32 rows; write the per-block guess profiles.
+    nblkd = (nchan + 127) // 128
+    xmom_unit = nchan * nbin * 4 + nchan * 16 + nchan * (32 * 16 + 4 * 8 + 8)
+    dsum_unit = nchan * nbin * 4 + nblkd * nbin * 8 + nblkd * 16
     kern = {
-        "xspec": dict(ms=stage_ms[1], unit=xspec_bytes,
-                      bytes=steps_subints * xspec_bytes +
-                      ncalls * nchan * nharm * 16),
-        "solve": dict(ms=stage_ms[3], unit=solve_bytes_per_pass,
-                      bytes=steps_subints * mean_passes *
-                      solve_bytes_per_pass),
-        "guess": dict(ms=stage_ms[2], unit=None, bytes=None),
-        "model_rfft": dict(ms=stage_ms[0], unit=model_bytes,
-                           bytes=ncalls * model_bytes),
+        "xmom": dict(name="k_xmom_g<%d, 0, true, true>" % (nbin // 4).bit_length(),
+                     ms=kern_ms[0], unit=xmom_unit,
+                     bytes=steps_subints * xmom_unit + ncalls * nchan * nharm * 16),
+        "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
+                     bytes=steps_subints * dsum_unit),
     }
     dom = max(kern, key=lambda k: kern[k]["ms"])
     dk = kern[dom]
-    if dk["bytes"] is None:
-        dom = "solve" if kern["solve"]["ms"] >= kern["xspec"]["ms"] else \
-            "xspec"
-        dk = kern[dom]
     achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
     # HBM traffic per launch from the PMC passes (profiles/pmc_reduce.py):
     # measured bytes per unit x the units one launch processes
@@ -188,20 +188,22 @@ def main():
     if os.path.exists(args.pmc):
         try:
             pm = json.load(open(args.pmc))["kernels"][dom]
-            traffic = round(pm["hbm_bytes"] * (dk["bytes"] / ncalls) /
-                            dk["unit"])
+            traffic = round(pm["hbm_bytes"] * (steps_subints / ncalls))
         except Exception:
             traffic = None
-    n_launch = ncalls
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                 unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                traffic=traffic, kernel="k_" + dom,
-                algorithmic_bytes_per_launch=dk["bytes"] / n_launch,
-                avg_launch_ms=dk["ms"] / n_launch)
-    stages = {k: dict(total_ms=round(v["ms"], 3),
-                      gbs=(None if not v["bytes"] or not v["ms"] else
-                           round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
-              for k, v in kern.items()}
+                traffic=traffic, kernel=dk["name"],
+                algorithmic_bytes_per_launch=dk["bytes"] / ncalls,
+                avg_launch_ms=round(dk["ms"] / ncalls, 4),
+                units_per_launch=steps_subints / ncalls)
+    names = ["model_rfft", "xspec", "guess", "solve"]
+    stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
+    kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),
+                       avg_launch_ms=round(float(v["ms"]) / ncalls, 4),
+                       gbs=(None if not v["ms"] else
+                            round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
+               for k, v in kern.items()}
     value = total * args.steps / dt
     out = dict(metric=METRIC, value=round(value, 2), unit="subint-fits/s",
                n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -214,7 +216,7 @@ def main():
                            (args.nsub, nchan, nbin), nsub_per_gpu=args.nsub,
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
                            fit="phase+DM", parallelism="dp%d" % world),
-               roofline=roof, stages=stages,
+               roofline=roof, stage_ms=stages, kernels=kernels,
                mean_passes_per_fit=round(mean_passes, 3),
                mean_evals_per_fit=round(mean_nfev, 3),
                fits_converged_frac=round(float(np.mean(

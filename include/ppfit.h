@@ -146,6 +146,11 @@ int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4);
  * oldest first, into ms[n][4]; returns the number written.  Events are kept
  * in a ring, so a timed loop records without synchronising. */
 int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms);
+/* Single-kernel times of the last n profiled ppf_fit_batch calls into
+ * ms[n][2]: [0] the first fused moment pass over the data (k_xmom_g, every
+ * moment-mode sub-int; 0 if the call had none), [1] the guess-profile pass
+ * (k_dsum_w; 0 without a guess).  Same event ring as ppf_stage_ms_history. */
+int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms);
 
 /* Workspace needed by ppf_fit_batch for `desc` (only sizes/flags are read). */
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc);

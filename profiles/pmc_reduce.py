@@ -7,10 +7,10 @@ per-unit HBM traffic (profiles/pmc_summary.json, read by bench.py).
 
 Counter handling follows MI355X_MICROARCH.md (HBM section): counters are in
 KiB; FETCH_SIZE counts half of the bytes of wide coalesced streaming reads on
-gfx950, so it is doubled; WRITE_SIZE is taken as is.  Units:
-  xspec  -- per sub-integration   (grid = nsub * nchan/32 workgroups of 256)
-  pass   -- per sub-integration pass (total over the k_pass<false,*> launches
-            of one ppf_fit_batch call / (nsub * mean passes per fit))
+gfx950, so it is doubled; WRITE_SIZE is taken as is.  Unit: one
+sub-integration; a launch processes `chunk` sub-integrations (bench config).
+  xmom -- the first (full) fused moment pass k_xmom_g<*, *, *, true>
+  dsum -- the guess-profile pass k_dsum_w
 """
 import argparse
 import collections
@@ -21,7 +21,8 @@ import os
 
 
 def load(d):
-    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
+                  recursive=True)[0]
     rows = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         rows[r["Kernel_Name"]].append(r)
@@ -32,17 +33,20 @@ def pick(rows, key):
     return [r for k, v in rows.items() if key in k for r in v]
 
 
+KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", "")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("bench_log")
-    ap.add_argument("--nchan", type=int, default=512)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(
         os.path.abspath(__file__)), "pmc_summary.json"))
     a = ap.parse_args()
     line = [l for l in open(a.bench_log) if l.startswith("{")][-1]
     bench = json.loads(line)
+    per_launch = min(bench["config"]["chunk"], bench["config"]["nsub_per_gpu"])
     fr, wr = load(a.fetch_dir), load(a.write_dir)
     KiB = 1024.0
     out = dict(source=dict(fetch=a.fetch_dir, write=a.write_dir,
@@ -50,27 +54,19 @@ def main():
                            correction="FETCH_SIZE x2 (gfx950 wide reads), "
                                       "WRITE_SIZE x1, KiB -> bytes"),
                kernels={})
-    # k_xspec: per sub-integration
-    xf, xw = pick(fr, "k_xspec"), pick(wr, "k_xspec")
-    nblk = (a.nchan + 31) // 32
-    nsub = sum(int(r["Grid_Size"]) for r in xf) / (256 * nblk)
-    fb = sum(float(r["Counter_Value"]) for r in xf) * KiB * 2 / nsub
-    wb = sum(float(r["Counter_Value"]) for r in xw) * KiB / nsub
-    out["kernels"]["xspec"] = dict(unit="sub-integration",
-                                   fetch_bytes=fb, write_bytes=wb,
-                                   hbm_bytes=fb + wb, launches=len(xf))
-    # k_pass<false, *>: per sub-integration pass
-    pf, pw = pick(fr, "k_pass<false"), pick(wr, "k_pass<false")
-    ncall = len(xf)
-    nsub_call = nsub / ncall
-    units = nsub * bench["mean_passes_per_fit"]
-    fb = sum(float(r["Counter_Value"]) for r in pf) * KiB * 2 / units
-    wb = sum(float(r["Counter_Value"]) for r in pw) * KiB / units
-    out["kernels"]["solve"] = dict(unit="sub-integration pass",
-                                   fetch_bytes=fb, write_bytes=wb,
-                                   hbm_bytes=fb + wb, launches=len(pf),
-                                   subints_per_call=nsub_call,
-                                   mean_passes=bench["mean_passes_per_fit"])
+    for key, (pre, post) in KERNELS.items():
+        sel = lambda rows: [r for k, v in rows.items()
+                            if pre in k and post in k for r in v]
+        f, w = sel(fr), sel(wr)
+        if not f or not w:
+            continue
+        fb = sum(float(r["Counter_Value"]) for r in f) * KiB * 2 / len(f)
+        wb = sum(float(r["Counter_Value"]) for r in w) * KiB / len(w)
+        out["kernels"][key] = dict(
+            unit="sub-integration", subints_per_launch=per_launch,
+            fetch_bytes=fb / per_launch, write_bytes=wb / per_launch,
+            hbm_bytes=(fb + wb) / per_launch, launches=len(f),
+            kernel=sorted({r["Kernel_Name"] for r in f}))
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -20,8 +20,11 @@ struct ppf_ctx {
     std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
     bool prof = false;
     static constexpr int kRing = 256;
-    hipEvent_t ring[kRing][5] = {};
-    bool ran[kRing][4] = {};
+    // [0..4]: stage boundaries; [5, 6]: the first moment pass (k_xmom_g,
+    // FULL); [7, 8]: the guess-profile pass (k_dsum_w)
+    static constexpr int kEv = 9;
+    hipEvent_t ring[kRing][kEv] = {};
+    bool ran[kRing][6] = {};
     long ncalls = 0;
     unsigned *host_active = nullptr;   // pinned, for the iteration loop
 };
@@ -74,7 +77,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, Mpow, needx, Bt, total;
+    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, needx, Bt, total;
     int nblk, cb, cbd, nblkd;
 };
 
@@ -99,6 +102,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.active = o; o += 256;
     L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
     L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
+    L.mres = o;  o += align256(sizeof(double) * nsub * 2 * nchan);
     L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.needx = o; o += align256(nsub);
     L.Bt = o;    o += align256(sizeof(double) * (nharm - 1) / 2 * 16);
@@ -202,6 +206,27 @@ int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms) {
     return n;
 }
 
+int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms) {
+    if (!ctx || !ms || n < 0) return PPF_EINVAL;
+    if (!ctx->prof) return fail(ctx, PPF_EINVAL, "profiling is off");
+    long avail = ctx->ncalls < ppf_ctx::kRing ? ctx->ncalls : ppf_ctx::kRing;
+    if (n > avail) n = (int)avail;
+    for (int c = 0; c < n; ++c) {
+        int slot = (int)((ctx->ncalls - n + c) % ppf_ctx::kRing);
+        hipError_t e = hipEventSynchronize(ctx->ring[slot][4]);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+        for (int i = 0; i < 2; ++i) {
+            float t = 0.f;
+            if (ctx->ran[slot][4 + i]) {
+                e = hipEventElapsedTime(&t, ctx->ring[slot][5 + 2 * i], ctx->ring[slot][6 + 2 * i]);
+                if (e != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+            }
+            ms[c * 2 + i] = (double)t;
+        }
+    }
+    return n;
+}
+
 int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4) {
     int n = ppf_stage_ms_history(ctx, 1, ms4);
     if (n < 0) return n;
@@ -236,6 +261,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     };
     for (int i = 0; i < 4; ++i) ctx->ran[slot][i] = true;
     ctx->ran[slot][2] = d->guess != 0;
+    ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
     ppf::RfftArgs ra{d->nbin, ilog2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
@@ -283,7 +309,10 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         da.freqs = d->freqs; da.P = d->P; da.guess_DM = d->guess_DM;
         da.guess_weights = d->guess_weights;
         da.gP = (double *)(ws + L.gP); da.gw = (double *)(ws + L.gw);
+        mark(7);
         if ((e = ppf::launch_dsum(da, st)) != hipSuccess) return hip_fail(ctx, e, "k_dsum");
+        mark(8);
+        ctx->ran[slot][5] = true;
         double2 *msum = (double2 *)(ws + L.Msum);
         if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
             return hip_fail(ctx, e, "k_model_sum");
@@ -319,6 +348,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.moments = use_moments;
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
+    sa.mres = (double *)(ws + L.mres);
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
     ppf::XmomArgs ma{};
@@ -328,7 +358,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ma.chan = xa.chan; ma.dphi = sa.dphi; ma.T = T; ma.T2 = T2; ma.state = sa.state;
     ma.mom = (double *)sa.mom;
     ma.Bt = (const double *)(ws + L.Bt);
-    ma.kc = kc; ma.errs = d->errs; ma.Mpow = Mpow;
+    ma.kc = kc; ma.errs = d->errs; ma.Mpow = Mpow; ma.mres = sa.mres; ma.nmodel = d->nmodel;
     if (fused && (e = ppf::launch_btab(d->nbin / 2, (double *)(ws + L.Bt), st)) != hipSuccess)
         return hip_fail(ctx, e, "k_btab");
     // trust-region iterations.  Scattering fits: each iteration = one
@@ -343,8 +373,14 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         for (int g = 0; g < group; ++g) {
             if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
             if (sa.moments) {
-                e = fused ? ppf::launch_xmom(ma, st) : ppf::launch_moments(sa, st);
+                const bool full = iter == 0 && g == 0;
+                if (full && fused) mark(5);
+                e = fused ? ppf::launch_xmom(ma, full, st) : ppf::launch_moments(sa, st);
                 if (e != hipSuccess) return hip_fail(ctx, e, fused ? "k_xmom" : "k_moments");
+                if (full && fused) {
+                    mark(6);
+                    ctx->ran[slot][4] = true;
+                }
             }
             if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");

@@ -44,7 +44,7 @@ struct DsumArgs {
 
 // k_xmom: fused re-FFT + cross spectrum + Taylor moments (no X in HBM)
 struct XmomArgs {
-    int nsub, nchan, nbin, log2N, nblk, cb, dtype, xcd_swizzle;
+    int nsub, nchan, nbin, log2N, nblk, cb, dtype, xcd_swizzle, nmodel;
     const void *data;
     const double2 *Mft;
     const int32_t *model_index;
@@ -58,6 +58,7 @@ struct XmomArgs {
     int kc;                      // get_noise_PS cut
     const double *errs;          // [nsub][nchan] or null
     const double *Mpow;          // [nmodel][nchan]
+    double *mres;                // [nsub][2][nchan] centre residual phi_c,n - s_n/nbin
 };
 
 struct GuessArgs {
@@ -99,6 +100,7 @@ struct SolveArgs {
     int moments;                 // 1: enabled
     double2 *mom;                // [nsub][2][nchan][kMoments]
     double *dphi;                // [nsub][nchan][2]: d phi_n / d(DM, GM)
+    double *mres;                // [nsub][2][nchan]: moment-centre residual per channel
 };
 
 struct RotateArgs {
@@ -145,7 +147,7 @@ hipError_t launch_guess(const GuessArgs &a, hipStream_t st);
 hipError_t launch_dsum(const DsumArgs &a, hipStream_t st);
 bool xspec_wave_supported(int log2N, int cb);
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);
-hipError_t launch_xmom(const XmomArgs &a, hipStream_t st);
+hipError_t launch_xmom(const XmomArgs &a, bool full, hipStream_t st);
 hipError_t launch_btab(int N, double *Bt, hipStream_t st);
 hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
                            int moments, uint8_t *needx, hipStream_t st);

@@ -533,12 +533,14 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
 //   sum_k Y_k e^{2 pi i k Delta} = e^{i x} sum_m (i x)^m / m! mu_m,
 //   mu_m = sum_k Y_k u_k^m,  and k = h (1 + u) gives the k- and k^2-weighted
 // sums (C', C'') from mu_m + mu_{m+1} and mu_m + 2 mu_{m+1} + mu_{m+2}.
-// kMoments = 32 moments and |x| <= 2.5 bound the truncation of the
-// second-derivative series by 2.5^30 / 30! < 4e-21 of sum_k |Y_k|, so every
+// kMoments = 32 moments and |x| <= 3.2 bound the truncation of the
+// second-derivative series by 3.2^30 / 30! < 6e-18 of sum_k |Y_k|, so every
 // trust-region evaluation inside that radius costs O(nchan) instead of a pass
 // over the cross spectrum; a point outside it re-centres (k_moments).
+// Delta_n includes the per-channel centre residual mres (k_xmom_g rounds the
+// centre to a whole bin, |residual| <= 1/(2 nbin), i.e. |x| <= pi/4).
 // ===========================================================================
-constexpr double kXMax = 2.5;
+constexpr double kXMax = 3.2;
 constexpr int kMomChans = 64;                    // channels per k_moments workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -564,6 +566,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
     if (valid) {
         const double *dp = a.dphi + ((int64_t)s * a.nchan + n) * 2;
         phin = c0 + c1 * dp[0] + c2 * dp[1];
+        if (kk == 0) a.mres[((int64_t)s * 2 + q) * a.nchan + n] = 0.0;   // exact centre
     }
     const double2 *Xr = a.X + ((int64_t)s * a.nchan + (valid ? n : 0)) * nharm;
     const double2 W4 = cexp2pi(4.0 * phin);
@@ -653,6 +656,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *chan = a.chan + (int64_t)s * a.nchan * 4;
     const double2 *MOM = a.mom + (int64_t)s * 2 * a.nchan * kMoments;
+    const double *MRES = a.mres + (int64_t)s * 2 * a.nchan;
     double *stats = a.stats + (int64_t)s * 2 * a.nchan * 10;
     const int flagmask = L.flagmask;
     if (lane == 0) L.need_mom = 0;
@@ -666,10 +670,11 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
             const int cand = t == 0 ? L.macc : 1 - L.macc;
             if (!L.mvalid[cand]) continue;
             const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
+            const double *rc = MRES + (int64_t)cand * a.nchan;
             double xm = 0.0;
             for (int n = lane; n < a.nchan; n += 64) {
                 if (mask && !mask[n]) continue;
-                xm = fmax(xm, fabs(e0 + e1 * dp[2 * n] + e2 * dp[2 * n + 1]));
+                xm = fmax(xm, fabs(e0 + e1 * dp[2 * n] + e2 * dp[2 * n + 1] + rc[n]));
             }
             xm = wave_max(xm);
             if (kTwoPi * h * xm <= kXMax) qsel = cand;
@@ -688,6 +693,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
         }
         const double e0 = t0 - L.mc[qsel][0], e1 = t1 - L.mc[qsel][1], e2 = t2 - L.mc[qsel][2];
         const double2 *Mq = MOM + (int64_t)qsel * a.nchan * kMoments;
+        const double *rq = MRES + (int64_t)qsel * a.nchan;
         double *st = stats + (int64_t)L.slot_eval * a.nchan * 10;
         double acc[10];
 #pragma unroll
@@ -695,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
         for (int n = lane; n < a.nchan; n += 64) {
             if (mask && !mask[n]) continue;
             const double d1 = dp[2 * n], d2 = dp[2 * n + 1];
-            const double del = e0 + e1 * d1 + e2 * d2;
+            const double del = e0 + e1 * d1 + e2 * d2 + rq[n];
             const double x = kTwoPi * h * del;
             double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
             taylor_acc<0>(Mq + (int64_t)n * kMoments, x, 1.0, 0.0, 0.0, G0, G1, G2);

@@ -9,10 +9,10 @@
 //   streams it (scattering fits, k_pass):
 //     get_noise_PS noise (pplib.py:2312-2332), Sd_n, S_n(tau = 0)
 //     X_k = D_k conj(M_k) / sigma~_n^2 (pptoaslib.py:1014-1031), k = 0 zeroed
-//   Sub-ints fitted from moments (TRState.mmode) are skipped: k_xmom_w
+//   Sub-ints fitted from moments (TRState.mmode) are skipped: k_xmom_g
 //   produces everything they need without X.
 //
-// k_xmom_w<LOG2N, DT, XW>: the fused moment pass (fits without scattering).
+// k_xmom_g<LOG2N, DT, SH>: the fused moment pass (fits without scattering).
 //   The cross spectrum never reaches HBM: for every sub-int that asks for a
 //   moment set (need_mom, centre mc[mtarget]) the workgroup re-reads its
 //   block of channel rows and per row forms the noise, Sd_n, S_n (chan[]) and
@@ -24,13 +24,13 @@
 //     mu_2j+1 = sum_{k<N/2} (Y_k - Y_{N-k}) u_k   (u_k^2)^j
 //   so both halves share one B tile (v_k^j, v = u^2, j < 16) and the MFMA
 //   K loop runs over N/2 harmonics.  A = 16 rows of v_mfma_f64_16x16x4f64
-//   from the XW wave buffers: XW = 8 -> 8 channels x {Re, Im}, one MFMA per
-//   half; XW = 4 -> 4 channels x {even, odd} x {Re, Im}, one MFMA.  Each
-//   wave takes 1/XW of the folded harmonics; the partial tiles are summed in
+//   from the 8 wave buffers: 8 sub-ints x {Re, Im}, one MFMA per half.  Each
+//   wave takes 1/8 of the folded harmonics; the partial tiles are summed in
 //   wave order through LDS (deterministic) and scaled by 1/sigma~_n^2.
 //   Output: mu[s][q][n][m] (k_tr_mom consumes it).  HBM traffic per sub-int:
 //   the data rows (nchan nbin s_in B) + the moments (nchan 32 16 B).
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "ppf_internal.hpp"
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
 }
 
 // ===========================================================================
-// k_xmom_w: fused moment pass (see the file header)
+// k_xmom_g: fused moment pass (see the file header and below)
 // ===========================================================================
 template <int LOG2N, int XW>
 __host__ __device__ constexpr int xmom_slw() {
@@ -212,121 +212,226 @@ __host__ __device__ constexpr int xmom_slw() {
     return (wfft::buf_slots<LOG2N>() < 272 ? 272 : wfft::buf_slots<LOG2N>()) + (XW == 8 ? 2 : 4);
 }
 
-template <int LOG2N, int DT, int XW>
-__global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2))) void k_xmom_w(XmomArgs a) {
+
+// ===========================================================================
+// k_xmom_g: the fused moment pass with the sub-int group layout.
+//   Block = (group of 8 sub-ints, block of a.cb <= 64 channels); wave w owns
+//   sub-int 8 g + w, and round r processes channel cb a.cb + r for all eight
+//   waves.  The round's model row M_n (and sum_k |M_nk|^2) is shared by the
+//   eight rows, so it is staged once in LDS instead of being re-read from L2
+//   by every row (SH = true: one model per batch).  With several models
+//   (SH = false) every wave reads its own model row from L2 with the same
+//   arithmetic, so a sub-int's moments do not depend on the batch it is in.
+//   The moment centre of each channel is rounded to a whole bin, s_n = rint(nbin phi_c,n) (bin_centre): the phasor e^{2 pi i k s_n /
+//   nbin} is then an exact circular shift of the time-domain row, applied by
+//   the load indices, and Y_k = D'_k conj(M_k) needs no phasor arithmetic;
+//   k_tr_mom adds the residual phi_c,n - s_n/nbin (mres) to every expansion
+//   offset.  MFMA A rows = 8 sub-ints x {Re, Im}; B = v_k^j computed in
+//   registers.
+//   Memory ordering: the only global loads inside the round loop are the
+//   prefetches for the NEXT round (model row first, then the data row), so no
+//   s_waitcnt inside a round waits for them (vmcnt is in order on gfx950):
+//   FFT twiddles live in LDS, and the per-channel inputs (dphi, errs, mask)
+//   are read once per block into lane registers and broadcast by readlane.
+// ===========================================================================
+#ifndef PPF_G_CUT
+#define PPF_G_CUT 1
+#endif
+#if PPF_G_CUT
+#define G_CUT() __builtin_amdgcn_sched_barrier(0)
+#else
+#define G_CUT()
+#endif
+__device__ __forceinline__ double bin_centre(double phc, int nbin) {
+    return rint(phc * (double)nbin);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// largest FFT twiddle index + 1 used by wfft stages >= 1
+template <int LOG2N>
+__host__ __device__ constexpr int tw_slots() {
     using P = wfft::Plan<LOG2N>;
+    return P::NST > 1 ? P::N / P::radix(P::NST - 1) : 1;
+}
+template <int LOG2N>
+__host__ __device__ constexpr size_t xmom_g_lds() {
+    return ((size_t)8 * xmom_slw<LOG2N, 8>() + (1 << LOG2N) + 2 + tw_slots<LOG2N>()) * sizeof(double2);
+}
+
+// FULL = true: the batch's first moment pass (every moment-mode sub-int);
+// false: re-centring passes for the few sub-ints that left the expansion
+// radius.  Same code; separate instantiations keep the two launch kinds
+// apart in kernel traces (the first pass is the one bench.py prices).
+template <int LOG2N, int DT, bool SH, bool FULL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_xmom_g(XmomArgs a) {
+    using P = wfft::Plan<LOG2N>;
+    constexpr int XW = 8;
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;
     constexpr int SLW = xmom_slw<LOG2N, XW>();
     constexpr int SIDE = SLW - 1;      // Y_{N/2}
     constexpr int SIDE2 = SLW - 2;     // 1/sigma~_n^2 of the row (.x)
     constexpr int KPW = N / 2 / XW;    // folded harmonics (MFMA K) per wave
+    constexpr int MPT = (NH + 511) / 512;   // model-row elements per thread
+    constexpr int TWN = tw_slots<LOG2N>();
+    using ElT = typename std::conditional<DT == 0, float, double>::type;
     using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double2 *buf = lds + wave * SLW;
+    double2 *mrow = lds + XW * SLW;    // model row M_n[0..N], [NH] = (sum |M|^2, 0)
+    double2 *tw = mrow + NH + 1;       // FFT twiddles T[0..TWN)
 
-    int s, cb;
-    block_map(a.xcd_swizzle, a.nblk, s, cb);
-    const TRState &S = reinterpret_cast<const TRState *>(a.state)[s];
-    if (!S.mmode || !S.need_mom) return;                 // uniform per workgroup
-    const int q = S.mtarget;
-    const double c0 = S.mc[q][0], c1 = S.mc[q][1], c2 = S.mc[q][2];
+    int g, cb;
+    block_map(a.xcd_swizzle, a.nblk, g, cb);
+    const int s = g * XW + wave;
+    const TRState *st = reinterpret_cast<const TRState *>(a.state);
+    const bool act = s < a.nsub && st[s].mmode && st[s].need_mom;
+    if (!__syncthreads_or(act)) return;                  // uniform per workgroup
+    const int q = act ? st[s].mtarget : 0;
+    const double c0 = act ? st[s].mc[q][0] : 0.0, c1 = act ? st[s].mc[q][1] : 0.0,
+                 c2 = act ? st[s].mc[q][2] : 0.0;
+    const int sv = act ? s : 0;
 
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
-    const int nround = (a.cb + XW - 1) / XW;
-    const int mi = a.model_index ? a.model_index[s] : 0;
-    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
+    const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)sv * a.nchan * (2 * N);
+    const double2 *Mbase = a.Mft;
+    // SH = false: this wave's own model (rows [nchan][NH], powers [nchan])
+    const int mi = (!SH && a.model_index) ? a.model_index[sv] : 0;
+    const double2 *Mwave = a.Mft + (int64_t)mi * a.nchan * NH;
+    const double *Pwave = a.Mpow + (int64_t)mi * a.nchan;
+    double *mres = a.mres + ((int64_t)sv * 2 + q) * a.nchan;
     const double2 w_seed = a.T2[lane], w_step = a.T2[64];
     const double sqrtN = sqrt((double)N);
-    double *mom = a.mom + (((int64_t)s * 2 + q) * a.nchan) * kMoments * 2;
+    double *mom = a.mom + (((int64_t)sv * 2 + q) * a.nchan) * kMoments * 2;
 
-    // MFMA operand roles (v_mfma_f64_16x16x4f64: A row = lane & 15, B col =
-    // lane & 15, K index = lane >> 4); B = v_k^col from the table Bt
-    const int arow = lane & 15, kk = lane >> 4;
-    const int ach = XW == 8 ? arow >> 1 : arow >> 2;
-    const int aset = XW == 8 ? 0 : (arow >> 1) & 1;
-    const double *abase = reinterpret_cast<const double *>(lds + ach * SLW) + (arow & 1);
+    // per-lane channel tables: lane l holds channel cbase + l
+    double ch_d0 = 0.0, ch_d1 = 0.0, ch_e = 0.0;
+    int ch_use = 0;
+    if (act && lane < cend - cbase) {
+        const int64_t row = (int64_t)sv * a.nchan + cbase + lane;
+        ch_d0 = a.dphi[row * 2];
+        ch_d1 = a.dphi[row * 2 + 1];
+        if (a.errs) ch_e = a.errs[row];
+        ch_use = (!a.mask || a.mask[row]) ? 1 : 0;
+    }
+
+    const int arow = lane & 15, kk = lane >> 4, bj = lane & 15;
+    const double *abase = reinterpret_cast<const double *>(lds + (arow >> 1) * SLW) + (arow & 1);
     constexpr double ih = 2.0 / (double)N;
     const int k0 = wave * KPW;
-    const double *btab = a.Bt + (int64_t)(k0 + kk) * 16 + (lane & 15);
 
-    auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
-    RowT zr[R];
-    double nx_d0 = 0.0, nx_d1 = 0.0, nx_e = 0.0;         // next row's scalars
-    auto fetch = [&](int n) {
-        const int64_t row = (int64_t)s * a.nchan + n;
-        const RowT *src = rows + row * N;
+    vd2 mp[MPT];
+    double mpw = 0.0;
+    auto mload = [&](int n) {
+        if constexpr (!SH) return;
+        const int nn = min(n, a.nchan - 1);
+        const double2 *src = Mbase + (int64_t)nn * NH;
 #pragma unroll
-        for (int qq = 0; qq < R; ++qq) zr[qq] = src[lane + 64 * qq];
-        nx_d0 = a.dphi[row * 2];
-        nx_d1 = a.dphi[row * 2 + 1];
-        if (a.errs) nx_e = a.errs[row];
-    };
-    int n = cbase + wave;
-    if (usable(n)) fetch(n);
-    for (int r = 0; r < nround; ++r, n += XW) {
-        const bool live = usable(n);
-        if (n < cend && !live) {
-            if (lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
-            if (usable(n + XW)) fetch(n + XW);
+        for (int i = 0; i < MPT; ++i) {
+            const int k = tid + 512 * i;
+            const double2 v = src[k < NH ? k : 0];
+            mp[i] = vd2{v.x, v.y};
         }
+        if (tid == 0) mpw = a.Mpow[nn];
+    };
+    auto mstore = [&]() {
+        if constexpr (!SH) return;
+#pragma unroll
+        for (int i = 0; i < MPT; ++i) {
+            const int k = tid + 512 * i;
+            if (k < NH) mrow[k] = cmk(mp[i][0], mp[i][1]);
+        }
+        if (tid == 0) mrow[NH] = cmk(mpw, 0.0);
+    };
+    // shifted row: z_j = x[(2j + sh) mod 2N] + i x[(2j + 1 + sh) mod 2N]
+    RowT zr[R];
+    double nx_r = 0.0;
+    auto fetch = [&](int n) {
+        const int r = n - cbase;
+        const double phc = c0 + c1 * readlane_d(ch_d0, r) + c2 * readlane_d(ch_d1, r);
+        const double sb = bin_centre(phc, 2 * N);
+        const int sh = (int)(sb - (double)(2 * N) * floor(sb / (double)(2 * N)));
+        nx_r = phc - sb / (double)(2 * N);          // residual centre offset
+        const ElT *x = rows + (int64_t)n * (2 * N);
+#pragma unroll
+        for (int qq = 0; qq < R; ++qq) {
+            const int j2 = 2 * (lane + 64 * qq) + sh;
+            zr[qq] = RowT{x[j2 & (2 * N - 1)], x[(j2 + 1) & (2 * N - 1)]};
+        }
+    };
+    auto usable = [&](int n) {
+        return act && n < cend && __builtin_amdgcn_readlane(ch_use, n - cbase) != 0;
+    };
+
+    for (int i = tid; i < TWN; i += 512) tw[i] = a.T[i];
+    int n = cbase;
+    mload(n);
+    mstore();
+    if (act) fetch(n);
+    __syncthreads();
+    for (; n < cend; ++n) {
+        const bool live = usable(n);
+        const double res_in = nx_r;
+        const double errs_in = a.errs ? readlane_d(ch_e, n - cbase) : 0.0;
+        double2 x[R];
+#pragma unroll
+        for (int qq = 0; qq < R; ++qq) x[qq] = cmk((double)zr[qq][0], (double)zr[qq][1]);
+        // next round's model row, then its data row, in flight during this
+        // round (the data load is unconditional for active waves: keeps zr[]
+        // in VGPRs)
+        mload(n + 1);
+        if (act) fetch(n + 1 < cend ? n + 1 : n);
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
-            double2 x[R];
-#pragma unroll
-            for (int qq = 0; qq < R; ++qq) x[qq] = cmk((double)zr[qq].x, (double)zr[qq].y);
-            const double phc = c0 + c1 * nx_d0 + c2 * nx_d1, errs_in = nx_e;
-            if (usable(n + XW)) fetch(n + XW);
-            wfft::fft_row<LOG2N>(x, buf, a.T, lane);
-
-            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-            __builtin_amdgcn_sched_barrier(0);
-            double2 E = cexp2pi((double)lane * phc);
-            __builtin_amdgcn_sched_barrier(0);
-            const double2 W = cexp2pi(64.0 * phc);
-            double2 Em = W;          // e^{2 pi i (N/2) phc} = W^(N/128)
-#pragma unroll
-            for (int t = 128; t < N; t <<= 1) Em = cmul(Em, Em);
-            const double2 EN = cmul(Em, Em);
-            __builtin_amdgcn_sched_barrier(0);
+#ifndef G_NOFFT
+            wfft::fft_row<LOG2N>(x, buf, tw, lane);
+#else
+            for (int qq = 0; qq < R; ++qq) buf[wfft::pad<LOG2N>(lane + 64 * qq)] = x[qq];
+#endif
             double2 Dm = cmk(0.0, 0.0);
             if (lane == 0) {
                 const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
                 Dm = cmk(zm.x, -zm.y);
             }
             // in place: iteration i reads and rewrites only pad(k) and
-            // pad(N - k), k = lane + 64 i: S_k -> pad(k), (Y_k - Y_{N-k}) u_k
-            // -> pad(N - k) (k = 0: -> pad(N/2), read above as Dm).  The
-            // power sums of the noise / Sd ride along.
+            // pad(N - k), k = lane + 64 i (k = 0: the pair (0, N) -> pad(0),
+            // pad(N/2), read above as Dm)
             double pn = 0.0, pd = 0.0;
+            auto pair = [&](const double2 *Mr, int i, double2 &w) {
+                    const int klo = lane + 64 * i, khi = N - klo;
+                    double2 Dlo, Dhi;
+                    rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                    w = cmul(w, w_step);
+                    const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                    if (klo >= a.kc) pn += p0;
+                    if (khi >= a.kc) pn += p1;
+                    if (klo >= 1) pd += p0;
+                    pd += p1;
+                    const double2 Ylo = klo == 0 ? cmk(0.0, 0.0) : cmulc(Dlo, Mr[klo]);
+                    const double2 Yhi = cmulc(Dhi, Mr[khi]);
+                    const double uk = (double)(klo - N / 2) * ih;
+                    buf[wfft::pad<LOG2N>(klo)] = cadd(Ylo, Yhi);
+                    buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
+                        cscale(csub(Ylo, Yhi), uk);
+            };
+            const double2 *Mr = SH ? mrow : Mwave + (int64_t)n * NH;
             double2 w = w_seed;
 #pragma unroll
             for (int i = 0; i < NP; ++i) {
-                const int klo = lane + 64 * i, khi = N - klo;
-                double2 Dlo, Dhi;
-                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
-                w = cmul(w, w_step);
-                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
-                if (klo >= a.kc) pn += p0;
-                if (khi >= a.kc) pn += p1;
-                if (klo >= 1) pd += p0;
-                pd += p1;
-                const double2 Ylo = klo == 0 ? cmk(0.0, 0.0) : cmul(cmulc(Dlo, Mrow[klo]), E);
-                const double2 Yhi = cmul(cmulc(Dhi, Mrow[khi]), cmul(EN, cconj(E)));
-                const double uk = (double)(klo - N / 2) * ih;
-                buf[wfft::pad<LOG2N>(klo)] = cadd(Ylo, Yhi);
-                buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
-                    cscale(csub(Ylo, Yhi), uk);
-                E = cmul(E, W);
-                XM_CUT();
+                pair(Mr, i, w);
+                G_CUT();
             }
+            if (lane == 0) buf[SIDE] = cmulc(Dm, Mr[N / 2]);
+            const double mpow = SH ? mrow[NH].x : Pwave[n];
             if (lane == 0) {
                 const double p = cabs2(Dm);
                 if (N / 2 >= a.kc) pn += p;
                 pd += p;
-                buf[SIDE] = cmul(cmulc(Dm, Mrow[N / 2]), Em);
             }
             pn = wave_sum(pn);
             pd = wave_sum(pd);
@@ -338,60 +443,54 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2))) vo
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
-                chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+                chan[2] = pd * inv_e2;        // Sd_n
+                chan[3] = mpow * inv_e2;      // S_n at tau = 0
+                mres[n] = res_in;
             }
-        } else {
-            for (int k = lane; k < SLW; k += 64) buf[k] = cmk(0.0, 0.0);
+        } else if (act && n < cend && lane < 4) {
+            a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;    // masked channel
         }
         __syncthreads();
+        mstore();                         // this round no longer reads mrow
 
-        // folded moments of the XW rows over this wave's harmonic range
         f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0;
+#ifndef G_NOMFMA
 #pragma unroll 4
         for (int t = 0; t < KPW / 4; ++t) {
             const int k = k0 + 4 * t + kk;
             const int se = wfft::pad<LOG2N>(k);
             const int so = k == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(N - k);
-            const double bv = btab[t * 64];
-            if constexpr (XW == 8) {
-                d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * se], bv, d0, 0, 0, 0);
-                d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * so], bv, d1, 0, 0, 0);
-            } else {
-                d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * (aset ? so : se)], bv, d0, 0, 0,
-                                                          0);
-            }
+            // B[k][j] = v_k^j, v = u_k^2 (same arithmetic as k_btab)
+            const double u = (double)(k - N / 2) * ih;
+            const double v = u * u, v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+            const double bv = ((bj & 1) ? v : 1.0) * ((bj & 2) ? v2 : 1.0) * ((bj & 4) ? v4 : 1.0) *
+                              ((bj & 8) ? v8 : 1.0);
+            d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * se], bv, d0, 0, 0, 0);
+            d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * so], bv, d1, 0, 0, 0);
         }
-        // output element tid: channel oc, moment om = 2 j + set, Re/Im ori;
-        // Y_{N/2} and 1/sigma~^2 of its channel read before the buffers
-        // take the partial tiles
-        const int oc = tid >> 6, om = (tid >> 1) & 31, ori = tid & 1;
-        double v = 0.0;
-        if (om == 0) v = reinterpret_cast<const double *>(lds + oc * SLW + SIDE)[ori];
-        const double ie = reinterpret_cast<const double *>(lds + oc * SLW + SIDE2)[0];
+#endif
+        // output element tid: this wave's sub-int, moment om = 2 j + set,
+        // Re/Im ori
+        const int om = (tid >> 1) & 31, ori = tid & 1;
+        double val = 0.0;
+        if (om == 0) val = reinterpret_cast<const double *>(buf + SIDE)[ori];
+        const double ie = reinterpret_cast<const double *>(buf + SIDE2)[0];
         __syncthreads();
         {
             double *sc = reinterpret_cast<double *>(buf);
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 sc[rr * 64 + lane] = d0[rr];
-                if constexpr (XW == 8) sc[256 + rr * 64 + lane] = d1[rr];
+                sc[256 + rr * 64 + lane] = d1[rr];
             }
         }
         __syncthreads();
         {
-            int idx;
-            if constexpr (XW == 8) {
-                const int row = 2 * oc + ori;
-                idx = (om & 1) * 256 + (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
-            } else {
-                const int row = 4 * oc + 2 * (om & 1) + ori;
-                idx = (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
-            }
+            const int row = 2 * wave + ori;
+            const int idx = (om & 1) * 256 + (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
 #pragma unroll
-            for (int w2 = 0; w2 < XW; ++w2) v += reinterpret_cast<const double *>(lds + w2 * SLW)[idx];
-            const int nc = cbase + r * XW + oc;
-            if (nc < cend) mom[((int64_t)nc * kMoments + om) * 2 + ori] = v * ie;
+            for (int w2 = 0; w2 < XW; ++w2) val += reinterpret_cast<const double *>(lds + w2 * SLW)[idx];
+            if (live) mom[((int64_t)n * kMoments + om) * 2 + ori] = val * ie;
         }
         __syncthreads();
     }
@@ -460,34 +559,35 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int L2, int DT, int XW>
-static void launch_xm(const XmomArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)XW * xmom_slw<L2, XW>() * sizeof(double2);
-    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * XW);
-    hipLaunchKernelGGL((k_xmom_w<L2, DT, XW>), g, b, lds, st, a);
-}
-template <int L2, int DT>
-static void launch_xm2(const XmomArgs &a, hipStream_t st) {
-    static const int xw = getenv("PPF_XMOM_WAVES") ? atoi(getenv("PPF_XMOM_WAVES")) : 8;
-    if (xw == 4) launch_xm<L2, DT, 4>(a, st);
-    else launch_xm<L2, DT, 8>(a, st);
-}
-
 hipError_t launch_btab(int N, double *Bt, hipStream_t st) {
     hipLaunchKernelGGL(k_btab, dim3((unsigned)((N / 2 * 16 + 255) / 256)), dim3(256), 0, st, N, Bt);
     return hipGetLastError();
 }
 
-hipError_t launch_xmom(const XmomArgs &a, hipStream_t st) {
+template <int L2, int DT>
+static void launch_xg(const XmomArgs &a, bool full, hipStream_t st) {
+    const size_t lds = xmom_g_lds<L2>();
+    static_assert(xmom_g_lds<10>() <= 163840, "k_xmom_g LDS");
+    dim3 g((unsigned)((int64_t)((a.nsub + 7) / 8) * a.nblk)), b(512);
+    if (a.nmodel == 1) {
+        if (full) hipLaunchKernelGGL((k_xmom_g<L2, DT, true, true>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_xmom_g<L2, DT, true, false>), g, b, lds, st, a);
+    } else {
+        if (full) hipLaunchKernelGGL((k_xmom_g<L2, DT, false, true>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_xmom_g<L2, DT, false, false>), g, b, lds, st, a);
+    }
+}
+
+hipError_t launch_xmom(const XmomArgs &a, bool full, hipStream_t st) {
     switch (a.log2N * 2 + a.dtype) {
-        case 14: launch_xm2<7, 0>(a, st); break;
-        case 15: launch_xm2<7, 1>(a, st); break;
-        case 16: launch_xm2<8, 0>(a, st); break;
-        case 17: launch_xm2<8, 1>(a, st); break;
-        case 18: launch_xm2<9, 0>(a, st); break;
-        case 19: launch_xm2<9, 1>(a, st); break;
-        case 20: launch_xm2<10, 0>(a, st); break;
-        case 21: launch_xm2<10, 1>(a, st); break;
+        case 14: launch_xg<7, 0>(a, full, st); break;
+        case 15: launch_xg<7, 1>(a, full, st); break;
+        case 16: launch_xg<8, 0>(a, full, st); break;
+        case 17: launch_xg<8, 1>(a, full, st); break;
+        case 18: launch_xg<9, 0>(a, full, st); break;
+        case 19: launch_xg<9, 1>(a, full, st); break;
+        case 20: launch_xg<10, 0>(a, full, st); break;
+        case 21: launch_xg<10, 1>(a, full, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -50,17 +50,62 @@ __device__ __forceinline__ double2 cexp2pi(double t) {
 // ---------------------------------------------------------------------------
 // reductions (fixed order -> bitwise reproducible)
 // ---------------------------------------------------------------------------
+// DPP move of a double (two 32-bit halves); lanes outside row_mask keep 0
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane63_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// Wave reductions on the DPP network (no LDS round trips): quad xor 1, xor
+// 2, half-row mirror, row mirror (every lane of a row then holds the row
+// total, bit-identically), then row_bcast15 / row_bcast31 fold rows 0+1 and
+// 2+3 and the pairs into lane 63, read back as a wave-uniform value.  Fixed
+// order: ((r3 + r2) + (r1 + r0)).  Needs all 64 lanes active.
+template <typename Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+    v = op(v, dpp_d<0xB1, 0xf>(v));     // quad_perm [1,0,3,2]
+    v = op(v, dpp_d<0x4E, 0xf>(v));     // quad_perm [2,3,0,1]
+    v = op(v, dpp_d<0x141, 0xf>(v));    // row_half_mirror
+    v = op(v, dpp_d<0x140, 0xf>(v));    // row_mirror
+    {
+        const double t = dpp_d<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+        const int r = (threadIdx.x >> 4) & 3;
+        if (r & 1) v = op(v, t);
+    }
+    {
+        const double t = dpp_d<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
+        if ((threadIdx.x & 63) >= 32) v = op(v, t);
+    }
+    return readlane63_d(v);
+}
+#ifdef PPF_SHFL_REDUCE
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
-
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
     return v;
 }
+#else
+__device__ __forceinline__ double wave_sum(double v) {
+    return wave_reduce(v, [](double x, double y) { return x + y; });
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+    return wave_reduce(v, [](double x, double y) { return fmax(x, y); });
+}
+#endif
 
 // wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
 // operations are processed in issue order; this keeps the compiler from
@@ -73,6 +118,26 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Sum K values per thread over the whole block; result valid in every thread.
 // scratch must hold kWaves*K doubles.  Contains two __syncthreads().
+// Max of K values per thread over the block (same contract as block_sum).
+template <int K>
+__device__ __forceinline__ void block_max(double (&v)[K], double *scratch) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < K; ++i) v[i] = wave_max(v[i]);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) scratch[wave * K + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double s = scratch[i];
+        for (int w = 1; w < kWaves; ++w) s = fmax(s, scratch[w * K + i]);
+        v[i] = s;
+    }
+    __syncthreads();
+}
+
 template <int K>
 __device__ __forceinline__ void block_sum(double (&v)[K], double *scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -266,73 +331,96 @@ struct TRModel {
     double H[5][5];
 };
 
-__device__ __forceinline__ double dotn(const double *a, const double *b, int n) {
+// The subspace dimension N (number of fitted parameters) is a template
+// argument: every loop unrolls and the vectors stay in registers (a runtime
+// bound made them scratch arrays, one memory round trip per element access
+// on the solver's serial path).
+template <int N>
+__device__ __forceinline__ double dotn(const double *a, const double *b) {
     double s = 0.0;
-    for (int i = 0; i < n; ++i) s += a[i] * b[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) s += a[i] * b[i];
     return s;
 }
-__device__ __forceinline__ void hessp(const TRModel &m, const double *p, double *out, int n) {
-    for (int i = 0; i < n; ++i) {
+template <int N>
+__device__ __forceinline__ void hessp(const TRModel &m, const double *p, double *out) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
         double s = 0.0;
-        for (int j = 0; j < n; ++j) s += m.H[i][j] * p[j];
+#pragma unroll
+        for (int j = 0; j < N; ++j) s += m.H[i][j] * p[j];
         out[i] = s;
     }
 }
-__device__ __forceinline__ double model_value(const TRModel &m, const double *p, int n) {
+template <int N>
+__device__ __forceinline__ double model_value(const TRModel &m, const double *p) {
     double Hp[5];
-    hessp(m, p, Hp, n);
-    return m.f + dotn(m.g, p, n) + 0.5 * dotn(p, Hp, n);
+    hessp<N>(m, p, Hp);
+    return m.f + dotn<N>(m.g, p) + 0.5 * dotn<N>(p, Hp);
 }
 // || z + t d || == R  ->  (ta, tb) sorted
-__device__ __forceinline__ void boundary_t(const double *z, const double *d, double R, int n,
-                                           double &ta, double &tb) {
-    double a = dotn(d, d, n), b = 2.0 * dotn(z, d, n), c = dotn(z, z, n) - R * R;
+template <int N>
+__device__ __forceinline__ void boundary_t(const double *z, const double *d, double R, double &ta,
+                                           double &tb) {
+    double a = dotn<N>(d, d), b = 2.0 * dotn<N>(z, d), c = dotn<N>(z, z) - R * R;
     double sq = sqrt(b * b - 4.0 * a * c);
     double aux = b + copysign(sq, b);
     double t1 = -aux / (2.0 * a), t2 = -2.0 * c / aux;
     ta = fmin(t1, t2);
     tb = fmax(t1, t2);
 }
-// Returns hits_boundary; p (length n) is the step.
-__device__ bool cg_steihaug(const TRModel &m, double jac_mag, double R, double *p, int n) {
+// Returns hits_boundary; p (length N) is the step.
+template <int N>
+__device__ bool cg_steihaug(const TRModel &m, double jac_mag, double R, double *p) {
     double tol = fmin(0.5, sqrt(jac_mag)) * jac_mag;
-    for (int i = 0; i < n; ++i) p[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = 0.0;
     if (jac_mag < tol) return false;
     double z[5], r[5], d[5], Bd[5];
-    for (int i = 0; i < n; ++i) { z[i] = 0.0; r[i] = m.g[i]; d[i] = -m.g[i]; }
+#pragma unroll
+    for (int i = 0; i < N; ++i) { z[i] = 0.0; r[i] = m.g[i]; d[i] = -m.g[i]; }
+#pragma unroll 1
     for (int it = 0; it < 64; ++it) {
-        hessp(m, d, Bd, n);
-        double dBd = dotn(d, Bd, n);
+        hessp<N>(m, d, Bd);
+        double dBd = dotn<N>(d, Bd);
         if (dBd <= 0.0) {
             double ta, tb;
-            boundary_t(z, d, R, n, ta, tb);
+            boundary_t<N>(z, d, R, ta, tb);
             double pa[5], pb[5];
-            for (int i = 0; i < n; ++i) { pa[i] = z[i] + ta * d[i]; pb[i] = z[i] + tb * d[i]; }
-            bool usea = model_value(m, pa, n) < model_value(m, pb, n);
-            for (int i = 0; i < n; ++i) p[i] = usea ? pa[i] : pb[i];
+#pragma unroll
+            for (int i = 0; i < N; ++i) { pa[i] = z[i] + ta * d[i]; pb[i] = z[i] + tb * d[i]; }
+            bool usea = model_value<N>(m, pa) < model_value<N>(m, pb);
+#pragma unroll
+            for (int i = 0; i < N; ++i) p[i] = usea ? pa[i] : pb[i];
             return true;
         }
-        double rr = dotn(r, r, n);
+        double rr = dotn<N>(r, r);
         double alpha = rr / dBd;
         double zn[5];
-        for (int i = 0; i < n; ++i) zn[i] = z[i] + alpha * d[i];
-        if (sqrt(dotn(zn, zn, n)) >= R) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) zn[i] = z[i] + alpha * d[i];
+        if (sqrt(dotn<N>(zn, zn)) >= R) {
             double ta, tb;
-            boundary_t(z, d, R, n, ta, tb);
-            for (int i = 0; i < n; ++i) p[i] = z[i] + tb * d[i];
+            boundary_t<N>(z, d, R, ta, tb);
+#pragma unroll
+            for (int i = 0; i < N; ++i) p[i] = z[i] + tb * d[i];
             return true;
         }
         double rn[5];
-        for (int i = 0; i < n; ++i) rn[i] = r[i] + alpha * Bd[i];
-        double rnn = dotn(rn, rn, n);
+#pragma unroll
+        for (int i = 0; i < N; ++i) rn[i] = r[i] + alpha * Bd[i];
+        double rnn = dotn<N>(rn, rn);
         if (sqrt(rnn) < tol) {
-            for (int i = 0; i < n; ++i) p[i] = zn[i];
+#pragma unroll
+            for (int i = 0; i < N; ++i) p[i] = zn[i];
             return false;
         }
         double beta = rnn / rr;
-        for (int i = 0; i < n; ++i) { d[i] = -rn[i] + beta * d[i]; z[i] = zn[i]; r[i] = rn[i]; }
+#pragma unroll
+        for (int i = 0; i < N; ++i) { d[i] = -rn[i] + beta * d[i]; z[i] = zn[i]; r[i] = rn[i]; }
     }
-    for (int i = 0; i < n; ++i) p[i] = z[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = z[i];
     return false;
 }
 

@@ -412,12 +412,9 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
 // gtol = -1 (pptoaslib.py:1047-1048), eta 0.15, initial radius 1, max radius
 // 1000, maxiter 200 * len(x0).  Returns 1 when a new proposal is pending.
 // ===========================================================================
-__device__ int tr_update(TRState &S, const double *o, int max_iter) {
+template <int NF>
+__device__ int tr_update_t(TRState &S, const double *o, int max_iter, const int (&idx)[5]) {
     const int phase = S.phase;
-    const int flagmask = S.flagmask;
-    int idx[5], nf = 0;
-    for (int i = 0; i < 5; ++i)
-        if (flagmask >> i & 1) idx[nf++] = i;
     const int maxiter = max_iter > 0 ? max_iter : 200 * 5;
     TRModel m;
     bool done = false;
@@ -450,22 +447,25 @@ __device__ int tr_update(TRState &S, const double *o, int max_iter) {
     }
     if (!done) {
         m.f = S.f;
-        for (int q = 0; q < nf; ++q) {
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
             m.g[q] = S.g[idx[q]];
-            for (int r = 0; r < nf; ++r) {
+#pragma unroll
+            for (int r = 0; r < NF; ++r) {
                 int i = min(idx[q], idx[r]), j = max(idx[q], idx[r]);
                 m.H[q][r] = S.H[uidx(i, j)];
             }
         }
         double p[5];
-        const double jm = sqrt(dotn(m.g, m.g, nf));
-        const bool hb = cg_steihaug(m, jm, S.radius, p, nf);
-        const double pv = model_value(m, p, nf);
+        const double jm = sqrt(dotn<NF>(m.g, m.g));
+        const bool hb = cg_steihaug<NF>(m, jm, S.radius, p);
+        const double pv = model_value<NF>(m, p);
         if (m.f - pv <= 0.0) {
             done = true;                 // warnflag 2: no predicted improvement
         } else {
             for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
-            for (int q = 0; q < nf; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
+#pragma unroll
+            for (int q = 0; q < NF; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
             S.pred = pv;
             S.hb = hb ? 1 : 0;
             S.slot_eval = S.slot_cur ^ 1;
@@ -474,6 +474,28 @@ __device__ int tr_update(TRState &S, const double *o, int max_iter) {
     }
     S.phase = done ? PH_DONE : PH_PROPOSAL;
     return cmd;
+}
+// MAXNF: the largest subspace the caller can meet (3 for the moment path,
+// which never fits tau/alpha; instantiating only those keeps its registers
+// down)
+template <int MAXNF = 5>
+__device__ int tr_update(TRState &S, const double *o, int max_iter) {
+    const int flagmask = S.flagmask;
+    int idx[5] = {0, 0, 0, 0, 0}, nf = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        if (flagmask >> i & 1) idx[nf++] = i;
+    switch (nf) {
+        case 1: return tr_update_t<1>(S, o, max_iter, idx);
+        case 2: return tr_update_t<2>(S, o, max_iter, idx);
+        default:
+            if constexpr (MAXNF <= 3) return tr_update_t<3>(S, o, max_iter, idx);
+            else {
+                if (nf == 3) return tr_update_t<3>(S, o, max_iter, idx);
+                if (nf == 4) return tr_update_t<4>(S, o, max_iter, idx);
+                return tr_update_t<5>(S, o, max_iter, idx);
+            }
+    }
 }
 
 // ===========================================================================
@@ -632,37 +654,67 @@ __device__ __forceinline__ void taylor_acc(const double2 *mu, double x, double r
     }
 }
 
-// k_tr_mom: one wave per moment-mode sub-integration; runs trust-region
+// moments [M, M1) from registers (mu[m - M0]); the window r0..r2 and the
+// partial sums carry over between segments
+template <int M, int M1, int M0>
+__device__ __forceinline__ void taylor_seg(const double2 (&mu)[M1 - M0], double x, double &r0,
+                                           double &r1, double &r2, double2 &G0, double2 &G1,
+                                           double2 &G2) {
+    if constexpr (M < M1) {
+        const double2 v = mu[M - M0];
+        G0 = cadd(G0, rot_scale<M>(v, r0));
+        if constexpr (M >= 1) G1 = cadd(G1, rot_scale<M - 1>(v, r1));
+        if constexpr (M >= 2) G2 = cadd(G2, rot_scale<M - 2>(v, r2));
+        r2 = r1;
+        r1 = r0;
+        r0 = r0 * x * (1.0 / (double)(M + 1));
+        taylor_seg<M + 1, M1, M0>(mu, x, r0, r1, r2, G0, G1, G2);
+    }
+}
+
+#ifndef PPF_TRMOM_WPE
+#define PPF_TRMOM_WPE 2
+#endif
+// k_tr_mom: one workgroup per moment-mode sub-integration; runs trust-region
 // iterations back to back, every evaluation from the moments, until the fit
 // stops or a point leaves the expansion radius of both moment sets (then it
-// asks k_moments for a new centre and exits).
-__global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
-    __shared__ TRState sts[kWaves];
-    __shared__ int cmdb[kWaves];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int s = blockIdx.x * kWaves + wave;
+// asks for a new centre and exits).  Thread t owns channels t + 256 j; each
+// evaluation is one pass over them (moments of the next channel half in
+// flight while the current half is summed), a fixed-order block reduction
+// of f, g, H and the scipy trust-ncg update on thread 0.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WPE))) void k_tr_mom(SolveArgs a) {
+    __shared__ TRState L;
+    __shared__ double red[kWaves * 10];
+    __shared__ int cmdb;
+    const int tid = threadIdx.x;
+    const int s = blockIdx.x;
     if (s >= a.nsub) return;
     TRState &G = a.state[s];
-    if (!G.mmode || G.phase == PH_DONE) return;
-    TRState &L = sts[wave];
+    if (!G.mmode || G.phase == PH_DONE) return;          // uniform per workgroup
     static_assert(sizeof(TRState) % 8 == 0, "TRState copy");
     constexpr int NW = (int)(sizeof(TRState) / 8);
-    for (int i = lane; i < NW; i += 64)
+    for (int i = tid; i < NW; i += kBlock)
         reinterpret_cast<double *>(&L)[i] = reinterpret_cast<const double *>(&G)[i];
-    wave_lds_sync();
+    __syncthreads();
     const int nharm = (a.nbin >> 1) + 1;
     const double h = 0.5 * (double)(nharm - 1);
     const double *dp = a.dphi + (int64_t)s * a.nchan * 2;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    // mask bytes are loaded unconditionally (no per-channel branch between
+    // the loads): without a mask from any valid address and ignored
+    const bool use_mask = mask != nullptr;
+    const uint8_t *mk = use_mask ? mask : reinterpret_cast<const uint8_t *>(a.dphi);
     const double *chan = a.chan + (int64_t)s * a.nchan * 4;
     const double2 *MOM = a.mom + (int64_t)s * 2 * a.nchan * kMoments;
     const double *MRES = a.mres + (int64_t)s * 2 * a.nchan;
     double *stats = a.stats + (int64_t)s * 2 * a.nchan * 10;
     const int flagmask = L.flagmask;
-    if (lane == 0) L.need_mom = 0;
+    const int nit = (a.nchan + kBlock - 1) / kBlock;
+    __syncthreads();
+    if (tid == 0) L.need_mom = 0;
     const int cap = (a.max_iter > 0 ? a.max_iter : 1000) + 4;
     for (int it = 0; it < cap; ++it) {
-        wave_lds_sync();
+        __syncthreads();
         const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
         // moment set whose centre is within the expansion radius for every channel
         int qsel = -1;
@@ -671,16 +723,25 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
             if (!L.mvalid[cand]) continue;
             const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
             const double *rc = MRES + (int64_t)cand * a.nchan;
-            double xm = 0.0;
-            for (int n = lane; n < a.nchan; n += 64) {
-                if (mask && !mask[n]) continue;
-                xm = fmax(xm, fabs(e0 + e1 * dp[2 * n] + e2 * dp[2 * n + 1] + rc[n]));
+            double xm[1] = {0.0};
+            for (int n0 = 0; n0 < a.nchan; n0 += 4 * kBlock) {   // 4 channels' loads, then use
+                double v1[4], v2[4], vr[4];
+                bool ok[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int n = n0 + tid + kBlock * j, nc = min(n, a.nchan - 1);
+                    v1[j] = dp[2 * nc]; v2[j] = dp[2 * nc + 1]; vr[j] = rc[nc];
+                    ok[j] = n < a.nchan && (!use_mask || mk[nc] != 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (ok[j]) xm[0] = fmax(xm[0], fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
             }
-            xm = wave_max(xm);
-            if (kTwoPi * h * xm <= kXMax) qsel = cand;
+            block_max<1>(xm, red);
+            if (kTwoPi * h * xm[0] <= kXMax) qsel = cand;
         }
         if (qsel < 0) {
-            if (lane == 0) {
+            if (tid == 0) {
                 const int tgt = L.mvalid[L.macc] ? 1 - L.macc : L.macc;
                 L.mtarget = tgt;
                 L.mc[tgt][0] = t0; L.mc[tgt][1] = t1; L.mc[tgt][2] = t2;
@@ -698,20 +759,52 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
         double acc[10];
 #pragma unroll
         for (int i = 0; i < 10; ++i) acc[i] = 0.0;
-        for (int n = lane; n < a.nchan; n += 64) {
-            if (mask && !mask[n]) continue;
-            const double d1 = dp[2 * n], d2 = dp[2 * n + 1];
-            const double del = e0 + e1 * d1 + e2 * d2 + rq[n];
+        // channel n = tid + 256 i; its 32 moments come in quarters of 8
+        // (8 x 16 B loads), two buffers rotating so that the next quarter is
+        // in flight while the current one is summed
+        constexpr int KQ = kMoments / 4;
+        double2 qa[KQ], qb[KQ];
+        double c_d1, c_d2, c_rq, c_S;           // channel scalars, prefetched with quarter 0
+        int c_ok;
+        auto ldq = [&](int i, int quarter, double2 (&b)[KQ]) {
+            const int n = min(tid + kBlock * i, a.nchan - 1);
+            const double2 *p = Mq + (int64_t)n * kMoments + KQ * quarter;
+#pragma unroll
+            for (int m = 0; m < KQ; ++m) b[m] = p[m];
+        };
+        auto ldc = [&](int i) {
+            const int n = min(tid + kBlock * i, a.nchan - 1);
+            c_d1 = dp[2 * n]; c_d2 = dp[2 * n + 1]; c_rq = rq[n]; c_S = chan[n * 4 + 3];
+            c_ok = mk[n];
+        };
+        ldq(0, 0, qa);
+        ldc(0);
+        for (int i = 0; i < nit; ++i) {
+            const int n = tid + kBlock * i;
+            ldq(i, 1, qb);
+            const bool valid = n < a.nchan && (!use_mask || c_ok != 0);
+            const double d1 = c_d1, d2 = c_d2, Sn = c_S;
+            const double del = e0 + e1 * d1 + e2 * d2 + c_rq;
             const double x = kTwoPi * h * del;
             double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
-            taylor_acc<0>(Mq + (int64_t)n * kMoments, x, 1.0, 0.0, 0.0, G0, G1, G2);
+            double r0 = 1.0, r1 = 0.0, r2 = 0.0;
+            taylor_seg<0, KQ, 0>(qa, x, r0, r1, r2, G0, G1, G2);
+            ldq(i, 2, qa);
+            taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+            ldq(i, 3, qb);
+            taylor_seg<2 * KQ, 3 * KQ, 2 * KQ>(qa, x, r0, r1, r2, G0, G1, G2);
+            if (i + 1 < nit) {
+                ldq(i + 1, 0, qa);
+                ldc(i + 1);
+            }
+            taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+            if (!valid) continue;
             const double2 eix = cexp2pi(h * del);
             const double2 F = cmul(eix, G0);
             const double2 K1 = cscale(cmul(eix, cadd(G0, G1)), h);
             const double2 K2 = cscale(cmul(eix, cadd(cadd(G0, G2), cscale(G1, 2.0))), h * h);
             const double C = F.x, Cp = -kTwoPi * K1.y, Cpp = -kTwoPi * kTwoPi * K2.x;
             double *sn = st + (int64_t)n * 10;
-            const double Sn = chan[n * 4 + 3];
             sn[0] = C; sn[1] = Cp; sn[2] = Cpp; sn[6] = Sn;
             const double iS = 1.0 / Sn;
             const double dph[3] = {1.0, d1, d2};
@@ -719,33 +812,32 @@ __global__ __launch_bounds__(kBlock) void k_tr_mom(SolveArgs a) {
             // acc: f, g(phi, DM, GM), H upper triangle 00 01 02 11 12 22
             acc[0] += -C * C * iS;
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
-                if (flagmask >> i & 1) acc[1 + i] += -2.0 * C * Cp * dph[i] * iS;
+            for (int q = 0; q < 3; ++q)
+                if (flagmask >> q & 1) acc[1 + q] += -2.0 * C * Cp * dph[q] * iS;
             constexpr int hi[6] = {0, 0, 0, 1, 1, 2}, hj[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
             for (int e = 0; e < 6; ++e)
                 if ((flagmask >> hi[e] & 1) && (flagmask >> hj[e] & 1))
                     acc[4 + e] += hn * dph[hi[e]] * dph[hj[e]];
         }
-        double o[21];
+        block_sum<10>(acc, red);
+        if (tid == 0) {
+            double o[21];
 #pragma unroll
-        for (int i = 0; i < 21; ++i) o[i] = 0.0;
+            for (int i = 0; i < 21; ++i) o[i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = wave_sum(acc[i]);
-        {
+            for (int i = 0; i < 4; ++i) o[i] = acc[i];
             constexpr int hi[6] = {0, 0, 0, 1, 1, 2}, hj[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
-            for (int e = 0; e < 6; ++e) o[6 + uidx(hi[e], hj[e])] = wave_sum(acc[4 + e]);
-        }
-        if (lane == 0) {
+            for (int e = 0; e < 6; ++e) o[6 + uidx(hi[e], hj[e])] = acc[4 + e];
             L.meval = qsel;
-            cmdb[wave] = tr_update(L, o, a.max_iter);
+            cmdb = tr_update<3>(L, o, a.max_iter);
         }
-        wave_lds_sync();
-        if (!cmdb[wave]) break;
+        __syncthreads();
+        if (!cmdb) break;
     }
-    wave_lds_sync();
-    for (int i = lane; i < NW; i += 64)
+    __syncthreads();
+    for (int i = tid; i < NW; i += kBlock)
         reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&L)[i];
 }
 
@@ -1215,8 +1307,7 @@ hipError_t launch_moments(const SolveArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_tr_mom, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
-                       st, a);
+    hipLaunchKernelGGL(k_tr_mom, dim3((unsigned)a.nsub), dim3(kBlock), 0, st, a);
     return hipGetLastError();
 }
 

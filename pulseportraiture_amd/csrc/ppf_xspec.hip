@@ -520,14 +520,29 @@ __global__ void k_model_pow(const double2 *Mft, int nrows, int nharm, double *ou
 
 // sum_n M[model][n][k] over all channels, fixed order (mean model spectrum of
 // the GetTOAs guess; k_guess removes the masked channels)
-__global__ void k_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+// sum over channels of the model spectra: workgroup = 16 harmonics x 16
+// channel groups; each thread sums its group in channel order, then the 16
+// group partials are added in group order (deterministic)
+__global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan, int nharm,
+                                                   int nmodel, double2 *out) {
+    __shared__ double2 part[16][17];
+    const int kl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int k = blockIdx.x * 16 + kl;
     const int m = blockIdx.y;
-    if (k >= nharm || m >= nmodel) return;
-    const double2 *M = Mft + (int64_t)m * nchan * nharm;
+    const int per = (nchan + 15) / 16;
+    const int n0 = grp * per, n1 = min(nchan, n0 + per);
     double2 acc = cmk(0.0, 0.0);
-    for (int n = 0; n < nchan; ++n) acc = cadd(acc, M[(int64_t)n * nharm + k]);
-    out[(int64_t)m * nharm + k] = acc;
+    if (k < nharm) {
+        const double2 *M = Mft + (int64_t)m * nchan * nharm + k;
+        for (int n = n0; n < n1; ++n) acc = cadd(acc, M[(int64_t)n * nharm]);
+    }
+    part[grp][kl] = acc;
+    __syncthreads();
+    if (grp == 0 && k < nharm) {
+        double2 t = part[0][kl];
+        for (int g = 1; g < 16; ++g) t = cadd(t, part[g][kl]);
+        out[(int64_t)m * nharm + k] = t;
+    }
 }
 
 // ===========================================================================
@@ -603,7 +618,7 @@ hipError_t launch_model_pow(const double2 *Mft, int nchan, int nharm, int nmodel
 
 hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out,
                             hipStream_t st) {
-    dim3 g((unsigned)((nharm + 255) / 256), (unsigned)nmodel);
+    dim3 g((unsigned)((nharm + 15) / 16), (unsigned)nmodel);
     hipLaunchKernelGGL(k_model_sum, g, dim3(256), 0, st, Mft, nchan, nharm, nmodel, out);
     return hipGetLastError();
 }

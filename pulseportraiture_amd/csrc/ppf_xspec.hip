@@ -45,6 +45,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // across the row loop are not promoted to VGPRs
 typedef float vf2 __attribute__((ext_vector_type(2)));
 typedef double vd2 __attribute__((ext_vector_type(2)));
+typedef float vf4 __attribute__((ext_vector_type(4)));
 #ifndef PPF_SCHED_CUT
 #define PPF_SCHED_CUT 1
 #endif
@@ -242,6 +243,17 @@ __host__ __device__ constexpr int xmom_slw() {
 #else
 #define G_CUT()
 #endif
+#ifdef PPF_XM_PROF
+// section cycle counters of k_xmom_g (profiling builds only)
+__device__ unsigned long long g_xprof[8];
+#define XP_INIT() unsigned long long xp_acc[7] = {0, 0, 0, 0, 0, 0, 0}; unsigned long long xp_t = __builtin_amdgcn_s_memtime()
+#define XP(i) do { const unsigned long long xp_n = __builtin_amdgcn_s_memtime(); xp_acc[i] += xp_n - xp_t; xp_t = xp_n; } while (0)
+#define XP_DONE() do { if (lane == 0) for (int xi = 0; xi < 7; ++xi) atomicAdd(&g_xprof[xi], xp_acc[xi]); } while (0)
+#else
+#define XP_INIT()
+#define XP(i)
+#define XP_DONE()
+#endif
 __device__ __forceinline__ double bin_centre(double phc, int nbin) {
     return rint(phc * (double)nbin);
 }
@@ -279,7 +291,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     constexpr int MPT = (NH + 511) / 512;   // model-row elements per thread
     constexpr int TWN = tw_slots<LOG2N>();
     using ElT = typename std::conditional<DT == 0, float, double>::type;
-    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
+    // data rows move as 16-B vectors: VE elements per load, NLD loads per lane
+    using VecT = typename std::conditional<DT == 0, vf4, vd2>::type;
+    constexpr int VE = 16 / (int)sizeof(ElT), NLD = 2 * N / (64 * VE);
+    static_assert((2 * N + VE) * sizeof(ElT) <= SLW * sizeof(double2), "row staging fits the buffer");
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double2 *buf = lds + wave * SLW;
@@ -348,21 +363,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         if (tid == 0) mrow[NH] = cmk(mpw, 0.0);
     };
-    // shifted row: z_j = x[(2j + sh) mod 2N] + i x[(2j + 1 + sh) mod 2N]
-    RowT zr[R];
+    // The row is fetched unshifted with coalesced 16-B loads (lane l holds
+    // elements VE (l + 64 c)), staged through the wave's LDS buffer and read
+    // back shifted: z_j = x[(2j + sh) mod 2N] + i x[(2j + 1 + sh) mod 2N].
+    // (Per-element 4-B loads with the shift in the address cost 4x the
+    // vector-memory issue slots.)
+    VecT zr[NLD];
     double nx_r = 0.0;
+    int nx_sh = 0;
     auto fetch = [&](int n) {
         const int r = n - cbase;
         const double phc = c0 + c1 * readlane_d(ch_d0, r) + c2 * readlane_d(ch_d1, r);
         const double sb = bin_centre(phc, 2 * N);
-        const int sh = (int)(sb - (double)(2 * N) * floor(sb / (double)(2 * N)));
+        nx_sh = (int)(sb - (double)(2 * N) * floor(sb / (double)(2 * N)));
         nx_r = phc - sb / (double)(2 * N);          // residual centre offset
-        const ElT *x = rows + (int64_t)n * (2 * N);
+        const VecT *x = reinterpret_cast<const VecT *>(rows + (int64_t)n * (2 * N));
 #pragma unroll
-        for (int qq = 0; qq < R; ++qq) {
-            const int j2 = 2 * (lane + 64 * qq) + sh;
-            zr[qq] = RowT{x[j2 & (2 * N - 1)], x[(j2 + 1) & (2 * N - 1)]};
-        }
+        for (int c = 0; c < NLD; ++c) zr[c] = x[lane + 64 * c];
     };
     auto usable = [&](int n) {
         return act && n < cend && __builtin_amdgcn_readlane(ch_use, n - cbase) != 0;
@@ -374,22 +391,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     mstore();
     if (act) fetch(n);
     __syncthreads();
+    XP_INIT();
     for (; n < cend; ++n) {
         const bool live = usable(n);
         const double res_in = nx_r;
+        const int sh = nx_sh;
         const double errs_in = a.errs ? readlane_d(ch_e, n - cbase) : 0.0;
-        double2 x[R];
+        // stage: raw row + the first VE elements again past the end (the
+        // odd-shift read of element 2N - 1 takes its partner from there)
+        ElT *row = reinterpret_cast<ElT *>(buf);
+        if (live) {
 #pragma unroll
-        for (int qq = 0; qq < R; ++qq) x[qq] = cmk((double)zr[qq][0], (double)zr[qq][1]);
+            for (int c = 0; c < NLD; ++c) *reinterpret_cast<VecT *>(row + VE * (lane + 64 * c)) = zr[c];
+            if (lane == 0) *reinterpret_cast<VecT *>(row + 2 * N) = zr[0];
+        }
+        XP(6);
         // next round's model row, then its data row, in flight during this
         // round (the data load is unconditional for active waves: keeps zr[]
         // in VGPRs)
         mload(n + 1);
         if (act) fetch(n + 1 < cend ? n + 1 : n);
+        XP(0);
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
+            wfft::wave_sync();
+            double2 x[R];
+#pragma unroll
+            for (int qq = 0; qq < R; ++qq) {
+                const int j2 = (2 * (lane + 64 * qq) + sh) & (2 * N - 1);
+                x[qq] = cmk((double)row[j2], (double)row[j2 + 1]);
+            }
+            wfft::wave_sync();
 #ifndef G_NOFFT
             wfft::fft_row<LOG2N>(x, buf, tw, lane);
+            XP(1);
 #else
             for (int qq = 0; qq < R; ++qq) buf[wfft::pad<LOG2N>(lane + 64 * qq)] = x[qq];
 #endif
@@ -450,7 +485,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         } else if (act && n < cend && lane < 4) {
             a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;    // masked channel
         }
+        XP(2);
         __syncthreads();
+        XP(3);
         mstore();                         // this round no longer reads mrow
 
         f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0;
@@ -469,6 +506,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * so], bv, d1, 0, 0, 0);
         }
 #endif
+        XP(4);
         // output element tid: this wave's sub-int, moment om = 2 j + set,
         // Re/Im ori
         const int om = (tid >> 1) & 31, ori = tid & 1;
@@ -493,7 +531,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             if (live) mom[((int64_t)n * kMoments + om) * 2 + ori] = val * ie;
         }
         __syncthreads();
+        XP(5);
     }
+    XP_DONE();
 }
 
 // folded-moment B table: Bt[k][j] = (u_k^2)^j, u_k = (k - N/2)/(N/2), k < N/2
@@ -624,3 +664,15 @@ hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel
 }
 
 }  // namespace ppf
+
+#ifdef PPF_XM_PROF
+extern "C" int ppf_debug_xprof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ppf::g_xprof), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ppf::g_xprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -45,6 +45,12 @@ def parse():
     ap.add_argument("--nbin", type=int, default=2048)
     ap.add_argument("--chunk", type=int, default=2500,
                     help="sub-integrations per ppf_fit_batch call")
+    ap.add_argument("--fit", default="phase+DM",
+                    choices=["phase+DM", "full", "scat"],
+                    help="phase+DM: configs[1] (the metric); full: configs[2] "
+                    "fit (phi, DM, GM, tau, alpha) on data with injected "
+                    "scattering; scat: configs[4] fit (phi, DM, tau, alpha), "
+                    "CHIME-like band")
     ap.add_argument("--cpu-sample", type=int, default=48,
                     help="sub-integrations for the CPU baseline (0: skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
@@ -94,7 +100,19 @@ def main():
     nharm = nbin // 2 + 1
 
     # ---- resident inputs (untimed) ------------------------------------------
-    batch = synth.make_batch(count, nchan, nbin, first=first, dev=dev)
+    # fit modes: C3 injects tau = 2e-3 rot at 1500 MHz,
+    # C5 tau = 5e-3 rot at 600 MHz over 400-800 MHz; alpha = -4, and the
+    # GetTOAs guesses tau = 1/nbin (log10), alpha = -4 (pptoas.py:467-492)
+    FIT = {"phase+DM": dict(flags=[1, 1, 0, 0, 0], band=(1100.0, 800.0),
+                            tau=0.0, nu_tau=None, cfg=1),
+           "full": dict(flags=[1, 1, 1, 1, 1], band=(1100.0, 800.0),
+                        tau=2e-3, nu_tau=1500.0, cfg=2),
+           "scat": dict(flags=[1, 1, 0, 1, 1], band=(400.0, 400.0),
+                        tau=5e-3, nu_tau=600.0, cfg=4)}[args.fit]
+    scat_fit = FIT["tau"] > 0.0
+    batch = synth.make_batch(count, nchan, nbin, first=first, dev=dev,
+                             lo=FIT["band"][0], bw=FIT["band"][1],
+                             tau=FIT["tau"], nu_tau=FIT["nu_tau"])
     data = batch["data"]
     f64 = torch.float64
     model_t = torch.as_tensor(batch["model"], dtype=f64, device=dev)
@@ -103,8 +121,11 @@ def main():
     P_t = torch.as_tensor(batch["P"], dtype=f64, device=dev)
     init = np.zeros((count, 5))
     init[:, 1] = synth.DM0                       # DM_guess = DM_stored
+    if scat_fit:
+        init[:, 3] = np.log10(1.0 / nbin)
+        init[:, 4] = synth.GMODEL_ALPHA
     init_t = torch.as_tensor(init, dtype=f64, device=dev)
-    flags_t = torch.tensor([1, 1, 0, 0, 0], dtype=torch.int32,
+    flags_t = torch.tensor(FIT["flags"], dtype=torch.int32,
                            device=dev).repeat(count, 1)
     nu_fit = guess_fit_freq(batch["freqs"])      # pptoas.py:442
     nu_fits_t = torch.full((count, 3), nu_fit, dtype=f64, device=dev)
@@ -126,6 +147,7 @@ def main():
             res = engine.fit_batch(
                 data[sl], model_t, freqs_t[sl], P_t[sl], init_t[sl],
                 flags_t[sl], nu_fits=nu_fits_t[sl], nu_outs=nu_outs_t[sl],
+                log10_tau=scat_fit,
                 guess=True, guess_weights=gw_t[sl], guess_DM=gdm_t[sl],
                 guess_Ns=100, dev=dev, workspace=ws)
             ws = res["workspace"]
@@ -172,13 +194,24 @@ def main():
     nblkd = (nchan + 127) // 128
     xmom_unit = nchan * nbin * 4 + nchan * 16 + nchan * (32 * 16 + 4 * 8 + 8)
     dsum_unit = nchan * nbin * 4 + nblkd * nbin * 8 + nblkd * 16
+    #  k_xspec_w (scattering fits: the cross spectrum X streamed by every
+    #   evaluation): read the rows, write X (complex128) and 4 scalars/channel
+    xspec_unit = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
+    L2N = (nbin // 4).bit_length()
     kern = {
-        "xmom": dict(name="k_xmom_g<%d, 0, true, true>" % (nbin // 4).bit_length(),
-                     ms=kern_ms[0], unit=xmom_unit,
-                     bytes=steps_subints * xmom_unit + ncalls * nchan * nharm * 16),
         "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
                      bytes=steps_subints * dsum_unit),
     }
+    if scat_fit:
+        kern["xspec"] = dict(name="k_xspec_w<%d, 0>" % L2N, ms=stage_ms[1],
+                             unit=xspec_unit,
+                             bytes=steps_subints * xspec_unit +
+                             ncalls * nchan * nharm * 16)
+    else:
+        kern["xmom"] = dict(name="k_xmom_g<%d, 0, true, true>" % L2N,
+                            ms=kern_ms[0], unit=xmom_unit,
+                            bytes=steps_subints * xmom_unit +
+                            ncalls * nchan * nharm * 16)
     dom = max(kern, key=lambda k: kern[k]["ms"])
     dk = kern[dom]
     achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
@@ -205,17 +238,26 @@ def main():
                             round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
                for k, v in kern.items()}
     value = total * args.steps / dt
-    out = dict(metric=METRIC, value=round(value, 2), unit="subint-fits/s",
+    metric = METRIC if args.fit == "phase+DM" else (
+        "subint portrait fits/sec (%s, %dch×%dbin) at 1/2/4/8 MI355X" %
+        ("phi+DM+GM+tau+alpha" if args.fit == "full" else "phi+DM+tau+alpha",
+         nchan, nbin))
+    out = dict(metric=metric, value=round(value, 2), unit="subint-fits/s",
                n_gpus=world, steps=args.steps, warmup=args.warmup,
                ms_per_step=round(dt / args.steps * 1e3, 3),
                higher_is_better=True, scaling="weak", vs_baseline=None,
                dtype="f64", data="synthetic (device-generated example.gmodel "
                "portraits + white noise; float32 amplitudes)",
-               config=dict(workload="configs[1]: %d subints/GPU x %dch x "
-                           "%dbin, phase+DM wideband fit (GetTOAs path)" %
-                           (args.nsub, nchan, nbin), nsub_per_gpu=args.nsub,
+               config=dict(workload="configs[%d]: %d subints/GPU x %dch x "
+                           "%dbin, %s wideband fit (GetTOAs path)%s" %
+                           (FIT["cfg"], args.nsub, nchan, nbin, args.fit,
+                            "" if not scat_fit else
+                            ", injected tau %g rot at %g MHz" %
+                            (FIT["tau"], FIT["nu_tau"])),
+                           nsub_per_gpu=args.nsub,
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
-                           fit="phase+DM", parallelism="dp%d" % world),
+                           fit=args.fit, fit_flags=FIT["flags"],
+                           parallelism="dp%d" % world),
                roofline=roof, stage_ms=stages, kernels=kernels,
                mean_passes_per_fit=round(mean_passes, 3),
                mean_evals_per_fit=round(mean_nfev, 3),
@@ -227,7 +269,17 @@ def main():
         dme = res_np[:count, I["param_errs"]][:, 1]
         pull = (dm - batch["DM_true"]) / dme
         out["dm_pull_rms"] = round(float(np.sqrt(np.mean(pull ** 2))), 3)
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if scat_fit and rank == 0:
+        # log10 tau at the output reference frequency vs the injected truth
+        pr = res_np[:count, I["params"]]
+        pe = res_np[:count, I["param_errs"]]
+        nuo = res_np[:count, I["nu_out"]][:, 2]
+        truth = np.log10(FIT["tau"] * (nuo / FIT["nu_tau"]) ** synth.GMODEL_ALPHA)
+        out["tau_pull_rms"] = round(float(np.sqrt(np.mean(
+            ((pr[:, 3] - truth) / pe[:, 3]) ** 2))), 3)
+        out["alpha_pull_rms"] = round(float(np.sqrt(np.mean(
+            ((pr[:, 4] - synth.GMODEL_ALPHA) / pe[:, 4]) ** 2))), 3)
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and not scat_fit:
         out["cpu_baseline"] = cpu_baseline(batch, args.cpu_sample, nchan,
                                            nbin)
         out["vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"],

@@ -55,16 +55,37 @@ def truths(nsub, seed, first=0):
     return phi, dm
 
 
+def scattered(model, freqs, tau, alpha, nu_tau):
+    """The portrait convolved with the one-sided exponential scattering kernel
+    of the fit model: rfft(model_n) x B_nk, B_nk = 1 / (1 + 2 pi i k tau_n),
+    tau_n = tau (nu_n / nu_tau)^alpha [rot] (pplib.py:4212-4260)."""
+    nbin = model.shape[-1]
+    k = np.arange(nbin // 2 + 1)
+    taus = tau * (np.asarray(freqs) / nu_tau) ** alpha
+    B = 1.0 / (1.0 + 2j * np.pi * np.outer(taus, k))
+    return np.fft.irfft(np.fft.rfft(model, axis=-1) * B, n=nbin, axis=-1)
+
+
 def make_batch(nsub, nchan, nbin, seed=20250217, first=0, noise=1.5,
-               nu_ref=1500.0, dtype="float32", dev=None):
+               nu_ref=1500.0, dtype="float32", dev=None, lo=1100.0, bw=800.0,
+               tau=0.0, alpha=GMODEL_ALPHA, nu_tau=None):
     """Device batch: dict(data [nsub,nchan,nbin] device tensor, model, freqs,
-    P, phi_true, DM_true)."""
+    P, phi_true, DM_true[, tau_true, alpha_true, nu_tau]).  tau > 0 injects
+    scattering (tau [rot] at nu_tau, default nu_ref) into every sub-int; the
+    returned `model` is the unscattered template the fit starts from."""
     import torch
-    model, freqs = template(nchan, nbin)
+    model, freqs = template(nchan, nbin, lo, bw)
     phi, dm = truths(nsub, seed, first)
     P = np.full(nsub, P0)
-    data = engine.synth(model, freqs, phi, dm, P, nu_ref, noise, seed,
+    src = model
+    if tau > 0.0:
+        nu_tau = nu_ref if nu_tau is None else nu_tau
+        src = scattered(model, freqs, tau, alpha, nu_tau)
+    data = engine.synth(src, freqs, phi, dm, P, nu_ref, noise, seed,
                         torch.float32 if dtype == "float32" else torch.float64,
                         dev=dev, first=first)
-    return dict(data=data, model=model, freqs=freqs, P=P, phi_true=phi,
-                DM_true=dm, nu_ref=nu_ref)
+    out = dict(data=data, model=model, freqs=freqs, P=P, phi_true=phi,
+               DM_true=dm, nu_ref=nu_ref)
+    if tau > 0.0:
+        out.update(tau_true=tau, alpha_true=alpha, nu_tau=nu_tau)
+    return out

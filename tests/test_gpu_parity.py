@@ -401,3 +401,83 @@ def test_device_guess_matches_oracle_phase_shift():
                                mod=True)
         got = r["results"][i, _lib.RESULT_INDEX["phi_guess"]]
         assert abs(G.phase_diff(got, ph)) < 2e-4, (got, ph)
+
+
+# ------------------------------------------- wide-band scattering (C3 / C5) --
+def _scat_batch(nsub, nchan, nbin, first):
+    from pulseportraiture_amd import synth
+    from pulseportraiture_amd.pplib import guess_fit_freq, phase_transform
+    b = synth.make_batch(nsub, nchan, nbin, first=first, lo=400.0, bw=400.0,
+                         tau=5e-3, nu_tau=600.0)
+    nu_fit = guess_fit_freq(b["freqs"])
+    init = np.zeros((nsub, 5))
+    for i in range(nsub):    # start at the injected phase, moved to nu_fit
+        init[i, 0] = phase_transform(b["phi_true"][i], b["DM_true"][i],
+                                     b["nu_ref"], nu_fit, b["P"][i], mod=True)
+    init[:, 1] = synth.DM0
+    init[:, 3] = np.log10(1.0 / nbin)           # pptoas.py:488-490
+    init[:, 4] = synth.GMODEL_ALPHA
+    return b, nu_fit, init
+
+
+def test_wideband_scattering_2048ch_matches_oracle():
+    """configs[4]-style fit (phi, DM, tau, alpha; CHIME-like 400-800 MHz
+    band, injected tau = 5e-3 rot at 600 MHz) with 2048 channels -- more
+    channel blocks than any golden case -- against the oracle restatement
+    on the same float32 data: parameters within 0.01 sigma, chi2_red within
+    1e-8 (the reference itself cannot run this width: its dense covariance
+    cube, pptoaslib.py:731, would take 2048^3 x 8 B)."""
+    import oracle as O
+    from pulseportraiture_amd import engine, _lib
+    nsub, nchan, nbin = 1, 2048, 256
+    b, nu_fit, init = _scat_batch(nsub, nchan, nbin, first=4242)
+    flags = [1, 1, 0, 1, 1]
+    r = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags,
+        nu_fits=np.full((nsub, 3), nu_fit), log10_tau=True))
+    I = _lib.RESULT_INDEX
+    R = r["results"][0]
+    data = b["data"][0].double().cpu().numpy()
+    ref = O.fit_portrait_full(data, b["model"], list(init[0]), b["P"][0],
+                              b["freqs"], nu_fits=(nu_fit,) * 3,
+                              fit_flags=flags, log10_tau=True)
+    got = dict(params=R[I["params"]], nu_DM=R[I["nu_out"]][0],
+               nu_GM=R[I["nu_out"]][1], nu_tau=R[I["nu_out"]][2])
+    refd = dict(params=ref["params"], param_errs=ref["param_errs"],
+                nu_DM=ref["nu_DM"], nu_GM=ref["nu_GM"], nu_tau=ref["nu_tau"])
+    dev = G.param_deviation_sigma(got, refd, b["P"][0], True)
+    assert dev.max() < SIG, dev
+    assert abs(R[I["red_chi2"]] / ref["red_chi2"] - 1) < RCHI2
+    np.testing.assert_allclose(R[I["param_errs"]], ref["param_errs"],
+                               rtol=1e-4)
+    np.testing.assert_allclose(r["scales"][0], ref["scales"], rtol=1e-4,
+                               atol=1e-3 * np.abs(ref["scale_errs"]).min())
+
+
+def test_chime_shape_16384ch_scattering_fit_properties():
+    """configs[4] shape (16384 x 1024, phi+DM+tau+alpha): the fit converges,
+    recovers the injected DM / tau / alpha within 6 sigma, is bitwise
+    reproducible and independent of its batch."""
+    from pulseportraiture_amd import engine, _lib, synth
+    nsub, nchan, nbin = 2, 16384, 1024
+    b, nu_fit, init = _scat_batch(nsub, nchan, nbin, first=9000)
+    flags = [1, 1, 0, 1, 1]
+    kw = dict(nu_fits=np.full((nsub, 3), nu_fit), log10_tau=True)
+    r1 = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags, **kw))
+    r2 = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags, **kw))
+    np.testing.assert_array_equal(r1["results"], r2["results"])
+    one = engine.results_numpy(engine.fit_batch(
+        b["data"][1:2], b["model"], b["freqs"], b["P"][1:2], init[1:2], flags,
+        nu_fits=np.full((1, 3), nu_fit), log10_tau=True))
+    np.testing.assert_array_equal(one["results"][0], r1["results"][1])
+    I = _lib.RESULT_INDEX
+    R = r1["results"]
+    assert np.all((R[:, I["status"]].astype(int) & 0xff) == 2)
+    p, e = R[:, I["params"]], R[:, I["param_errs"]]
+    nuo = R[:, I["nu_out"]][:, 2]
+    tau_true = np.log10(5e-3 * (nuo / 600.0) ** synth.GMODEL_ALPHA)
+    assert np.all(np.abs((p[:, 1] - b["DM_true"]) / e[:, 1]) < 6)
+    assert np.all(np.abs((p[:, 3] - tau_true) / e[:, 3]) < 6)
+    assert np.all(np.abs((p[:, 4] - synth.GMODEL_ALPHA) / e[:, 4]) < 6)

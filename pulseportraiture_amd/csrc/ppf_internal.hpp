@@ -23,7 +23,7 @@ struct XspecArgs {
     const double *errs;          // [nsub][nchan] or null
     const double *freqs, *P;
     const double2 *T, *T2;
-    double2 *X;                  // [nsub][nchan][N+1]
+    double2 *X;                  // [nsub][N+1][nchan] (harmonic-major)
     double *chan;                // [nsub][nchan][4]
     // wave path: model row power sum_{k>=1} |M_nk|^2 ([nmodel][nchan]) and
     // the per-sub-int "write X" flag (null: every sub-int).  Sub-ints whose
@@ -80,6 +80,7 @@ struct TRState;
 struct SolveArgs {
     int nsub, nchan, nbin;
     const double2 *X, *Mft;
+    const double *MP;            // [nmodel][N+1][nchan] |M_nk|^2 (k = 0: 0)
     const int32_t *model_index;
     const double *chan;
     const double *freqs, *P;
@@ -168,5 +169,7 @@ hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
+hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmodel, double *MP,
+                              hipStream_t st);
 
 }  // namespace ppf

@@ -153,7 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
         else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)(2 * N)) * sqrt_half_nbin;
         const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-        double2 *Xrow = a.X + crow * NH;
+        double2 *Xrow = a.X + (int64_t)s * NH * a.nchan + n;   // X[s][k][n]
+        const int64_t xs = a.nchan;
         double mpow[1] = {0.0};
         // pass 2: cross spectrum (D recomputed from the LDS spectrum)
 #pragma unroll
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
                     Xrow[0] = cmk(0.0, 0.0);       // F0_fact = 0 (pplib.py:82)
                 } else {
                     mpow[0] += cabs2(M);
-                    Xrow[k] = cscale(cmulc(rfft_bin(buf, N, T2, k), M), inv_e2);
+                    Xrow[k * xs] = cscale(cmulc(rfft_bin(buf, N, T2, k), M), inv_e2);
                 }
             }
         }
@@ -492,14 +493,18 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double err = sig * sqrt((double)a.nbin / 2.0);
     const double phase = brute_fmin(xm, nharm, 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
                                     nullptr);
-    if (tid == 0) {
-        // nu_mean of the usable channels
+    // nu_mean of the usable channels (block reduction: 16384-channel
+    // portraits made a serial loop here cost ~0.2 ms per sub-int)
+    double nv[2] = {0.0, 0.0};
+    {
         const double *fr = a.freqs + (int64_t)s * a.nchan;
         const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-        double sum = 0.0, c = 0.0;
-        for (int n = 0; n < a.nchan; ++n)
-            if (!mask || mask[n]) { sum += fr[n]; c += 1.0; }
-        double nu_mean = sum / c;
+        for (int n = tid; n < a.nchan; n += kBlock)
+            if (!mask || mask[n]) { nv[0] += fr[n]; nv[1] += 1.0; }
+    }
+    block_sum<2>(nv, red);
+    if (tid == 0) {
+        double nu_mean = nv[0] / nv[1];
         double nu_fit = a.nu_fits[(int64_t)s * 3 + 0];
         if (nu_fit != nu_fit) nu_fit = nu_mean;
         double DM = a.guess_DM[s], P = a.P[s];

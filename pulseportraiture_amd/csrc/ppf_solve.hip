@@ -117,17 +117,21 @@ __device__ __forceinline__ Fac make_fac(double nu, const FitGeom &g, double alph
 
 // reference gates (taus.sum(), dtau.sum(), dalpha.sum()) at (tau_lin, alpha)
 // over the usable channels; wave-level (all 64 lanes of the calling wave).
-__device__ void wave_gates(const double *fr, const uint8_t *mask, int nchan, double tau_lin,
-                           double alpha, double nu_tau, int log10_tau, int &g_sum, int &g_tau,
-                           int &g_alpha) {
+// The reference's gates taus.sum(), dtau.sum(), dalpha.sum() != 0
+// (pptoaslib.py:271-276, 351-355, 368-382).  lnr[n] = ln(nu_n / nu_tau) is
+// cached per channel by k_tr_init (only the exact-zero outcome matters, so
+// tau_n = tau exp(alpha lnr) instead of the fit's pow form is equivalent).
+__device__ void wave_gates(const double *lnr, const uint8_t *mask, int nchan, double tau_lin,
+                           double alpha, int log10_tau, int &g_sum, int &g_tau, int &g_alpha) {
     const int lane = threadIdx.x & 63;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int n = lane; n < nchan; n += 64) {
         if (mask && !mask[n]) continue;
-        double tn = tau_lin * pow(fr[n] / nu_tau, alpha);
+        const double l = lnr[n];
+        const double tn = tau_lin * exp(alpha * l);
         s0 += tn;
         s1 += log10_tau ? kLn10 * tn : tn / tau_lin;
-        s2 += log(fr[n] / nu_tau) * tn;
+        s2 += l * tn;
     }
     s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2);
     g_sum = s0 != 0.0;
@@ -178,7 +182,15 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         if (nu_fit[i] != nu_fit[i]) nu_fit[i] = nu_mean;
     }
     int gs = 0, gt = 0, ga = 0;
-    if (scat) wave_gates(fr, mask, a.nchan, tau0, x[4], nu_fit[2], a.log10_tau, gs, gt, ga);
+    if (scat) {
+        // ln(nu_n / nu_tau) for the gates (the moment path's dphi slot is
+        // free for scattering fits)
+        double *lnr = a.dphi + (int64_t)s * a.nchan * 2;
+        for (int n = lane; n < a.nchan; n += 64) lnr[n] = log(fr[n] / nu_fit[2]);
+        wave_lds_sync();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_gates(lnr, mask, a.nchan, tau0, x[4], a.log10_tau, gs, gt, ga);
+    }
     if (lane == 0) {
         for (int i = 0; i < 5; ++i) { S.x[i] = x[i]; S.th[i] = x[i]; S.g[i] = 0.0; }
         S.f = 0.0;
@@ -241,13 +253,20 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
 
 // ===========================================================================
 // k_pass: one streaming pass over X for the sub-ints that asked for one
-// grid = nsub * nblk; workgroup = 4 waves; block = kPassChans channels
+// grid = nsub * nblk; workgroup = 4 waves; thread t owns channel
+// blk * kPassChans + t and runs its whole harmonic sum (X is harmonic-major,
+// so a wave's loads of one harmonic are 64 consecutive channels, 1 KiB):
+// no cross-lane reduction per channel, the per-channel setup (phase, the
+// scattering time, exact phasor seeds every 64 harmonics) amortised over the
+// row, one fixed-order block reduction of f, g, H per workgroup.
 // ===========================================================================
-constexpr int kPassChans = 64;                 // channels per workgroup
-constexpr int kWaveChans = kPassChans / kWaves; // 16 per wave
+constexpr int kPassChans = kBlock;             // channels per workgroup
 
-template <bool SCAT, int U>
-__global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
+#ifndef PPF_PASS_WPE
+#define PPF_PASS_WPE 2
+#endif
+template <bool SCAT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS_WPE))) void k_pass(SolveArgs a) {
     __shared__ double red[kWaves * 21];
     const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
     const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
@@ -258,8 +277,7 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *chan = a.chan + (int64_t)s * a.nchan * 4;
-    const double2 *X = a.X + (int64_t)s * a.nchan * nharm;
-    const double2 *M = a.Mft + (int64_t)(a.model_index ? a.model_index[s] : 0) * a.nchan * nharm;
+    const int mi = a.model_index ? a.model_index[s] : 0;
     double *stats = a.stats + ((int64_t)s * 2 + S.slot_eval) * a.nchan * 10;
     double th[5];
     for (int i = 0; i < 5; ++i) th[i] = S.th[i];
@@ -279,90 +297,117 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
     double acc[21];
 #pragma unroll
     for (int i = 0; i < 21; ++i) acc[i] = 0.0;
-    const int c0 = blk * kPassChans + wave * kWaveChans;
-    const int c1 = min(a.nchan, c0 + kWaveChans);
-    double my[10];
-#pragma unroll
-    for (int q = 0; q < 10; ++q) my[q] = 0.0;
-    for (int n = c0; n < c1; ++n) {
-        if (mask && !mask[n]) continue;
+    const int n = blk * kPassChans + threadIdx.x;
+    if (n < a.nchan && (!mask || mask[n])) {
         const double nu = fr[n];
         const double phin = th[0] + kDconst * th[1] * (pow(nu, -2.0) - nuDM2) / g.P +
                             kDconst * kDconst * th[2] * (pow(nu, -4.0) - nuGM4) / g.P;
-        const double2 W = cexp2pi(64.0 * phin);
-        const double2 *Xr = X + (int64_t)n * nharm;
-        const double2 *Mr = M + (int64_t)n * nharm;
+        const double2 W = cexp2pi(phin);
+        const double2 *Xc = a.X + (int64_t)s * nharm * a.nchan + n;
+        const double *Pc = a.MP + (int64_t)mi * nharm * a.nchan + n;
+        const int64_t xs = a.nchan;
         double aa = 0.0, inv_e2 = 0.0;
         if (SCAT) {
             aa = kTwoPi * tau_lin * pow(nu / g.nu_tau, alpha);
             inv_e2 = chan[n * 4 + 1];
         }
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-        double q1 = 0.0, q1p = 0.0, q2 = 0.0, s0 = 0.0, s1 = 0.0, s2a = 0.0, s2b = 0.0;
-        double2 E = cexp2pi((double)lane * phin);
-        for (int kb = lane; kb < nharm; kb += 64 * U) {
-            double2 xv[U];
-            double pk[U];
+        double q1 = 0.0, q1p = 0.0, q2 = 0.0, s0 = 0.0, t1 = 0.0, t2 = 0.0;
+        // Scattering terms in closed form (pptoaslib.py:344-455 restated):
+        // with u = 2 pi k tau_n, d = 1 / (1 + u^2), w = conj(B) = d (1 + iu),
+        //   B - 1 = -iu B, so dB ~ B (B - 1) = -iu B^2, d2B ~ -u^2 B^3 and
+        //   y conj(B) = y w = z1,  y conj(B (B-1)) = iu z2 (z2 = z1 w),
+        //   y conj(B (B-1)^2) = -u^2 z1 w^2 w,
+        //   |B|^2 = d, Re B conj(B(B-1)) = -u^2 d^2, |B(B-1)|^2 = u^2 d^2,
+        //   Re B conj(B(B-1)^2) = -u^2 d^3 (1 - u^2):
+        // the S sums need only the real t1 = sum u^2 d^2 P, t2 = sum
+        // u^2 d^3 (1 - u^2) P.
+        // harmonics in groups of KB: the next group's loads are issued before
+        // the current group is summed (software pipeline, one memory wait per
+        // group)
+#ifndef PPF_PASS_KB
+#define PPF_PASS_KB 4
+#endif
+        constexpr int KB = PPF_PASS_KB;
+        // three rotating groups: loads run two groups ahead of the sums
+        double2 xv[KB], xn[KB], xn2[KB];
+        double pv[KB], pn[KB], pn2[KB];
+        auto ldg = [&](int kb, double2 (&xo)[KB], double (&po)[KB]) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = kb + 64 * u;
-                xv[u] = (k < nharm) ? Xr[k] : cmk(0.0, 0.0);
-                if (SCAT) pk[u] = (k < nharm && k > 0) ? cabs2(Mr[k]) : 0.0;
+            for (int u = 0; u < KB; ++u) {
+                const int k = min(kb + u, nharm - 1);
+                // past the last harmonic: zero terms (no branch in the group)
+                const bool in = kb + u < nharm;
+                const double2 xl = Xc[k * xs];
+                xo[u] = in ? xl : cmk(0.0, 0.0);
+                if (SCAT) {
+                    const double pl = Pc[k * xs];
+                    po[u] = in ? pl : 0.0;
+                }
             }
+        };
+        ldg(0, xv, pv);
+        if (KB < nharm) ldg(KB, xn, pn);
+        double2 E = cmk(1.0, 0.0);
+        for (int kb = 0; kb < nharm; kb += KB) {
+            if (kb + 2 * KB < nharm) ldg(kb + 2 * KB, xn2, pn2);
+            if ((kb & 63) == 0) E = cexp2pi((double)kb * phin);   // exact seed every 64
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const double kk = (double)(kb + 64 * u);
+            for (int u = 0; u < KB; ++u) {
+                const double kk = (double)(kb + u);
                 const double2 y = cmul(xv[u], E);
                 if (!SCAT) {
                     a0 += y.x;
                     a1 = fma(kk, y.y, a1);
                     a2 = fma(kk * kk, y.x, a2);
                 } else {
-                    const double uu = aa * kk;
-                    const double d = 1.0 / fma(uu, uu, 1.0);
-                    const double2 B = cmk(d, -uu * d);
-                    const double2 Bm1 = cmk(d - 1.0, -uu * d);
-                    const double2 be = cmul(B, Bm1);
-                    const double2 be2 = cmul(be, Bm1);
-                    const double2 cy = cmulc(y, B);
-                    const double2 qy = cmulc(y, be);
-                    a0 += cy.x;
-                    a1 = fma(kk, cy.y, a1);
-                    a2 = fma(kk * kk, cy.x, a2);
-                    q1 += qy.x;
-                    q1p = fma(kk, qy.y, q1p);
-                    q2 += fma(y.x, be2.x, y.y * be2.y);
-                    const double Pk = pk[u] * inv_e2;
+                    const double uu = aa * kk, u2 = uu * uu;
+                    const double den = 1.0 + u2;
+                    // 1 / den: hardware reciprocal + two Newton steps (den in
+                    // [1, inf): no scaling or special cases needed)
+                    double d = __builtin_amdgcn_rcp(den);
+                    d = fma(d, fma(-den, d, 1.0), d);
+                    d = fma(d, fma(-den, d, 1.0), d);
+                    const double ud = uu * d;
+                    const double2 z1 = cmk(fma(y.x, d, -y.y * ud), fma(y.y, d, y.x * ud));
+                    const double2 z2 = cmk(fma(z1.x, d, -z1.y * ud), fma(z1.y, d, z1.x * ud));
+                    const double z3 = fma(z2.x, d, -z2.y * ud);
+                    a0 += z1.x;
+                    a1 = fma(kk, z1.y, a1);
+                    a2 = fma(kk * kk, z1.x, a2);
+                    q1 = fma(-uu, z2.y, q1);
+                    q1p = fma(kk * uu, z2.x, q1p);
+                    q2 = fma(-u2, z3, q2);
+                    const double Pk = pv[u] * inv_e2;
                     s0 = fma(d, Pk, s0);
-                    s1 = fma(2.0 * fma(B.x, be.x, B.y * be.y), Pk, s1);
-                    s2a = fma(2.0 * cabs2(be), Pk, s2a);
-                    s2b = fma(2.0 * fma(B.x, be2.x, B.y * be2.y), Pk, s2b);
+                    const double tp = u2 * d * d * Pk;
+                    t1 += tp;
+                    t2 = fma(tp * d, 1.0 - u2, t2);
                 }
                 E = cmul(E, W);
             }
-        }
-        double r0 = wave_sum(a0), r1 = -kTwoPi * wave_sum(a1);
-        double r2 = -kTwoPi * kTwoPi * wave_sum(a2);
-        if (lane == n - c0) { my[0] = r0; my[1] = r1; my[2] = r2; }
-        if (SCAT) {
-            double r3 = wave_sum(q1), r4 = -kTwoPi * wave_sum(q1p), r5 = wave_sum(q2);
-            double r6 = wave_sum(s0), r7 = wave_sum(s1), r8 = wave_sum(s2a), r9 = wave_sum(s2b);
-            if (lane == n - c0) {
-                my[3] = r3; my[4] = r4; my[5] = r5; my[6] = r6; my[7] = r7; my[8] = r8; my[9] = r9;
+#pragma unroll
+            for (int u = 0; u < KB; ++u) {
+                xv[u] = xn[u];
+                pv[u] = pn[u];
+                xn[u] = xn2[u];
+                pn[u] = pn2[u];
             }
-        } else if (lane == n - c0) {
+        }
+        double my[10];
+        my[0] = a0; my[1] = -kTwoPi * a1; my[2] = -kTwoPi * kTwoPi * a2;
+        if (SCAT) {
+            my[3] = q1; my[4] = -kTwoPi * q1p; my[5] = q2;
+            my[6] = s0; my[7] = -2.0 * t1; my[8] = 2.0 * t1; my[9] = -2.0 * t2;
+        } else {
+            my[3] = my[4] = my[5] = my[7] = my[8] = my[9] = 0.0;
             my[6] = chan[n * 4 + 3];
         }
-    }
-    // lane l owns channel c0 + l (l < kWaveChans)
-    const int n = c0 + lane;
-    if (lane < kWaveChans && n < c1 && (!mask || mask[n])) {
         double *dst = stats + (int64_t)n * 10;
 #pragma unroll
         for (int q = 0; q < 10; ++q) dst[q] = my[q];
         const double C = my[0], Sn = my[6], iS = 1.0 / Sn;
         if (!SCAT) {
-            const double nu = fr[n];
             const double dph[3] = {1.0, kDconst * (pow(nu, -2.0) - nuDM2) / g.P,
                                    kDconst * kDconst * (pow(nu, -4.0) - nuGM4) / g.P};
             const double Cp = my[1], Cpp = my[2];
@@ -375,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_pass(SolveArgs a) {
                     if (flagmask >> j & 1) acc[6 + uidx(i, j)] = hn * dph[i] * dph[j];
             }
         } else {
-            Fac fc = make_fac(fr[n], g, alpha);
+            Fac fc = make_fac(nu, g, alpha);
             double dC[5], dS[5], d2C[5][5], d2S[5][5];
             chan_derivs(my, fc, dC, dS, d2C, d2S);
             const double iS2 = iS * iS, iS3 = iS2 * iS, C2 = C * C;
@@ -539,8 +584,8 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
         const double t4 = __shfl(lane == 0 ? S.th[4] : 0.0, 0, 64);
         const double tl = a.log10_tau ? pow(10.0, t3) : t3;
         int gs, gt, ga;
-        wave_gates(a.freqs + (int64_t)s * a.nchan, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
-                   a.nchan, tl, t4, S.nu_fit[2], a.log10_tau, gs, gt, ga);
+        wave_gates(a.dphi + (int64_t)s * a.nchan * 2, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
+                   a.nchan, tl, t4, a.log10_tau, gs, gt, ga);
         if (lane == 0) { S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga; }
     }
 }
@@ -590,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
         phin = c0 + c1 * dp[0] + c2 * dp[1];
         if (kk == 0) a.mres[((int64_t)s * 2 + q) * a.nchan + n] = 0.0;   // exact centre
     }
-    const double2 *Xr = a.X + ((int64_t)s * a.nchan + (valid ? n : 0)) * nharm;
+    const double2 *Xr = a.X + (int64_t)s * nharm * a.nchan + (valid ? n : 0);   // X[s][k][n]
     const double2 W4 = cexp2pi(4.0 * phin);
     f64x4 dre0 = {0.0, 0.0, 0.0, 0.0}, dre1 = dre0, dim0 = dre0, dim1 = dre0;
     double2 E = cmk(1.0, 0.0);
@@ -601,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
 #pragma unroll
         for (int t = 0; t < KU; ++t) {
             const int k = kb + 4 * t + kk;
-            xv[t] = (valid && k < nharm) ? Xr[k] : cmk(0.0, 0.0);
+            xv[t] = (valid && k < nharm) ? Xr[(int64_t)k * a.nchan] : cmk(0.0, 0.0);
         }
 #pragma unroll
         for (int t = 0; t < KU; ++t) {
@@ -1256,11 +1301,6 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
 // ===========================================================================
 // launchers
 // ===========================================================================
-static int pass_unroll(int nharm) {
-    int j = (nharm + 63) / 64;
-    return j >= 17 ? 17 : j >= 9 ? 9 : j >= 5 ? 5 : j >= 3 ? 3 : j >= 2 ? 2 : 1;
-}
-
 hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
                            int moments, uint8_t *needx, hipStream_t st) {
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((nsub + 255) / 256)), dim3(256), 0, st, nsub,
@@ -1276,14 +1316,7 @@ hipError_t launch_tr_init(const SolveArgs &a, hipStream_t st) {
 
 template <bool SCAT>
 static void launch_pass_t(const SolveArgs &a, hipStream_t st, dim3 g) {
-    switch (pass_unroll(a.nbin / 2 + 1)) {
-        case 1: hipLaunchKernelGGL((k_pass<SCAT, 1>), g, dim3(kBlock), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_pass<SCAT, 2>), g, dim3(kBlock), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((k_pass<SCAT, 3>), g, dim3(kBlock), 0, st, a); break;
-        case 5: hipLaunchKernelGGL((k_pass<SCAT, 5>), g, dim3(kBlock), 0, st, a); break;
-        case 9: hipLaunchKernelGGL((k_pass<SCAT, 9>), g, dim3(kBlock), 0, st, a); break;
-        default: hipLaunchKernelGGL((k_pass<SCAT, 17>), g, dim3(kBlock), 0, st, a); break;
-    }
+    hipLaunchKernelGGL((k_pass<SCAT>), g, dim3(kBlock), 0, st, a);
 }
 
 hipError_t launch_pass(const SolveArgs &a, hipStream_t st) {

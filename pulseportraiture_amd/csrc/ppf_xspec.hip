@@ -94,12 +94,16 @@ __device__ __forceinline__ void rfft_pair(const double2 *buf, int k, double2 w, 
 // ===========================================================================
 // k_xspec_w: cross spectrum X of the sub-ints that stream it
 // ===========================================================================
+template <int LOG2N>
+__host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + 2; }
+
 template <int LOG2N, int DT>
 __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
-    constexpr int SL = wfft::buf_slots<LOG2N>();      // padded wave buffer
+    constexpr int SL = xspec_slw<LOG2N>();           // padded wave buffer + 2 side slots
+    constexpr int XNYQ = SL - 2;                      // X_{N/2} of the row
     using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -118,6 +122,10 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     // rfft post-pass twiddles w_k = exp(-i pi k / N), k = lane + 64 i, by
     // recurrence from w_lane (T2) with step exp(-i pi 64 / N) = T2[64]
     const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    // X[s][k][n] (harmonic-major: k_pass lanes are channels).  Each round the
+    // 8 rows' X are left in the wave buffers and written out together, 8
+    // channels x 16 B = one 128-B line per harmonic.
+    double2 *Xs = a.X + (int64_t)s * NH * a.nchan;
 
     auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
     RowT zr[R];
@@ -134,72 +142,92 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
             if (lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
             if (usable(n + kXW)) fetch(n + kXW);
         }
-        if (!live) continue;
-        const int64_t crow = (int64_t)s * a.nchan + n;
-        double2 x[R];
+        if (live) {
+            const int64_t crow = (int64_t)s * a.nchan + n;
+            double2 x[R];
 #pragma unroll
-        for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-        if (usable(n + kXW)) fetch(n + kXW);       // next row in flight during this FFT
-        wfft::fft_row<LOG2N>(x, buf, a.T, lane);
+            for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+            if (usable(n + kXW)) fetch(n + kXW);       // next row in flight during this FFT
+            wfft::fft_row<LOG2N>(x, buf, a.T, lane);
 
-        // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
-        double pn = 0.0, pd = 0.0;
-        {
-            double2 w = w_seed;
+            // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
+            double pn = 0.0, pd = 0.0;
+            {
+                double2 w = w_seed;
 #pragma unroll
-            for (int i = 0; i < NP; ++i) {
-                const int klo = lane + 64 * i, khi = N - klo;
-                double2 Dlo, Dhi;
-                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
-                w = cmul(w, w_step);
-                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
-                if (klo >= a.kc) pn += p0;
-                if (khi >= a.kc) pn += p1;
-                if (klo >= 1) pd += p0;
-                pd += p1;
-                SCHED_CUT();
+                for (int i = 0; i < NP; ++i) {
+                    const int klo = lane + 64 * i, khi = N - klo;
+                    double2 Dlo, Dhi;
+                    rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                    w = cmul(w, w_step);
+                    const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                    if (klo >= a.kc) pn += p0;
+                    if (khi >= a.kc) pn += p1;
+                    if (klo >= 1) pd += p0;
+                    pd += p1;
+                    SCHED_CUT();
+                }
+            }
+            double2 Dm = cmk(0.0, 0.0);
+            if (lane == 0) {
+                const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
+                Dm = cmk(zm.x, -zm.y);
+                const double p = cabs2(Dm);
+                if (N / 2 >= a.kc) pn += p;
+                pd += p;
+            }
+            pn = wave_sum(pn);
+            pd = wave_sum(pd);
+            double errs_FT;
+            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            {
+                // in place: X_k -> pad(k), X_{N-k} -> pad(N-k); the pair
+                // (0, N) keeps X_N in pad(N/2) (read above as Dm)
+                double2 w = w_seed;
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+                    const int klo = lane + 64 * i, khi = N - klo;
+                    double2 Dlo, Dhi;
+                    rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                    w = cmul(w, w_step);
+                    const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
+                    buf[wfft::pad<LOG2N>(klo)] =
+                        (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
+                    buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
+                        cscale(cmulc(Dhi, Mhi), inv_e2);
+                    SCHED_CUT();
+                }
+            }
+            if (lane == 0) {
+                buf[XNYQ] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
+                double *chan = a.chan + crow * 4;
+                chan[0] = errs_FT;
+                chan[1] = inv_e2;
+                chan[2] = pd * inv_e2;                                  // Sd_n
+                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
             }
         }
-        double2 Dm = cmk(0.0, 0.0);
-        if (lane == 0) {
-            const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
-            Dm = cmk(zm.x, -zm.y);
-            const double p = cabs2(Dm);
-            if (N / 2 >= a.kc) pn += p;
-            pd += p;
-        }
-        pn = wave_sum(pn);
-        pd = wave_sum(pd);
-        double errs_FT;
-        if (a.errs) errs_FT = a.errs[crow] * sqrtN;
-        else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
-        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-
-        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-        double2 *Xrow = a.X + crow * NH;
+        __syncthreads();
+        // write-out: thread t -> channel c = t % 8 of the round, harmonics
+        // k = t / 8 + 64 j
         {
-            double2 w = w_seed;
-#pragma unroll
-            for (int i = 0; i < NP; ++i) {
-                const int klo = lane + 64 * i, khi = N - klo;
-                double2 Dlo, Dhi;
-                rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
-                w = cmul(w, w_step);
-                const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
-                Xrow[klo] = (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
-                Xrow[khi] = cscale(cmulc(Dhi, Mhi), inv_e2);
-                SCHED_CUT();
+            const int c = threadIdx.x & 7, n0 = cbase + r * kXW;
+            const int nc = n0 + c;
+            if (nc < cend) {
+                const bool ok = !mask || mask[nc];
+                const double2 *b = lds + c * SL;
+                for (int k = threadIdx.x >> 3; k < NH; k += 64 * kXW / 8) {
+                    const int slot = k == N ? wfft::pad<LOG2N>(N / 2)
+                                            : (k == N / 2 ? XNYQ : wfft::pad<LOG2N>(k));
+                    Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);
+                }
             }
         }
-        if (lane == 0) {
-            Xrow[N / 2] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
-            double *chan = a.chan + crow * 4;
-            chan[0] = errs_FT;
-            chan[1] = inv_e2;
-            chan[2] = pd * inv_e2;                                  // Sd_n
-            chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
-        }
-        wfft::wave_sync();
+        __syncthreads();
     }
 }
 
@@ -590,7 +618,7 @@ __global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan
 // ===========================================================================
 template <int L2, int DT>
 static void launch_w(const XspecArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)kXW * wfft::buf_slots<L2>() * sizeof(double2);
+    const size_t lds = (size_t)kXW * xspec_slw<L2>() * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kXW);
     hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
 }
@@ -653,6 +681,33 @@ hipError_t launch_model_pow(const double2 *Mft, int nchan, int nharm, int nmodel
     const int nrows = nchan * nmodel;
     hipLaunchKernelGGL(k_model_pow, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, Mft, nrows,
                        nharm, out);
+    return hipGetLastError();
+}
+
+// |M_nk|^2 in harmonic-major layout for the scattering pass: 64 x 4 tiles
+// through LDS (reads along k, writes along n)
+__global__ __launch_bounds__(256) void k_model_pow_t(const double2 *Mft, int nchan, int nharm,
+                                                     double *MP) {
+    __shared__ double t[64][65];
+    const int m = blockIdx.z;
+    const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+    const double2 *M = Mft + (int64_t)m * nchan * nharm;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int nl = i >> 6, kl = i & 63, n = n0 + nl, k = k0 + kl;
+        t[nl][kl] = (n < nchan && k < nharm && k > 0) ? cabs2(M[(int64_t)n * nharm + k]) : 0.0;
+    }
+    __syncthreads();
+    double *out = MP + (int64_t)m * nharm * nchan;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int kl = i >> 6, nl = i & 63, n = n0 + nl, k = k0 + kl;
+        if (n < nchan && k < nharm) out[(int64_t)k * nchan + n] = t[nl][kl];
+    }
+}
+
+hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmodel, double *MP,
+                              hipStream_t st) {
+    dim3 g((unsigned)((nharm + 63) / 64), (unsigned)((nchan + 63) / 64), (unsigned)nmodel);
+    hipLaunchKernelGGL(k_model_pow_t, g, dim3(256), 0, st, Mft, nchan, nharm, MP);
     return hipGetLastError();
 }
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+# bench.py under several library variants: tools/var_bench.sh TAG "<bench args>" lib1.so [lib2.so ...]
+# -> gpurun_out/vb_TAG_<name>.log (one JSON line each)
+export TMPDIR=/tmp
+tag=$1; args=$2; shift 2
+for lib in "$@"; do
+  name=$(basename $lib .so)
+  PPFIT_LIB=$lib timeout -k 10 240 python bench.py $args --cpu-sample 0 > gpurun_out/vb_${tag}_$name.log 2>&1 || { echo "FAIL $lib"; exit 1; }
+  echo "$name $(grep '^{' gpurun_out/vb_${tag}_$name.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['stage_ms'])")"
+done

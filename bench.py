@@ -46,11 +46,12 @@ def parse():
     ap.add_argument("--chunk", type=int, default=2500,
                     help="sub-integrations per ppf_fit_batch call")
     ap.add_argument("--fit", default="phase+DM",
-                    choices=["phase+DM", "full", "scat"],
+                    choices=["phase+DM", "full", "scat", "align"],
                     help="phase+DM: configs[1] (the metric); full: configs[2] "
                     "fit (phi, DM, GM, tau, alpha) on data with injected "
                     "scattering; scat: configs[4] fit (phi, DM, tau, alpha), "
-                    "CHIME-like band")
+                    "CHIME-like band; align: configs[3] ppalign iteration "
+                    "(--nsub archives, default shape 256 x 1024)")
     ap.add_argument("--cpu-sample", type=int, default=48,
                     help="sub-integrations for the CPU baseline (0: skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
@@ -84,8 +85,85 @@ def O_DM0():
     return DM0
 
 
+def bench_align(args):
+    """configs[3]: ppalign.align_archives iterations over --nsub tscrunched
+    archives (256 ch x 1024 bin by default).  One step = one iteration: the
+    batched guess + phase/DM fit of every archive against the current
+    template, the weighted rotate-and-sum (ppf_align_accum), normalisation,
+    (+ the all-reduce of the portrait at N > 1).  Sharded by archive."""
+    import torch
+    from types import SimpleNamespace
+    from pulseportraiture_amd import dist, engine, ppalign, synth
+    from pulseportraiture_amd.pplib import guess_fit_freq
+    rank, world, local = dist.init("nccl")
+    dev = torch.device("cuda", local)
+    total = args.nsub * world
+    first, count = dist.shard(total, rank, world)
+    nchan, nbin = args.nchan, args.nbin
+    b = synth.make_batch(count, nchan, nbin, first=first, dev=dev)
+    noise = engine.noise_rows(b["data"]).cpu().numpy()     # get_noise_PS
+    freqs = np.tile(b["freqs"], (count, 1))
+    R = SimpleNamespace(
+        n=count, data=b["data"][:, None], freqs=freqs,
+        mask=np.ones((count, nchan), np.uint8), errs=noise,
+        gw=np.ones((count, nchan)), P=b["P"],
+        DM_guess=np.full(count, synth.DM0),
+        nu_fit=np.full(count, guess_fit_freq(b["freqs"])),
+        nchanx=np.full(count, nchan))
+    # initial template: archive 0's mean profile tiled (SURVEY.md C4)
+    prof = b["data"][0].double().mean(dim=0).cpu().numpy()
+    model0 = np.tile(prof, (nchan, 1))
+    comm = dist.is_dist()
+
+    def step(model_port):
+        out = torch.zeros((nchan, nbin), dtype=torch.float64, device=dev)
+        wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
+        ph, w = ppalign._fit_and_weights(R, model_port, True, nbin, dev)
+        engine.align_accum(R.data[:, 0], ph, w, out, wsum, dev=dev)
+        if comm:
+            dist.allreduce_sum_(out, wsum)
+        good = wsum > 0
+        out[good] /= wsum[good][:, None]
+        return out.cpu().numpy()
+
+    m = model0
+    for _ in range(args.warmup):
+        m = step(m)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    m = model0 if args.warmup == 0 else m
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step(m)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    dt = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    value = total * args.steps / dt
+    out = dict(metric="archive fits+aligns/sec (ppalign iteration, %dch×"
+                      "%dbin) at 1/2/4/8 MI355X" % (nchan, nbin),
+               value=round(value, 2), unit="archive-iterations/s",
+               n_gpus=world, steps=args.steps, warmup=args.warmup,
+               ms_per_step=round(dt / args.steps * 1e3, 3),
+               higher_is_better=True, scaling="weak", vs_baseline=None,
+               dtype="f64", data="synthetic (device-generated example.gmodel "
+               "archives, float32)",
+               config=dict(workload="configs[3]: %d tscrunched archives/GPU x "
+                           "%dch x %dbin, ppalign iteration (phase+DM fit + "
+                           "weighted rotate-and-sum)" % (args.nsub, nchan,
+                                                          nbin),
+                           nsub_per_gpu=args.nsub, nchan=nchan, nbin=nbin,
+                           fit="align", parallelism="dp%d" % world),
+               roofline=None, cpu_baseline=None,
+               template_peak=float(np.abs(m).max()))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+
+
 def main():
     args = parse()
+    if args.fit == "align":
+        return bench_align(args)
     import torch
     from pulseportraiture_amd import _lib, dist, engine, synth
     from pulseportraiture_amd.pplib import guess_fit_freq

@@ -174,6 +174,21 @@ int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
                      int32_t in_dtype, const void *in, const double *phases,
                      double *out, void *stream);
 
+/* ppalign.align_archives accumulation (ppalign.py:236-247, the inner
+ * "aligned_port += weights * rotate_data(...)" / "total_weights += weights"
+ * over every sub-integration of every archive):
+ *   out[n][:] += sum_s w[s][n] * irfft(rfft(in[s][n]) * exp(2 pi i k ph[s][n]))
+ *   wsum[n]   += sum_s w[s][n]
+ * Rows with w == 0 are skipped.  in: [nsub][nchan][nbin] (in_dtype);
+ * phases, weights: [nsub][nchan]; out: [nchan][nbin] f64; wsum: [nchan].
+ * The sum over sub-ints is taken in a fixed order (bitwise reproducible).
+ * workspace: device scratch of ppf_align_workspace_bytes() bytes. */
+size_t ppf_align_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin);
+int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                    int32_t in_dtype, const void *in, const double *phases,
+                    const double *weights, double *out, double *wsum,
+                    void *workspace, size_t workspace_bytes, void *stream);
+
 /* Per-row power-spectrum noise: pplib.get_noise_PS(chans=True)
  * (pplib.py:2312-2332): sqrt(mean(|rfft(x)|^2/nbin over k >= int((1-1/frac)
  * * nharm))).  in: [nrows][nbin]; out: [nrows]. */

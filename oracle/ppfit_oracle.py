@@ -17,7 +17,7 @@ __all__ = [
     "DCONST", "F0_FACT", "get_bin_centers", "noise_ps", "phase_transform",
     "guess_fit_freq", "channel_terms", "objective", "gradient", "hessian",
     "fit_portrait_full", "fit_portrait", "rotate_rows", "rotate_data",
-    "fit_phase_shift", "nu_zeros", "get_toas_archive",
+    "fit_phase_shift", "nu_zeros", "get_toas_archive", "align_archives",
 ]
 
 DCONST = 0.000241 ** -1          # pplib.py:64-67 (Dconst = Dconst_trad)
@@ -684,3 +684,75 @@ def get_toas_archive(subints, models, freqs, weights, SNRs, Ps, DM_stored,
     out["DeltaDM_mean"] = mean
     out["DeltaDM_err"] = var ** 0.5
     return out
+
+
+# ---------------------------------------------------------------------------
+# ppalign.align_archives (ppalign.py:65-257), the iteration only: archives
+# come in as DataBunch-like objects (the keys of pplib.py:2904-2914), no
+# archive I/O, no output archive.
+# ---------------------------------------------------------------------------
+def align_archives(archives, model_data, fit_dm=True, niter=1, npol=1):
+    """archives: list of objects with .subints [nsub, npol, nchan, nbin],
+    .weights, .freqs, .Ps, .SNRs, .noise_stds, .ok_isubs, .ok_ichans, .DM,
+    .dmc, .nbin; model_data likewise (one sub-int).  Returns (aligned_port
+    [npol, nchan, nbin], total_weights [nchan, nbin])."""
+    model_port = (model_data.masks * model_data.subints)[0, 0]
+    nchan, nbin = model_port.shape
+    for _ in range(niter):
+        aligned_port = np.zeros((npol, nchan, nbin))
+        total_weights = np.zeros((nchan, nbin))
+        for data in archives:
+            try:
+                fd = data.freqs - model_data.freqs
+                same_freqs = fd.min() == fd.max() == 0.0
+            except Exception:
+                same_freqs = False
+            DM_guess = data.DM * np.logical_not(data.dmc)
+            for isub in data.ok_isubs:
+                if same_freqs:
+                    ichans = np.intersect1d(data.ok_ichans[isub],
+                                            model_data.ok_ichans[0])
+                    model_ichans = ichans
+                else:
+                    ichans = data.ok_ichans[isub]
+                    mok = model_data.ok_ichans[0]
+                    model_ichans = np.array([
+                        mok[np.argmin(abs(model_data.freqs[0][mok] -
+                                          data.freqs[isub, ic]))]
+                        for ic in ichans])
+                port = data.subints[isub, 0, ichans]
+                freqs = data.freqs[isub, ichans]
+                model = model_port[model_ichans]
+                P = data.Ps[isub]
+                SNRs = data.SNRs[isub, 0, ichans]
+                errs = data.noise_stds[isub, 0, ichans]
+                nu_fit = guess_fit_freq(freqs, SNRs)
+                rot_port = rotate_data(port, 0.0, DM_guess, P, freqs, nu_fit)
+                phase_guess = fit_phase_shift(
+                    np.average(rot_port, axis=0,
+                               weights=data.weights[isub, ichans]),
+                    model.mean(axis=0), Ns=nbin)["phase"]
+                if len(freqs) > 1:
+                    flags = [1, int(bool(fit_dm)), 0, 0, 0]
+                    r = fit_portrait_full(port, model,
+                                          [phase_guess, DM_guess, 0.0, 0.0,
+                                           0.0], P, freqs, [nu_fit] * 3,
+                                          [None] * 3, errs, flags,
+                                          log10_tau=False)
+                    phase, DM, nu_ref = r["phi"], r["DM"], r["nu_DM"]
+                    scales = r["scales"]
+                else:
+                    r = fit_phase_shift(port[0], model[0], errs[0], Ns=nbin)
+                    phase, DM, nu_ref = r["phase"], data.DM, freqs[0]
+                    scales = np.array([r["scale"]])
+                weights = np.outer(scales / errs ** 2, np.ones(nbin))
+                for ipol in range(npol):
+                    aligned_port[ipol, model_ichans] += weights * rotate_data(
+                        data.subints[isub, ipol, ichans], phase, DM, P, freqs,
+                        nu_ref)
+                total_weights[model_ichans] += weights
+        good = np.where(total_weights > 0)[0]
+        for ipol in range(npol):
+            aligned_port[ipol, good] /= total_weights[good]
+        model_port = aligned_port[0]
+    return aligned_port, total_weights

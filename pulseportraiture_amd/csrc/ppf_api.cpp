@@ -433,6 +433,45 @@ int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype
     return PPF_OK;
 }
 
+size_t ppf_align_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin) {
+    if (nsub <= 0 || nchan <= 0 || nbin <= 0) return 0;
+    const size_t g = (size_t)ppf::align_groups(nsub, nchan);
+    return align256(g * nchan * (size_t)(nbin / 2 + 1) * sizeof(double2)) +
+           align256(g * nchan * sizeof(double));
+}
+
+int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int32_t in_dtype,
+                    const void *in, const double *phases, const double *weights, double *out,
+                    double *wsum, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nsub < 0 || nchan <= 0) return fail(ctx, PPF_EINVAL, "bad align shape");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (nsub == 0) return PPF_OK;
+    if (!in || !phases || !weights || !out || !wsum || !workspace)
+        return fail(ctx, PPF_EINVAL, "null align argument");
+    const size_t need = ppf_align_workspace_bytes(nsub, nchan, nbin);
+    if (workspace_bytes < need)
+        return fail(ctx, PPF_ENOMEM, "align workspace %zu < %zu bytes", workspace_bytes, need);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    ppf::AlignArgs a{};
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = in_dtype;
+    a.ngroup = ppf::align_groups(nsub, nchan);
+    a.in = in; a.phases = phases; a.weights = weights; a.T = T; a.T2 = T2;
+    char *ws = (char *)workspace;
+    a.part = (double2 *)ws;
+    a.wpart = (double *)(ws + align256((size_t)a.ngroup * nchan * (size_t)(nbin / 2 + 1) *
+                                        sizeof(double2)));
+    a.out = out; a.wsum = wsum;
+    if ((e = ppf::launch_align(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_align");
+    return PPF_OK;
+}
+
 int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
                     int32_t frac, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;

@@ -112,6 +112,22 @@ struct RotateArgs {
     double *out;
 };
 
+// ppalign accumulation (ppalign.py:236-247): per channel, sum_s w_sn *
+// rotate(x_sn, phase_sn), done in the frequency domain
+struct AlignArgs {
+    int nsub, nchan, nbin, log2N, dtype, ngroup;
+    const void *in;              // [nsub][nchan][nbin]
+    const double *phases;        // [nsub][nchan]
+    const double *weights;       // [nsub][nchan]
+    const double2 *T, *T2;
+    double2 *part;               // [ngroup][nchan][N+1] partial spectra
+    double *wpart;               // [ngroup][nchan] partial weight sums
+    double *out;                 // [nchan][nbin] (accumulated into)
+    double *wsum;                // [nchan]      (accumulated into)
+};
+int align_groups(int nsub, int nchan);
+hipError_t launch_align(const AlignArgs &a, hipStream_t st);
+
 struct NoiseArgs {
     int nbin, log2N, dtype, kc;
     const void *in;

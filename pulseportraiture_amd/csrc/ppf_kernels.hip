@@ -791,6 +791,122 @@ hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st) {
     }
     return hipGetLastError();
 }
+// ===========================================================================
+// ppalign accumulation.  k_align_part: workgroup = (channel n, group g of
+// sub-ints); for each of its sub-ints in order, rfft of the row, times
+// w exp(2 pi i k phase), summed in registers (the rotate-then-sum of the
+// reference is linear, so the sum is taken before the single inverse FFT).
+// k_align_fin: per channel, the group partials in group order, DC and
+// Nyquist imaginary parts dropped (as numpy irfft does), irfft, added to out.
+// ===========================================================================
+int align_groups(int nsub, int nchan) {
+    int g = (2048 + nchan - 1) / nchan;       // >= 2048 workgroups in flight
+    if (g > nsub) g = nsub;
+    return g < 1 ? 1 : g;
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int N = a.nbin >> 1;
+    const int n = blockIdx.x % a.nchan, g = blockIdx.x / a.nchan;
+    const int per = (a.nsub + a.ngroup - 1) / a.ngroup;
+    const int s0 = g * per, s1 = min(a.nsub, s0 + per);
+    double2 Ak[KMAX], An[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) Ak[i] = An[i] = cmk(0.0, 0.0);
+    double wtot = 0.0;
+    for (int s = s0; s < s1; ++s) {
+        const int64_t row = (int64_t)s * a.nchan + n;
+        const double w = a.weights[row];
+        if (w == 0.0) continue;                     // uniform per workgroup
+        const double ph = a.phases[row];
+        wtot += w;
+        load_row(lds, a.in, a.dtype, row, a.nbin);
+        __syncthreads();
+        lds_fft(lds, a.log2N, a.T, false);
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < N) {
+                const double2 X1 = cmul(rfft_bin(lds, N, a.T2, k), cexp2pi((double)k * ph));
+                const double2 X2 =
+                    cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
+                Ak[i] = cadd(Ak[i], cscale(X1, w));
+                An[i] = cadd(An[i], cscale(X2, w));
+            }
+        }
+        __syncthreads();
+    }
+    double2 *P = a.part + ((int64_t)g * a.nchan + n) * (N + 1);
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        const int k = threadIdx.x + i * kBlock;
+        if (k < N) {
+            P[k] = Ak[i];
+            if (k == 0) P[N] = An[i];               // (k, N - k) = (0, N)
+            else P[N - k] = An[i];
+        }
+    }
+    if (threadIdx.x == 0) a.wpart[(int64_t)g * a.nchan + n] = wtot;
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int N = a.nbin >> 1, n = blockIdx.x;
+    double2 Xk[KMAX], Xn[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        const int k = threadIdx.x + i * kBlock;
+        if (k < N) {
+            double2 s1 = cmk(0.0, 0.0), s2 = s1;
+            for (int g = 0; g < a.ngroup; ++g) {
+                const double2 *P = a.part + ((int64_t)g * a.nchan + n) * (N + 1);
+                s1 = cadd(s1, P[k]);
+                s2 = cadd(s2, P[N - k]);
+            }
+            if (k == 0) { s1.y = 0.0; s2.y = 0.0; }  // DC and Nyquist: real parts only
+            Xk[i] = s1;
+            Xn[i] = s2;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        const int k = threadIdx.x + i * kBlock;
+        if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+    }
+    __syncthreads();
+    lds_fft(lds, a.log2N, a.T, true);
+    const double sc = 1.0 / (double)N;
+    double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)n * N;
+    for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cadd(o[j], cscale(lds[j], sc));
+    if (threadIdx.x == 0) {
+        double w = 0.0;
+        for (int g = 0; g < a.ngroup; ++g) w += a.wpart[(int64_t)g * a.nchan + n];
+        a.wsum[n] += w;
+    }
+}
+
+hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    dim3 gp((unsigned)((int64_t)a.ngroup * a.nchan)), gf((unsigned)a.nchan), b(kBlock);
+    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+        case 1: hipLaunchKernelGGL(k_align_part<1>, gp, b, lds, st, a);
+                hipLaunchKernelGGL(k_align_fin<1>, gf, b, lds, st, a); break;
+        case 2: hipLaunchKernelGGL(k_align_part<2>, gp, b, lds, st, a);
+                hipLaunchKernelGGL(k_align_fin<2>, gf, b, lds, st, a); break;
+        case 4: hipLaunchKernelGGL(k_align_part<4>, gp, b, lds, st, a);
+                hipLaunchKernelGGL(k_align_fin<4>, gf, b, lds, st, a); break;
+        case 8: hipLaunchKernelGGL(k_align_part<8>, gp, b, lds, st, a);
+                hipLaunchKernelGGL(k_align_fin<8>, gf, b, lds, st, a); break;
+        case 16: hipLaunchKernelGGL(k_align_part<16>, gp, b, lds, st, a);
+                 hipLaunchKernelGGL(k_align_fin<16>, gf, b, lds, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     hipLaunchKernelGGL(k_noise, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);

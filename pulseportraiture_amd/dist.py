@@ -77,3 +77,17 @@ def max_over_ranks(x, device=None):
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def is_dist():
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
+def allreduce_sum_(*tensors):
+    """In-place sum over ranks (ppalign's aligned portrait and channel
+    weights: the one exchange of the alignment iteration)."""
+    if not is_dist():
+        return tensors
+    for t in tensors:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return tensors

@@ -176,6 +176,34 @@ def rotate_rows(rows, phases, dev=None):
     return out.reshape(shape)
 
 
+def align_accum(data, phases, weights, out, wsum, dev=None):
+    """ppalign accumulation on the device (ppf_align_accum):
+    out[n] += sum_s w[s,n] rotate(data[s,n], phases[s,n]); wsum[n] += sum_s
+    w[s,n].  data [nsub, nchan, nbin]; out [nchan, nbin] and wsum [nchan] are
+    float64 device tensors updated in place."""
+    dev = device(dev)
+    d = to_dev(data, dev, _data_dtype(data))
+    if d.dim() != 3:
+        raise ValueError("data must be [nsub, nchan, nbin]")
+    nsub, nchan, nbin = d.shape
+    ph = to_dev(phases, dev, torch.float64).reshape(nsub, nchan).contiguous()
+    w = to_dev(weights, dev, torch.float64).reshape(nsub, nchan).contiguous()
+    if out.shape != (nchan, nbin) or out.dtype != torch.float64 or \
+            wsum.shape != (nchan,) or wsum.dtype != torch.float64:
+        raise ValueError("out must be float64 [nchan, nbin], wsum [nchan]")
+    lib = _lib.load()
+    nbytes = lib.ppf_align_workspace_bytes(nsub, nchan, nbin)
+    ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = lib.ppf_align_accum(
+        ctx, nsub, nchan, nbin,
+        _lib.PPF_F32 if d.dtype == torch.float32 else _lib.PPF_F64,
+        _p(d), _p(ph), _p(w), _p(out), _p(wsum), _p(ws), int(nbytes),
+        _stream(dev))
+    _lib.check(rc, ctx)
+    return out, wsum
+
+
 def noise_rows(rows, frac=4, dev=None):
     """get_noise_PS per row of rows [..., nbin] -> [...] float64."""
     dev = device(dev)

@@ -1,0 +1,323 @@
+"""Drop-in mirror of PulsePortraiture's ``ppalign.align_archives``
+(ppalign.py:65-280): iterative phase/DM alignment and weighted averaging of
+homogeneous archives into a template portrait (BASELINE.json configs[3]).
+
+Per iteration the reference loops over archives and sub-integrations with
+one ``fit_portrait_full`` and one ``rotate_data`` each (ppalign.py:118-247).
+Here every usable sub-integration of every archive goes into ONE batched
+device fit (``ppf_fit_batch``: the ``fit_phase_shift(Ns=nbin)`` guess on the
+dedispersed weighted mean profile, the phase+DM wideband fit, ν₀, scales),
+and the weighted sum of the rotated sub-integrations is ONE device call
+(``ppf_align_accum``: rotation and accumulation in the frequency domain, a
+fixed summation order).  The data are loaded once and stay resident in HBM
+across iterations (the reference re-reads every archive every iteration).
+
+Multi-GPU: pass ``comm=True`` inside a ``torch.distributed`` job and give
+each rank its share of ``metafile``; the aligned portrait and the channel
+weights are summed across ranks with one all-reduce per iteration (RCCL over
+xGMI), the only exchange the algorithm has.
+
+Archive I/O stays on PSRCHIVE (``pptoas.load_data``, host side); the output
+archive is written through the template archive object exactly as
+ppalign.py:259-277 does when one is attached (``model_data.arch``).
+"""
+import numpy as np
+import torch
+
+from . import _lib, engine
+from . import pptoas as _pptoas
+from .pplib import (DataBunch, Dconst, fit_phase_shift, gaussian_profile,
+                    get_noise, guess_fit_freq, rotate_data)
+
+rm_baseline = _pptoas.rm_baseline       # ppalign.py imports it from pptoas
+
+
+def normalize_portrait(port, method="rms", weights=None, return_norms=False):
+    """pplib.py:2553-2600."""
+    if method not in ("mean", "max", "prof", "rms", "abs"):
+        print("Unknown method for normalize_portrait(...), '%s'." % method)
+        return None
+    port = np.asarray(port, dtype=np.float64)
+    norm_port = np.zeros(port.shape)
+    norm_vals = np.ones(len(port))
+    if method == "prof":
+        good = np.where(port.sum(axis=1) != 0.0)[0]
+        w = np.ones(len(good)) if weights is None else weights[good]
+        mean_prof = np.average(port[good], axis=0, weights=w)
+    for ichan in range(len(port)):
+        if port[ichan].any():
+            if method == "mean":
+                norm = port[ichan].mean()
+            elif method == "max":
+                norm = port[ichan].max()
+            elif method == "prof":
+                norm = fit_phase_shift(port[ichan], mean_prof).scale
+            elif method == "rms":
+                norm = get_noise(port[ichan])
+            else:
+                norm = (port[ichan] ** 2.0).sum() ** 0.5
+            norm_port[ichan] = port[ichan] / norm
+            norm_vals[ichan] = norm
+    if return_norms:
+        return norm_port, norm_vals
+    return norm_port
+
+
+def _load(name, state, tscrunch, pscrunch, quiet):
+    return _pptoas.load_data(name, state=state, dedisperse=False,
+                             tscrunch=tscrunch, pscrunch=pscrunch,
+                             fscrunch=False, rm_baseline=rm_baseline,
+                             flux_prof=False, refresh_arch=False,
+                             return_arch=False, quiet=quiet)
+
+
+def _usable(data, name, model_data, SNR_cutoff, quiet):
+    """The reference's per-archive skip tests (ppalign.py:155-185); returns
+    False to skip.  Channels with a NaN S/N are dropped in place."""
+    if data.nbin != model_data.nbin:
+        if not quiet:
+            print("%s: %d != %d phase bins.  Skipping it." %
+                  (name, data.nbin, model_data.nbin))
+        return False
+    if data.prof_SNR < SNR_cutoff:
+        if not quiet:
+            print("%s: %d < %d S/N cutoff.  Skipping it." %
+                  (name, data.prof_SNR, SNR_cutoff))
+        return False
+    if np.isnan(data.prof_SNR):
+        print("Profile has nan SNR, must skip")
+        return False
+    nnan = len(data.SNRs[np.isnan(data.SNRs)])
+    if nnan > 10:
+        print("More than 10 frequency channels with nan SNR")
+        return False
+    if nnan:
+        print("This file has %s frequency channels with a nan SNR" % nnan)
+        print(name)
+        for isub in data.ok_isubs:
+            for ipol in range(data.npol):
+                oc = np.array(data.ok_ichans[isub])
+                data.ok_ichans[isub] = oc[~np.isnan(data.SNRs[isub, ipol][oc])]
+    return True
+
+
+def _channel_map(data, isub, model_data, same_freqs):
+    """(ichans, model_ichans) of ppalign.py:192-207."""
+    if same_freqs:
+        ichans = np.intersect1d(data.ok_ichans[isub], model_data.ok_ichans[0])
+        return ichans, ichans
+    ichans = np.asarray(data.ok_ichans[isub])
+    mok = np.asarray(model_data.ok_ichans[0])
+    mch = np.array([mok[np.argmin(abs(model_data.freqs[0][mok] -
+                                      data.freqs[isub, ic]))]
+                    for ic in ichans], dtype=int)
+    return ichans, mch
+
+
+class _Rows(object):
+    """Every usable sub-integration of every archive, laid out in MODEL
+    channel order (row s, channel m = the data channel mapped onto model
+    channel m), device-resident."""
+
+    def __init__(self, archives, model_data, npol, dev):
+        nchan, nbin = model_data.nchan, model_data.nbin
+        rows, meta = [], []
+        for data in archives:
+            try:
+                fd = data.freqs - model_data.freqs
+                same = fd.min() == fd.max() == 0.0
+            except Exception:
+                same = False
+            DM_guess = data.DM * np.logical_not(data.dmc)
+            for isub in data.ok_isubs:
+                ichans, mch = _channel_map(data, isub, model_data, same)
+                if len(ichans) == 0:
+                    continue
+                # numpy fancy-index "+=" keeps the LAST of duplicate model
+                # channels (ppalign.py:244-247): keep that one
+                last = {}
+                for i, m in enumerate(mch):
+                    last[int(m)] = i
+                sel = np.array(sorted(last.values()), dtype=int)
+                ich, mch = ichans[sel], mch[sel]
+                x = np.zeros((npol, nchan, nbin), dtype=np.float32)
+                for ipol in range(npol):
+                    x[ipol, mch] = data.subints[isub, ipol, ich]
+                freqs = np.ones(nchan) * np.nan
+                freqs[mch] = data.freqs[isub, ich]
+                m = dict(mask=np.zeros(nchan, np.uint8), freqs=freqs,
+                         P=float(data.Ps[isub]), DM_guess=float(DM_guess),
+                         DM=float(data.DM), errs=np.ones(nchan),
+                         gw=np.zeros(nchan), nchanx=len(ich))
+                m["mask"][mch] = 1
+                m["errs"][mch] = data.noise_stds[isub, 0, ich]
+                m["gw"][mch] = data.weights[isub, ich]
+                m["nu_fit"] = guess_fit_freq(data.freqs[isub, ich],
+                                             data.SNRs[isub, 0, ich])
+                rows.append(x)
+                meta.append(m)
+        self.n = len(rows)
+        self.meta = meta
+        if self.n:
+            self.data = torch.as_tensor(np.stack(rows)).to(dev)   # [S, npol, nchan, nbin]
+        fill = np.nanmean([np.nanmean(m["freqs"]) for m in meta]) if meta else 1.0
+        self.freqs = np.array([np.where(np.isnan(m["freqs"]), fill, m["freqs"])
+                               for m in meta])
+        self.mask = np.array([m["mask"] for m in meta])
+        self.errs = np.array([m["errs"] for m in meta])
+        self.gw = np.array([m["gw"] for m in meta])
+        self.P = np.array([m["P"] for m in meta])
+        self.DM_guess = np.array([m["DM_guess"] for m in meta])
+        self.nu_fit = np.array([m["nu_fit"] for m in meta])
+        self.nchanx = np.array([m["nchanx"] for m in meta])
+
+
+def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
+    """One batched fit of every row against the current template: the
+    per-row rotation phases and weights of ppalign.py:222-247."""
+    S = R.n
+    nchan = model_port.shape[0]
+    phases = np.zeros((S, nchan))
+    weights = np.zeros((S, nchan))
+    multi = np.where(R.nchanx > 1)[0]
+    if len(multi):
+        rows = R.data[:, 0] if len(multi) == S else \
+            R.data[torch.as_tensor(multi, device=dev), 0]
+        init = np.zeros((len(multi), 5))
+        init[:, 1] = R.DM_guess[multi]
+        flags = [1, int(bool(fit_dm)), 0, 0, 0]
+        res = engine.fit_batch(
+            rows, model_port, R.freqs[multi], R.P[multi], init,
+            flags, nu_fits=np.repeat(R.nu_fit[multi, None], 3, axis=1),
+            nu_outs=np.full((len(multi), 3), np.nan), errs=R.errs[multi],
+            chan_mask=R.mask[multi], log10_tau=False, is_toa=True,
+            guess=True, guess_weights=R.gw[multi],
+            guess_DM=R.DM_guess[multi], guess_Ns=nbin, dev=dev)
+        r = engine.results_numpy(res)
+        I = _lib.RESULT_INDEX
+        st = r["results"][:, I["status"]].astype(np.int64)
+        bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
+        if len(bad):
+            from .pplib import _raise_status
+            _raise_status(int(st[bad[0]]))
+        phi = r["results"][:, I["params"]][:, 0]
+        DM = r["results"][:, I["params"]][:, 1]
+        nu_ref = r["results"][:, I["nu_out"]][:, 0]
+        ok = R.mask[multi] != 0
+        fr = R.freqs[multi]
+        ph = phi[:, None] + (Dconst * DM / R.P[multi])[:, None] * (
+            fr ** -2.0 - (nu_ref ** -2.0)[:, None])
+        phases[multi] = np.where(ok, ph, 0.0)
+        weights[multi] = np.where(ok, r["scales"] / R.errs[multi] ** 2, 0.0)
+    for s in np.where(R.nchanx == 1)[0]:      # 1-channel hack (ppalign.py:231-236)
+        m = int(np.where(R.mask[s])[0][0])
+        x = R.data[s, 0, m].double().cpu().numpy()
+        fr = fit_phase_shift(x, model_port[m], R.errs[s, m], Ns=nbin)
+        phases[s, m] = fr.phase          # DM = data.DM at nu_ref = freqs[0]: 0
+        weights[s, m] = fr.scale / R.errs[s, m] ** 2
+    return phases, weights
+
+
+def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
+                   pscrunch=True, SNR_cutoff=0.0, outfile=None, norm=None,
+                   rot_phase=0.0, place=None, niter=1, quiet=False,
+                   comm=False, dev=None):
+    """ppalign.py:65-280.  Returns a DataBunch(port=[npol, nchan, nbin]
+    aligned portrait, total_weights=[nchan, nbin], nit=niter) and, like the
+    reference, writes ``outfile`` through ``model_data.arch`` when the
+    template archive object is attached."""
+    if isinstance(metafile, str):
+        datafiles = [l[:-1] for l in open(metafile, "r").readlines()]
+        if outfile is None:
+            outfile = metafile + ".algnd.fits"
+    else:
+        datafiles = list(metafile)
+    state, npol = ("Intensity", 1) if pscrunch else ("Stokes", 4)
+    try:
+        model_data = _pptoas.load_data(
+            initial_guess, state=state, dedisperse=True, dededisperse=False,
+            tscrunch=True, pscrunch=pscrunch, fscrunch=False,
+            rm_baseline=True, flux_prof=False, refresh_arch=True,
+            return_arch=True, quiet=quiet)
+    except IndexError:
+        print("%s: has npol = 1; need npol == 4." % initial_guess)
+        raise SystemExit
+    nchan, nbin = model_data.nchan, model_data.nbin
+    model_port = np.asarray((model_data.masks * model_data.subints)[0, 0],
+                            dtype=np.float64)
+    dev = engine.device(dev)
+    # archives are read once and kept resident (the reference re-reads them
+    # every iteration; the skip tests give the same outcome each time)
+    archives = []
+    for name in datafiles:
+        try:
+            data = _load(name, state, tscrunch, pscrunch, quiet)
+        except RuntimeError:
+            if not quiet:
+                print("%s: cannot load_data().  Skipping it." % name)
+            continue
+        except IndexError:
+            if not quiet:
+                print("%s: has npol = 1.  Skipping it." % name)
+            continue
+        if _usable(data, name, model_data, SNR_cutoff, quiet):
+            archives.append(data)
+    R = _Rows(archives, model_data, npol, dev)
+    from . import dist as _dist
+    count = 1
+    while niter:
+        if not quiet:
+            print("Doing iteration %d..." % count)
+        out = torch.zeros((npol, nchan, nbin), dtype=torch.float64, device=dev)
+        wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
+        if R.n:
+            phases, weights = _fit_and_weights(R, model_port, fit_dm, nbin, dev)
+            for ipol in range(npol):
+                w = torch.zeros_like(wsum)
+                engine.align_accum(R.data[:, ipol], phases, weights, out[ipol],
+                                   wsum if ipol == 0 else w, dev=dev)
+        if comm:
+            _dist.allreduce_sum_(out, wsum)
+        good = wsum > 0
+        out[:, good] /= wsum[good][None, :, None]
+        aligned_port = out.cpu().numpy()
+        total_weights = np.outer(wsum.cpu().numpy(), np.ones(nbin))
+        model_port = aligned_port[0]
+        niter -= 1
+        count += 1
+    if norm in ("mean", "max", "prof", "rms", "abs"):
+        for ipol in range(npol):
+            aligned_port[ipol] = normalize_portrait(aligned_port[ipol], norm,
+                                                    weights=None)
+    if rot_phase:
+        aligned_port = rotate_data(aligned_port, rot_phase)
+    if place is not None:
+        prof = np.average(aligned_port[0], axis=0, weights=None)
+        delta = prof.max() * gaussian_profile(len(prof), place, 0.0001)
+        phase = fit_phase_shift(prof, delta, Ns=nbin).phase
+        aligned_port = rotate_data(aligned_port, phase)
+    try:
+        arch = model_data.arch
+    except (AttributeError, KeyError):
+        arch = None
+    if arch is not None and outfile is not None:    # ppalign.py:259-277
+        arch.tscrunch()
+        if pscrunch:
+            arch.pscrunch()
+        else:
+            arch.convert_state("Stokes")
+        arch.set_dispersion_measure(0.0)
+        for subint in arch:
+            for ipol in range(arch.get_npol()):
+                for ichan in range(arch.get_nchan()):
+                    prof = subint.get_Profile(ipol, ichan)
+                    prof.get_amps()[:] = aligned_port[ipol, ichan]
+                    if total_weights[ichan].sum() == 0.0:
+                        subint.set_weight(ichan, 0.0)
+                    else:
+                        subint.set_weight(ichan, 1.0)
+        arch.unload(outfile)
+        if not quiet:
+            print("\nUnloaded %s.\n" % outfile)
+    return DataBunch(port=aligned_port, total_weights=total_weights,
+                     nsub_fit=R.n)

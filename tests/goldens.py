@@ -117,3 +117,46 @@ def ref_bunch(c):
     return dict(params=c["out_params"], param_errs=c["out_param_errs"],
                 nu_DM=float(c["out_nu_DM"]), nu_GM=float(c["out_nu_GM"]),
                 nu_tau=float(c["out_nu_tau"]))
+
+
+class Bunch(dict):
+    """DataBunch stand-in (attribute access), as pplib.DataBunch."""
+    __getattr__ = dict.__getitem__
+
+
+def align():
+    z = _load("align.npz")
+    return Case({k: z[k] for k in z.files})
+
+
+def align_inputs(c=None):
+    """(archives, model_data) of the ppalign golden case, rebuilt exactly as
+    tests/golden/make_golden_align.py handed them to the reference."""
+    c = align() if c is None else c
+    nfile, nsub = int(c["nfile"]), int(c["nsub"])
+    nchan, nbin = int(c["nchan"]), int(c["nbin"])
+    freqs = c["freqs"]
+    P, DM0 = float(c["P"]), float(c["DM0"])
+    archives = []
+    for i in range(nfile):
+        sub = c["f%d_subints" % i].astype(np.float64)[:, None]
+        w = c["f%d_weights" % i]
+        wnorm = np.where(w == 0.0, 0.0, 1.0)
+        archives.append(Bunch(
+            DM=DM0, dmc=0, freqs=np.tile(freqs, (nsub, 1)),
+            masks=np.einsum("ij,k", wnorm, np.ones(nbin))[:, None],
+            nbin=nbin, nchan=nchan,
+            noise_stds=c["f%d_noise" % i][:, None], npol=1, nsub=nsub,
+            ok_ichans=[np.compress(wnorm[j], list(range(nchan)))
+                       for j in range(nsub)],
+            ok_isubs=np.arange(nsub), prof_SNR=100.0,
+            Ps=np.ones(nsub) * P, SNRs=c["f%d_snrs" % i][:, None],
+            subints=sub, weights=w, state="Intensity"))
+    model_data = Bunch(
+        DM=0.0, dmc=1, freqs=freqs[None, :], masks=np.ones([1, 1, nchan, nbin]),
+        nbin=nbin, nchan=nchan, noise_stds=np.ones([1, 1, nchan]), npol=1,
+        nsub=1, ok_ichans=[np.arange(nchan)], ok_isubs=np.arange(1),
+        prof_SNR=100.0, Ps=np.ones(1) * P, SNRs=np.ones([1, 1, nchan]),
+        subints=c["guess"][None, None], weights=np.ones([1, nchan]),
+        arch=None, state="Intensity")
+    return archives, model_data

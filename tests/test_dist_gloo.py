@@ -77,3 +77,52 @@ def test_shard_is_a_balanced_partition():
             for (f0, c0), (f1, _) in zip(got, got[1:]):
                 assert f0 + c0 == f1
             assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def _align_worker(rank, world, port, n_total, q):
+    """ppalign's exchange: each rank accumulates the weighted rotated rows of
+    its archives (oracle rotation on CPU), then allreduce_sum_ of the
+    portrait and the weights."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    pdist.init("gloo")
+    out, w = _align_partial(*pdist.shard(n_total, rank, world))
+    pdist.allreduce_sum_(out, w)
+    if rank == 0:
+        q.put((out.numpy(), w.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _align_partial(first, count, nchan=6, nbin=64):
+    import oracle as O
+    out = torch.zeros((nchan, nbin), dtype=torch.float64)
+    w = torch.zeros(nchan, dtype=torch.float64)
+    for g in range(first, first + count):
+        rng = np.random.default_rng(500 + g)
+        x = rng.normal(size=(nchan, nbin))
+        ph = rng.uniform(-0.5, 0.5, nchan)
+        wt = rng.uniform(0.5, 1.5, nchan)
+        out += torch.as_tensor(wt[:, None] * O.rotate_rows(x, ph))
+        w += torch.as_tensor(wt)
+    return out, w
+
+
+def test_align_allreduce_equals_serial():
+    n_total = 9
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_align_worker, args=(r, 2, port, n_total, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    out, w = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    ref, rw = _align_partial(0, n_total)
+    np.testing.assert_allclose(out, ref.numpy(), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(w, rw.numpy(), rtol=1e-14)

@@ -150,3 +150,18 @@ def test_host_gmodel_matches_reference_model():
         ref = c["model"].astype(np.float64)
         ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
         assert np.all(np.abs(model - ref) <= ulp + 1e-12)
+
+
+def test_oracle_align_archives_matches_reference():
+    """The oracle's ppalign iteration (restated from ppalign.py:118-257)
+    reproduces the reference's aligned portrait (2 iterations, 5 archives x 2
+    sub-ints, one archive with zapped channels)."""
+    import oracle as O
+    c = G.align()
+    archives, model_data = G.align_inputs(c)
+    port, tw = O.align_archives(archives, model_data, fit_dm=True,
+                                niter=int(c["niter"]))
+    ref = c["out_aligned"]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(port[0], ref, rtol=0, atol=1e-6 * scale)
+    np.testing.assert_array_equal(tw[:, 0] > 0, c["out_weights"] > 0)

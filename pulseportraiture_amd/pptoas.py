@@ -525,3 +525,200 @@ class GetTOAs(object):
                                             ).sum()))
         if not already_warned:
             pass
+
+    def get_narrowband_TOAs(self, datafile=None, tscrunch=False,
+                            fit_scat=False, log10_tau=True, scat_guess=None,
+                            print_phase=False, print_flux=False,
+                            print_parangle=False,
+                            add_instrumental_response=False,
+                            addtnl_toa_flags={}, method="trust-ncg",
+                            bounds=None, show_plot=False, quiet=None):
+        """pptoas.py:794-1189: one FFTFIT (fit_phase_shift, Ns=100) per usable
+        channel of every sub-integration; all the channels of an archive are
+        fitted in ONE batched device call (ppf_phase_shift_batch, the model
+        row of each channel selected by index), then the reference's TOA
+        bookkeeping per channel.  The reference's own fit_scat branch is
+        unreachable (its rot_prof / nu_fit_tau are undefined there,
+        pptoas.py:1001-1017); it raises here."""
+        if quiet is None:
+            quiet = self.quiet
+        if fit_scat:
+            raise NameError("name 'nu_fit_tau' is not defined "
+                            "(pptoas.py:1002, the reference's narrowband "
+                            "scattering branch is incomplete)")
+        if add_instrumental_response and (self.ird["DM"] or
+                                          len(self.ird["wids"])):
+            raise NotImplementedError("instrumental response (SURVEY.md row "
+                                      "19) is not on the accelerated path")
+        print("You are using an experimental functionality of pptoas!")
+        self.nfit = 1
+        self.fit_phi = True
+        self.fit_tau = fit_scat
+        self.fit_flags = [int(self.fit_phi), int(self.fit_tau)]
+        self.log10_tau = log10_tau = False
+        self.scat_guess = scat_guess
+        start = time.time()
+        datafiles = self.datafiles if datafile is None else [datafile]
+        self.tscrunch = tscrunch
+        self.add_instrumental_response = add_instrumental_response
+        for iarch, datafile in enumerate(datafiles):
+            fit_duration = 0.0
+            try:
+                data = load_data(datafile, dedisperse=False,
+                                 dededisperse=False, tscrunch=tscrunch,
+                                 pscrunch=True, fscrunch=False,
+                                 rm_baseline=rm_baseline, flux_prof=False,
+                                 refresh_arch=False, return_arch=False,
+                                 quiet=quiet)
+                if data.dmc:
+                    if not quiet:
+                        print("%s is dedispersed (dmc = 1).  Reloading it." %
+                              datafile)
+                    data = load_data(datafile, dedisperse=False,
+                                     dededisperse=True, tscrunch=tscrunch,
+                                     pscrunch=True, fscrunch=False,
+                                     rm_baseline=rm_baseline,
+                                     flux_prof=False, refresh_arch=False,
+                                     return_arch=False, quiet=quiet)
+                if not len(data.ok_isubs):
+                    if not quiet:
+                        print("No subints to fit for %s.  Skipping it." %
+                              datafile)
+                    continue
+                self.ok_idatafiles.append(iarch)
+            except RuntimeError:
+                if not quiet:
+                    print("Cannot load_data(%s).  Skipping it." % datafile)
+                continue
+            d = data
+            nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
+            if d.source is None:
+                d.source = "noname"
+            obs = DataBunch(telescope=d.telescope, backend=d.backend,
+                            frontend=d.frontend)
+            phis = np.zeros([nsub, nchan])
+            phi_errs = np.zeros([nsub, nchan])
+            TOAs = np.zeros([nsub, nchan], dtype="object")
+            TOA_errs = np.zeros([nsub, nchan], dtype="object")
+            taus = np.zeros([nsub, nchan])
+            tau_errs = np.zeros([nsub, nchan])
+            scales = np.zeros([nsub, nchan])
+            scale_errs = np.zeros([nsub, nchan])
+            channel_snrs = np.zeros([nsub, nchan])
+            profile_fluxes = np.zeros([nsub, nchan])
+            profile_flux_errs = np.zeros([nsub, nchan])
+            channel_red_chi2s = np.zeros([nsub, nchan])
+            covariances = np.zeros([nsub, nchan, self.nfit, self.nfit])
+            nfevals = np.zeros([nsub, nchan], dtype="int")
+            rcs = np.zeros([nsub, nchan], dtype="int")
+            MJDs = np.array([d.epochs[isub].in_days() for isub in range(nsub)],
+                            dtype=np.double)
+            ok_isubs = list(d.ok_isubs)
+            models, model_index = self._models(d, ok_isubs, False, quiet)
+            # every (sub-int, usable channel) row of the archive
+            rows_s, rows_c, midx = [], [], []
+            for j, isub in enumerate(ok_isubs):
+                for ichan in d.ok_ichans[isub]:
+                    rows_s.append(isub)
+                    rows_c.append(int(ichan))
+                    midx.append(model_index[j] * nchan + int(ichan))
+            rows_s = np.array(rows_s, dtype=int)
+            rows_c = np.array(rows_c, dtype=int)
+            t_fit = time.time()
+            out = np.zeros((0, 8))
+            if len(rows_s):
+                prof = np.asarray(d.subints)[rows_s, 0, rows_c]
+                p32 = prof.astype(np.float32)
+                if np.array_equal(p32.astype(np.float64), prof):
+                    prof = p32
+                errs = np.asarray(d.noise_stds)[rows_s, 0, rows_c]
+                out = engine.phase_shift_batch(
+                    prof, models.reshape(-1, nbin), errs, Ns=100,
+                    bounds=(-0.5, 0.5),
+                    model_index=np.array(midx, dtype=np.int32)).cpu().numpy()
+            per = (time.time() - t_fit) / max(1, len(rows_s))
+            for r, (isub, ichan) in enumerate(zip(rows_s, rows_c)):
+                phase, phase_err, scale, scale_err, snr, red_chi2 = out[r, :6]
+                fit_duration += per
+                P = d.Ps[isub]
+                epoch = d.epochs[isub]
+                TOA_r = epoch + _MJD((phase * P + d.backend_delay) /
+                                     (3600 * 24.))
+                TOA_err = phase_err * P * 1e6
+                if print_flux:
+                    model_prof = models[model_index[ok_isubs.index(isub)]][
+                        ichan]
+                    smm = np.copy(model_prof).mean()
+                    profile_fluxes[isub, ichan] = smm * scale
+                    profile_flux_errs[isub, ichan] = abs(smm) * scale_err
+                phis[isub, ichan] = phase
+                phi_errs[isub, ichan] = phase_err
+                TOAs[isub, ichan] = TOA_r
+                TOA_errs[isub, ichan] = TOA_err
+                scales[isub, ichan] = scale
+                scale_errs[isub, ichan] = scale_err
+                channel_snrs[isub, ichan] = snr
+                channel_red_chi2s[isub] = red_chi2     # (sic) pptoas.py:1094
+                toa_flags = {}
+                toa_flags["be"] = d.backend
+                toa_flags["fe"] = d.frontend
+                toa_flags["f"] = d.frontend + "_" + d.backend
+                toa_flags["nbin"] = nbin
+                toa_flags["bw"] = abs(d.bw) / nchan
+                toa_flags["subint"] = isub
+                toa_flags["chan"] = ichan
+                toa_flags["tobs"] = d.subtimes[isub]
+                toa_flags["tmplt"] = self.modelfile
+                toa_flags["snr"] = snr
+                toa_flags["gof"] = red_chi2
+                if print_phase:
+                    # the reference reads results.phi, which fit_phase_shift
+                    # does not return (pptoas.py:1120)
+                    raise AttributeError("'DataBunch' object has no "
+                                         "attribute 'phi'")
+                if print_flux:
+                    # the reference reads fluxes[isub], never defined on this
+                    # path (pptoas.py:1123)
+                    raise NameError("name 'fluxes' is not defined")
+                if print_parangle:
+                    toa_flags["par_angle"] = d.parallactic_angles[isub]
+                for k, v in addtnl_toa_flags.items():
+                    toa_flags[k] = v
+                self.TOA_list.append(TOA(datafile, d.freqs[isub, ichan],
+                                         TOA_r, TOA_err, d.telescope,
+                                         d.telescope_code, None, None,
+                                         toa_flags))
+            self.order.append(datafile)
+            self.obs.append(obs)
+            self.doppler_fs.append(d.doppler_factors)
+            self.ok_isubs.append(d.ok_isubs)
+            self.epochs.append(d.epochs)
+            self.MJDs.append(MJDs)
+            self.Ps.append(d.Ps)
+            self.phis.append(phis)
+            self.phi_errs.append(phi_errs)
+            self.TOAs.append(TOAs)
+            self.TOA_errs.append(TOA_errs)
+            self.taus.append(taus)
+            self.tau_errs.append(tau_errs)
+            self.scales.append(scales)
+            self.scale_errs.append(scale_errs)
+            self.channel_snrs.append(channel_snrs)
+            self.profile_fluxes.append(profile_fluxes)
+            self.profile_flux_errs.append(profile_flux_errs)
+            self.covariances.append(covariances)
+            self.channel_red_chi2s.append(channel_red_chi2s)
+            self.nfevals.append(nfevals)
+            self.rcs.append(rcs)
+            self.fit_durations.append(fit_duration)
+            if not quiet:
+                print("--------------------------")
+                print(datafile)
+                print("~%.4f sec/TOA" % (fit_duration / len(self.TOA_list)))
+                print("Med. TOA error is %.3f us" % (np.median(
+                    phi_errs[d.ok_isubs]) * d.Ps.mean() * 1e6))
+        tot_duration = time.time() - start
+        if not quiet and len(self.ok_isubs):
+            print("--------------------------")
+            print("Total time: %.2f sec, ~%.4f sec/TOA" % (
+                tot_duration, tot_duration / len(self.TOA_list)))

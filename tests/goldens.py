@@ -160,3 +160,8 @@ def align_inputs(c=None):
         subints=c["guess"][None, None], weights=np.ones([1, nchan]),
         arch=None, state="Intensity")
     return archives, model_data
+
+
+def narrowband():
+    z = _load("narrowband.npz")
+    return Case({k: z[k] for k in z.files})

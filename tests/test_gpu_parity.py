@@ -574,3 +574,67 @@ def test_align_archives_matches_reference(monkeypatch):
     np.testing.assert_allclose(rec.amps[0], ref, rtol=0, atol=1e-6 * scale)
     np.testing.assert_array_equal(rec.weights, c["out_weights"])
     assert rec.dm == 0.0 and rec.outfile == "aligned.fits"
+
+
+# -------------------------------------------------- narrowband TOAs --------
+def test_narrowband_toas_match_reference(monkeypatch, tmp_path, capsys):
+    """GetTOAs.get_narrowband_TOAs (pptoas.py:794-1189): one FFTFIT per
+    usable channel, all channels of an archive in one batched device call,
+    against the reference's own run (tests/golden/narrowband.npz): phases
+    within 0.01 of their errors, errors / scales / S/N / gof to 1e-6, and
+    the .tim lines to their printed precision."""
+    import os
+    from pulseportraiture_amd import pptoas, pplib
+    from pulseportraiture_amd.pplib import DataBunch, get_bin_centers
+    g = G.narrowband()
+    nsub, nchan, nbin = int(g["nsub"]), int(g["nchan"]), int(g["nbin"])
+    files = {}
+    for f in range(int(g["nfile"])):
+        sub = g["f%d_subints" % f].astype(np.float64)[:, None]
+        w = g["f%d_weights" % f]
+        wn = np.where(w == 0.0, 0.0, 1.0)
+        files["nb%d.fits" % f] = DataBunch(
+            arch=None, backend="fake_be", backend_delay=1e-5, bw=800.0,
+            doppler_factors=np.ones(nsub), DM=float(g["DM0"]), dmc=0,
+            epochs=[_MJD(e) for e in g["f%d_epochs" % f]],
+            filename="nb%d.fits" % f, flux_prof=np.array([]),
+            freqs=np.tile(g["freqs"], (nsub, 1)), frontend="fake_rx",
+            integration_length=60.0 * nsub, masks=None, nbin=nbin,
+            nchan=nchan, noise_stds=g["f%d_noise" % f][:, None], npol=1,
+            nsub=nsub, nu0=1500.0,
+            ok_ichans=[np.compress(wn[i], list(range(nchan)))
+                       for i in range(nsub)],
+            ok_isubs=np.arange(nsub), parallactic_angles=np.zeros(nsub),
+            phases=get_bin_centers(nbin), prof=None, prof_noise=1.0,
+            prof_SNR=100.0, Ps=np.ones(nsub) * float(g["P"]),
+            SNRs=g["f%d_snrs" % f][:, None, :], source="J1234-5678",
+            state="Intensity", subints=sub, subtimes=[60.0] * nsub,
+            telescope="GBT", telescope_code="1", weights=w)
+    monkeypatch.setattr(pptoas, "load_data", lambda fn, **kw: files[fn])
+    monkeypatch.setattr(pptoas, "_MJD", _MJD)
+    meta = tmp_path / "meta.txt"
+    meta.write_text("".join(n + "\n" for n in files))
+    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+    gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    gt.get_narrowband_TOAs(quiet=True)
+    for f in range(int(g["nfile"])):
+        used = g["out_phi_errs"][f] > 0
+        dphi = np.abs(G.phase_diff(gt.phis[f], g["out_phis"][f]))[used]
+        assert np.all(dphi < SIG * g["out_phi_errs"][f][used]), dphi
+        for key in ("phi_errs", "scales", "scale_errs", "channel_snrs",
+                    "channel_red_chi2s"):
+            np.testing.assert_allclose(getattr(gt, key)[f],
+                                       g["out_" + key][f], rtol=1e-6,
+                                       err_msg=key)
+    capsys.readouterr()
+    pplib.write_TOAs(gt.TOA_list)
+    lines = capsys.readouterr().out.splitlines()
+    ref = list(g["out_tim_lines"])
+    assert len(lines) == len(ref)
+    for a, b in zip(lines, ref):
+        ta, tb = a.split(), b.split()
+        assert len(ta) == len(tb)
+        for x, y in zip(ta, tb):
+            if x.endswith("example.gmodel"):     # -tmplt path differs
+                continue
+            assert _same_printed_number(x, y), (a, b)

@@ -189,6 +189,18 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
                     const double *weights, double *out, double *wsum,
                     void *workspace, size_t workspace_bytes, void *stream);
 
+/* Channel reduced chi^2 of a fit (pptoas.get_channels_to_zap,
+ * pptoas.py:1266-1343, through show_fit 1375-1480 and get_red_chi2
+ * pplib.py:754-779): for each row r,
+ *   out[r] = sum_t (rot(in[r], phases[r])[t] - scales[r] model[model_row[r]][t])^2
+ *            / errs[r]^2 / dof
+ * with rot the rfft-phasor-irfft rotation of ppf_rotate_batch.
+ * in: [nrows][nbin]; model: [*][nbin] f64; phases, scales, errs, out: [nrows]. */
+int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
+                         const void *in, const double *phases, const double *model,
+                         const int32_t *model_row, const double *scales,
+                         const double *errs, double dof, double *out, void *stream);
+
 /* Per-row power-spectrum noise: pplib.get_noise_PS(chans=True)
  * (pplib.py:2312-2332): sqrt(mean(|rfft(x)|^2/nbin over k >= int((1-1/frac)
  * * nharm))).  in: [nrows][nbin]; out: [nrows]. */

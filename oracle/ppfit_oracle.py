@@ -18,6 +18,7 @@ __all__ = [
     "guess_fit_freq", "channel_terms", "objective", "gradient", "hessian",
     "fit_portrait_full", "fit_portrait", "rotate_rows", "rotate_data",
     "fit_phase_shift", "nu_zeros", "get_toas_archive", "align_archives",
+    "channel_red_chi2s", "select_zap_channels",
 ]
 
 DCONST = 0.000241 ** -1          # pplib.py:64-67 (Dconst = Dconst_trad)
@@ -756,3 +757,45 @@ def align_archives(archives, model_data, fit_dm=True, niter=1, npol=1):
             aligned_port[ipol, good] /= total_weights[good]
         model_port = aligned_port[0]
     return aligned_port, total_weights
+
+
+# ---------------------------------------------------------------------------
+# GetTOAs.get_channels_to_zap (pptoas.py:1266-1343): per-channel reduced chi^2
+# of the rotated data against the scaled model (show_fit, pptoas.py:1375-1480;
+# get_red_chi2, pplib.py:754-779), then the S/N / chi^2 selection.
+# ---------------------------------------------------------------------------
+def channel_red_chi2s(rows, phases, model_rows, scales, errs, dof):
+    """rows / model_rows [n, nbin]; phases, scales, errs [n].  Row r:
+    sum((rotate(rows[r], phases[r]) - scales[r] model_rows[r]) / errs[r])^2
+    / dof, with the rotation of rotate_portrait_full (pptoaslib.py:61-90)."""
+    rot = rotate_rows(np.asarray(rows, dtype=np.float64), phases)
+    res = rot - np.asarray(scales)[:, None] * np.asarray(model_rows)
+    return np.sum((res / np.asarray(errs)[:, None]) ** 2, axis=-1) / dof
+
+
+def select_zap_channels(red_chi2s, ok_ichans, channel_snrs, SNR_threshold,
+                        rchi2_threshold, iterate):
+    """pptoas.py:1296-1333 for one sub-integration: red_chi2s per ok channel
+    (same order as ok_ichans); channel_snrs indexed by absolute channel.
+    Returns the bad channel list in the reference's append order."""
+    nchx = len(ok_ichans)
+    thr = (SNR_threshold ** 2.0 / nchx) ** 0.5
+    bad = []
+    for ichan, c in zip(ok_ichans, red_chi2s):
+        if c > rchi2_threshold or np.isnan(c):
+            bad.append(ichan)
+        elif SNR_threshold and channel_snrs[ichan] < thr:
+            bad.append(ichan)
+    if iterate and SNR_threshold and len(bad):
+        old = len(bad)
+        added = True
+        while added and (nchx - len(bad)):
+            thr = (SNR_threshold ** 2.0 / (nchx - len(bad))) ** 0.5
+            for ichan in ok_ichans:
+                if ichan in bad:
+                    continue
+                if channel_snrs[ichan] < thr:
+                    bad.append(ichan)
+            added = bool(len(bad) - old)
+            old = len(bad)
+    return bad

@@ -472,6 +472,29 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int
     return PPF_OK;
 }
 
+int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
+                         const void *in, const double *phases, const double *model,
+                         const int32_t *model_row, const double *scales, const double *errs,
+                         double dof, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nrows < 0 || (nrows > 0 && (!in || !phases || !model || !model_row || !scales || !errs ||
+                                    !out)))
+        return fail(ctx, PPF_EINVAL, "bad resid_chi2 arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (nrows == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    ppf::ResidArgs a{nbin, ilog2(nbin / 2), in_dtype, in, phases, model, model_row, scales, errs,
+                     dof, T, T2, out};
+    if ((e = ppf::launch_resid_chi2(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_resid_chi2");
+    return PPF_OK;
+}
+
 int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
                     int32_t frac, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;

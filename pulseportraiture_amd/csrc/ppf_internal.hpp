@@ -128,6 +128,21 @@ struct AlignArgs {
 int align_groups(int nsub, int nchan);
 hipError_t launch_align(const AlignArgs &a, hipStream_t st);
 
+// per-row reduced chi^2 of (rotated data - scale * model) (the channel test
+// of pptoas.get_channels_to_zap, pptoas.py:1266-1343 via show_fit 1375-1480)
+struct ResidArgs {
+    int nbin, log2N, dtype;
+    const void *in;              // [nrows][nbin]
+    const double *phases;        // [nrows]
+    const double *model;         // [nmodelrows][nbin]
+    const int32_t *model_row;    // [nrows]
+    const double *scales, *errs; // [nrows]
+    double dof;
+    const double2 *T, *T2;
+    double *out;                 // [nrows]
+};
+hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st);
+
 struct NoiseArgs {
     int nbin, log2N, dtype, kc;
     const void *in;

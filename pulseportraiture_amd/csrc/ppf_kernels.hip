@@ -907,6 +907,71 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// k_resid_chi2: get_red_chi2(rotate_portrait_full(x)[n], scale_n model_n,
+// err_n, dof) per row (pplib.py:754-779): rotation as k_rotate (rfft,
+// phasor, irfft dropping the DC / Nyquist imaginary parts), then the
+// residual sum of squares over the bins with a fixed-order block reduction.
+// ===========================================================================
+template <int KMAX>
+__global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    __shared__ double red[kWaves * 4];
+    const int N = a.nbin >> 1;
+    const int64_t row = blockIdx.x;
+    load_row(lds, a.in, a.dtype, row, a.nbin);
+    __syncthreads();
+    lds_fft(lds, a.log2N, a.T, false);
+    double2 Xk[KMAX], Xn[KMAX];
+    const double ph = a.phases[row];
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        int k = threadIdx.x + i * kBlock;
+        if (k < N) {
+            double2 X1 = cmul(rfft_bin(lds, N, a.T2, k), cexp2pi((double)k * ph));
+            double2 X2 = cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
+            if (k == 0) { X1.y = 0.0; X2.y = 0.0; }
+            Xk[i] = X1;
+            Xn[i] = X2;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        int k = threadIdx.x + i * kBlock;
+        if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+    }
+    __syncthreads();
+    lds_fft(lds, a.log2N, a.T, true);
+    const double sc = 1.0 / (double)N, s = a.scales[row];
+    const double *m = a.model + (int64_t)a.model_row[row] * a.nbin;
+    double acc[1] = {0.0};
+    for (int j = threadIdx.x; j < N; j += kBlock) {
+        const double2 x = cscale(lds[j], sc);
+        const double r0 = x.x - s * m[2 * j], r1 = x.y - s * m[2 * j + 1];
+        acc[0] = fma(r0, r0, fma(r1, r1, acc[0]));
+    }
+    block_sum<1>(acc, red);
+    if (threadIdx.x == 0) {
+        const double e = a.errs[row];
+        a.out[row] = acc[0] / (e * e) / a.dof;
+    }
+}
+
+hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) {
+    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    dim3 g((unsigned)nrows), b(kBlock);
+    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+        case 1: hipLaunchKernelGGL(k_resid_chi2<1>, g, b, lds, st, a); break;
+        case 2: hipLaunchKernelGGL(k_resid_chi2<2>, g, b, lds, st, a); break;
+        case 4: hipLaunchKernelGGL(k_resid_chi2<4>, g, b, lds, st, a); break;
+        case 8: hipLaunchKernelGGL(k_resid_chi2<8>, g, b, lds, st, a); break;
+        case 16: hipLaunchKernelGGL(k_resid_chi2<16>, g, b, lds, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     hipLaunchKernelGGL(k_noise, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);

@@ -204,6 +204,34 @@ def align_accum(data, phases, weights, out, wsum, dev=None):
     return out, wsum
 
 
+def resid_chi2_rows(rows, phases, model_rows, model_index, scales, errs, dof,
+                    dev=None):
+    """Per row: sum_t (rotate(row, phase) - scale * model_rows[index])^2 /
+    err^2 / dof (ppf_resid_chi2_batch) -> float64 [nrows]."""
+    dev = device(dev)
+    r = to_dev(rows, dev, _data_dtype(rows))
+    nbin = r.shape[-1]
+    r2 = r.reshape(-1, nbin).contiguous()
+    n = r2.shape[0]
+    ph = to_dev(phases, dev, torch.float64).reshape(-1).contiguous()
+    m = to_dev(model_rows, dev, torch.float64).reshape(-1, nbin).contiguous()
+    mi = to_dev(model_index, dev, torch.int32).reshape(-1).contiguous()
+    sc = to_dev(scales, dev, torch.float64).reshape(-1).contiguous()
+    er = to_dev(errs, dev, torch.float64).reshape(-1).contiguous()
+    if not (ph.numel() == mi.numel() == sc.numel() == er.numel() == n):
+        raise ValueError("need one phase / model index / scale / err per row")
+    if n and (int(mi.min()) < 0 or int(mi.max()) >= m.shape[0]):
+        raise ValueError("model index out of range")
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_resid_chi2_batch(
+        ctx, n, nbin, _lib.PPF_F32 if r2.dtype == torch.float32 else
+        _lib.PPF_F64, _p(r2), _p(ph), _p(m), _p(mi), _p(sc), _p(er),
+        float(dof), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
 def noise_rows(rows, frac=4, dev=None):
     """get_noise_PS per row of rows [..., nbin] -> [...] float64."""
     dev = device(dev)

@@ -263,6 +263,26 @@ def get_noise_PS(data, frac=4, chans=False):
     return float(engine.noise_rows(row[None, :], frac).cpu().numpy()[0])
 
 
+def get_red_chi2(data, model, errs=None, dof=None):
+    """pplib.py:754-779 (host: a single residual sum; the batched per-channel
+    form used by get_channels_to_zap runs on the GPU, ppf_resid_chi2_batch)."""
+    data = np.asarray(data, dtype=np.float64)
+    resids = data - model
+    if errs is None:
+        if len(data.shape) == 1:
+            errs = get_noise(data)
+        elif len(data.shape) == 2:
+            errs = get_noise(data, chans=True)
+        else:
+            print("Can only handle 1- or 2-D input.")
+    if dof is None:
+        dof = sum(data.shape)
+    if len(data.shape) == 1:
+        return np.sum((resids / errs) ** 2.0) / dof
+    return np.array([(resids[ii] / errs[ii]) ** 2.0 for ii in
+                     range(len(resids))]).sum() / dof
+
+
 def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
     """pplib.py:2427-2515: per-row phases on the host, FFT rotation on the
     GPU (ppf_rotate_batch)."""

@@ -20,6 +20,7 @@ from .pplib import (DataBunch, file_is_type, guess_fit_freq, read_model,
                     scattering_alpha, write_TOAs, weighted_mean,
                     scattering_times, scattering_portrait_FT,
                     gen_gaussian_portrait, _raise_status)
+from . import pptoaslib as _pptl
 from .pptoaslib import unpack_result, _status_message, _nu_zero_messages
 
 max_nfile = 999                    # pptoas.py:33
@@ -722,3 +723,193 @@ class GetTOAs(object):
             print("--------------------------")
             print("Total time: %.2f sec, ~%.4f sec/TOA" % (
                 tot_duration, tot_duration / len(self.TOA_list)))
+
+    # ------------------------------------------------------------------
+    # fit inspection and channel zapping (pptoas.py:1266-1480)
+    # ------------------------------------------------------------------
+    def _load_fit_data(self, datafile, quiet):
+        """show_fit's reload of the archive (pptoas.py:1393-1409)."""
+        kw = dict(dedisperse=False, dededisperse=False,
+                  tscrunch=getattr(self, "tscrunch", False), pscrunch=True,
+                  fscrunch=False, rm_baseline=True, flux_prof=False,
+                  refresh_arch=False, return_arch=False, quiet=quiet)
+        data = load_data(datafile, **kw)
+        if data.dmc:
+            if not quiet:
+                print("%s is dedispersed (dmc = 1).  Reloading it." %
+                      datafile)
+            kw["dededisperse"] = True
+            data = load_data(datafile, **kw)
+        return data
+
+    def _fit_model(self, data, ifile, isub, quiet, cache=None):
+        """The unscaled (scattered) model portrait of show_fit
+        (pptoas.py:1415-1459) for one sub-integration.  Un-scattered models
+        depend only on the channel frequencies and are cached per archive."""
+        if self.is_FITS_model:
+            raise NotImplementedError("FITS (archive) templates need PSRCHIVE")
+        if self.add_instrumental_response and \
+                (self.ird["DM"] or len(self.ird["wids"])):
+            raise NotImplementedError("instrumental response (SURVEY.md row "
+                                      "19) is not on the accelerated path")
+        freqs = data.freqs[isub]
+        tau = self.taus[ifile][isub]
+        key = freqs.tobytes()
+        if tau == 0.0 and cache is not None and key in cache:
+            return cache[key]
+        model_name, ngauss, model = read_model(
+            self.modelfile, data.phases, freqs, data.Ps.mean(), quiet=quiet)
+        if tau != 0.0:
+            (model_name, model_code, model_nu_ref, ngauss, gparams, _mff,
+             _ma, _mfa) = read_model(self.modelfile, quiet=quiet)
+            gparams = np.copy(gparams)
+            gparams[1] = 0.0
+            model = gen_gaussian_portrait(model_code, gparams, 0.0,
+                                          data.phases, freqs, model_nu_ref)
+            if self.log10_tau:
+                tau = 10 ** tau
+            nu_ref_tau = self.nu_refs[ifile][isub][2]
+            model = np.fft.irfft(scattering_portrait_FT(
+                scattering_times(tau, self.alphas[ifile][isub], freqs,
+                                 nu_ref_tau), data.nbin) *
+                np.fft.rfft(model, axis=1), axis=1)
+        elif cache is not None:
+            cache[key] = (model_name, model)
+        return model_name, model
+
+    def _fit_phases(self, data, ifile, isub):
+        """Per-channel rotation of show_fit's rotate_portrait_full call
+        (pptoas.py:1410-1418, 1460-1461): fitted phi, DM, GM (Doppler
+        corrected back to the topocentric values) at the output ν_refs."""
+        phi = self.phis[ifile][isub]
+        DM = self.DMs[ifile][isub]
+        GM = self.GMs[ifile][isub]
+        if self.bary:
+            DM /= self.doppler_fs[ifile][isub]
+            GM /= self.doppler_fs[ifile][isub] ** 3
+        nu_ref_DM, nu_ref_GM, _ = self.nu_refs[ifile][isub]
+        return _pptl.phase_shifts(phi, DM, GM, data.freqs[isub], nu_ref_DM,
+                                  nu_ref_GM, data.Ps[isub], False)
+
+    def show_fit(self, datafile=None, isub=0, rotate=0.0, show=True,
+                 return_fit=False, savefig=False, quiet=None):
+        """pptoas.py:1375-1480: the rotated data portrait and the scaled
+        fitted model of one sub-integration (rotation on the GPU).  The plot
+        itself is outside the accelerated path: show=True raises."""
+        if quiet is None:
+            quiet = self.quiet
+        if show:
+            raise NotImplementedError("plotting is outside the accelerated "
+                                      "path (SURVEY.md section 2, row 20)")
+        if datafile is None:
+            datafile = self.datafiles[0]
+        ifile = list(np.array(self.datafiles)[self.ok_idatafiles]).index(
+            datafile)
+        data = self._load_fit_data(datafile, quiet)
+        model_name, model = self._fit_model(data, ifile, isub, quiet)
+        ph = self._fit_phases(data, ifile, isub)
+        port = engine.rotate_rows(np.asarray(data.subints[isub, 0]),
+                                  ph).cpu().numpy()
+        if rotate:
+            model = _pplib.rotate_data(model, rotate)
+            port = _pplib.rotate_data(port, rotate)
+        if data.masks is not None:
+            port *= data.masks[isub, 0]
+        model_scaled = np.transpose(self.scales[ifile][isub] *
+                                    np.transpose(model))
+        if return_fit:
+            return (port, model_scaled, data.ok_ichans[isub],
+                    data.freqs[isub], data.noise_stds[isub, 0])
+
+    def get_channels_to_zap(self, SNR_threshold=8.0, rchi2_threshold=1.3,
+                            iterate=True, show=False):
+        """pptoas.py:1266-1343.  NB: get_TOAs(...) needs to have been called
+        first.  Per archive, the reduced chi^2 of every usable channel of
+        every fitted sub-integration (show_fit + get_red_chi2 with
+        dof = nbin - 2, pplib.py:754-779) is ONE batched device call
+        (ppf_resid_chi2_batch: rotate, subtract the scaled model, reduce);
+        the S/N / chi^2 selection that follows is the reference's host logic.
+        Fills self.channel_red_chi2s and self.zap_channels."""
+        if show:
+            raise NotImplementedError("plotting is outside the accelerated "
+                                      "path (SURVEY.md section 2, row 20)")
+        for iarch, ok_idatafile in enumerate(self.ok_idatafiles):
+            datafile = self.datafiles[ok_idatafile]
+            data = self._load_fit_data(datafile, True)
+            nbin = data.nbin
+            isubs = list(self.ok_isubs[iarch])
+            cache, slots, models, rows, phases, midx, scl, errs, chans = \
+                {}, {}, [], [], [], [], [], [], []
+            for isub in isubs:
+                ok = np.asarray(data.ok_ichans[isub], dtype=int)
+                _, model = self._fit_model(data, iarch, isub, True, cache)
+                port = np.asarray(data.subints[isub, 0])[ok]
+                if data.masks is not None:
+                    m = np.asarray(data.masks[isub, 0])[ok]
+                    if not np.all(m == 1.0):
+                        port = port * m
+                rows.append(port)
+                phases.append(self._fit_phases(data, iarch, isub)[ok])
+                slot = slots.setdefault(id(model), len(models))
+                if slot == len(models):
+                    models.append(model)
+                midx.append(slot * data.nchan + ok)
+                scl.append(np.asarray(self.scales[iarch][isub])[ok])
+                errs.append(np.asarray(data.noise_stds[isub, 0])[ok])
+                chans.append(ok)
+            if len(isubs):
+                rows_a = np.concatenate(rows)
+                r32 = rows_a.astype(np.float32)
+                if np.array_equal(r32.astype(np.float64), rows_a):
+                    rows_a = r32          # PSRCHIVE amplitudes are float32
+                chi2 = engine.resid_chi2_rows(
+                    rows_a, np.concatenate(phases),
+                    np.concatenate(models).reshape(-1, nbin),
+                    np.concatenate(midx), np.concatenate(scl),
+                    np.concatenate(errs), nbin - 2).cpu().numpy()
+            channel_red_chi2s, zap_channels = [], []
+            pos = 0
+            for j, isub in enumerate(isubs):
+                ok_ichans = chans[j]
+                red_chi2s = list(chi2[pos:pos + len(ok_ichans)])
+                pos += len(ok_ichans)
+                channel_snrs = self.channel_snrs[iarch][isub]
+                channel_red_chi2s.append(red_chi2s)
+                zap_channels.append(_select_zap(
+                    red_chi2s, ok_ichans, channel_snrs, SNR_threshold,
+                    rchi2_threshold, iterate))
+            self.channel_red_chi2s.append(channel_red_chi2s)
+            self.zap_channels.append(zap_channels)
+
+
+def _select_zap(red_chi2s, ok_ichans, channel_snrs, SNR_threshold,
+                rchi2_threshold, iterate):
+    """The channel selection of pptoas.py:1296-1333 for one sub-integration:
+    chi^2 above threshold or NaN, or channel S/N below
+    (SNR_threshold^2 / nchx)^0.5; with iterate, the S/N threshold is raised
+    as channels are removed until nothing new is cut."""
+    nchx = len(ok_ichans)
+    bad = []
+    threshold = (SNR_threshold ** 2.0 / nchx) ** 0.5 if nchx else np.inf
+    for ok_ichan, rchi2 in zip(ok_ichans, red_chi2s):
+        if rchi2 > rchi2_threshold:
+            bad.append(ok_ichan)
+        elif np.isnan(rchi2):
+            bad.append(ok_ichan)
+        elif SNR_threshold and channel_snrs[ok_ichan] < threshold:
+            bad.append(ok_ichan)
+    if iterate and SNR_threshold and len(bad):
+        old_len = len(bad)
+        added_new = True
+        while added_new and (nchx - len(bad)):
+            threshold = (SNR_threshold ** 2.0 / (nchx - len(bad))) ** 0.5
+            bad_set = set(int(b) for b in bad)
+            for ok_ichan in ok_ichans:
+                if int(ok_ichan) in bad_set:
+                    continue
+                if channel_snrs[ok_ichan] < threshold:
+                    bad.append(ok_ichan)
+                    bad_set.add(int(ok_ichan))
+            added_new = bool(len(bad) - old_len)
+            old_len = len(bad)
+    return bad

@@ -165,3 +165,29 @@ def align_inputs(c=None):
 def narrowband():
     z = _load("narrowband.npz")
     return Case({k: z[k] for k in z.files})
+
+
+def zap():
+    """tests/golden/zap.npz (make_golden_zap.py) plus the reference's ragged
+    get_channels_to_zap outputs unflattened to [call][file][sub] lists."""
+    z = _load("zap.npz")
+    c = Case({k: z[k] for k in z.files})
+    nfile, nsub = int(c["nfile"]), int(c["nsub"])
+    ncall = len(c["calls"])
+    chi, zp = [], []
+    ic = iz = j = 0
+    for _ in range(ncall):
+        cc, zz = [], []
+        for _ in range(nfile):
+            cs, zs = [], []
+            for _ in range(nsub):
+                n, m = int(c["out_chi2_n"][j]), int(c["out_zap_n"][j])
+                cs.append(c["out_chi2"][ic:ic + n])
+                zs.append([int(v) for v in c["out_zap"][iz:iz + m]])
+                ic, iz, j = ic + n, iz + m, j + 1
+            cc.append(cs)
+            zz.append(zs)
+        chi.append(cc)
+        zp.append(zz)
+    c["chi2"], c["zap"] = chi, zp
+    return c

@@ -638,3 +638,111 @@ def test_narrowband_toas_match_reference(monkeypatch, tmp_path, capsys):
             if x.endswith("example.gmodel"):     # -tmplt path differs
                 continue
             assert _same_printed_number(x, y), (a, b)
+
+
+# ------------------------------------------------------ channel zapping -----
+def _zap_files(g):
+    from pulseportraiture_amd.pplib import DataBunch, get_bin_centers
+    nsub, nchan, nbin = int(g["nsub"]), int(g["nchan"]), int(g["nbin"])
+    files = {}
+    for f in range(int(g["nfile"])):
+        sub = g["f%d_subints" % f].astype(np.float64)[:, None]
+        w = g["f%d_weights" % f]
+        wn = np.where(w == 0.0, 0.0, 1.0)
+        files["zap%d.fits" % f] = DataBunch(
+            arch=None, backend="fake_be", backend_delay=0.0, bw=800.0,
+            doppler_factors=g["f%d_dfs" % f], DM=float(g["DM0"]), dmc=0,
+            epochs=[_MJD(e) for e in g["f%d_epochs" % f]],
+            filename="zap%d.fits" % f, flux_prof=np.array([]),
+            freqs=np.tile(g["freqs"], (nsub, 1)), frontend="fake_rx",
+            integration_length=60.0 * nsub,
+            masks=np.einsum("ij,k", wn, np.ones(nbin))[:, None], nbin=nbin,
+            nchan=nchan, noise_stds=g["f%d_noise" % f][:, None], npol=1,
+            nsub=nsub, nu0=1500.0,
+            ok_ichans=[np.compress(wn[i], list(range(nchan)))
+                       for i in range(nsub)],
+            ok_isubs=np.arange(nsub), parallactic_angles=np.zeros(nsub),
+            phases=get_bin_centers(nbin), prof=None, prof_noise=1.0,
+            prof_SNR=100.0, Ps=np.ones(nsub) * float(g["P"]),
+            SNRs=g["f%d_snrs" % f][:, None, :], source="J1234-5678",
+            state="Intensity", subints=sub, subtimes=[60.0] * nsub,
+            telescope="GBT", telescope_code="1", weights=w)
+    return files
+
+
+def test_resid_chi2_kernel_matches_oracle_on_reference_fit():
+    """ppf_resid_chi2_batch against the oracle restatement of show_fit +
+    get_red_chi2, fed the reference's own fitted parameters
+    (tests/golden/zap.npz): every channel chi^2 to 1e-10 relative, fp32 and
+    fp64 inputs, and the reference's own chi^2s to 1e-9."""
+    import oracle.ppfit_oracle as OO
+    from pulseportraiture_amd import engine, pplib as PL
+    import os
+    g = G.zap()
+    nsub, nchan, nbin = int(g["nsub"]), int(g["nchan"]), int(g["nbin"])
+    P, freqs = float(g["P"]), g["freqs"]
+    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+    _, _, model = PL.read_model(gm, PL.get_bin_centers(nbin), freqs, P,
+                                quiet=True)
+    D = 0.000241 ** -1
+    rows, ph, mi, sc, er, ref = [], [], [], [], [], []
+    for f in range(int(g["nfile"])):
+        w = g["f%d_weights" % f]
+        for s in range(nsub):
+            ok = np.where(w[s] != 0)[0]
+            DM = g["out_DMs"][f][s] / g["out_doppler_fs"][f][s]
+            nu_DM = g["out_nu_refs"][f][s][0]
+            rows.append(g["f%d_subints" % f][s, ok])
+            ph.append(g["out_phis"][f][s] + D * DM * (freqs[ok] ** -2 -
+                                                      nu_DM ** -2) / P)
+            mi.append(ok)
+            sc.append(g["out_scales"][f][s][ok])
+            er.append(g["f%d_noise" % f][s][ok])
+            ref.append(g["chi2"][0][f][s])
+    rows, ph, mi = np.concatenate(rows), np.concatenate(ph), \
+        np.concatenate(mi).astype(np.int32)
+    sc, er, ref = np.concatenate(sc), np.concatenate(er), np.concatenate(ref)
+    want = OO.channel_red_chi2s(rows.astype(np.float64), ph, model[mi], sc,
+                                er, nbin - 2)
+    for rr in (rows, rows.astype(np.float64)):
+        got = engine.resid_chi2_rows(rr, ph, model, mi, sc, er,
+                                     nbin - 2).cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=1e-10, atol=0)
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=0)
+    with pytest.raises(ValueError):
+        engine.resid_chi2_rows(rows, ph, model, mi + nchan, sc, er, nbin - 2)
+
+
+def test_channels_to_zap_matches_reference(monkeypatch, tmp_path):
+    """GetTOAs.get_TOAs then get_channels_to_zap (pptoas.py:1266-1343) for
+    the four (S/N, chi^2, iterate) settings of make_golden_zap.py: channel
+    chi^2s within 1e-5 relative of the reference's run (the fitted
+    parameters themselves agree to 1e-3 sigma) and the zap lists, in the
+    reference's order, identical."""
+    import os
+    from pulseportraiture_amd import pptoas
+    g = G.zap()
+    files = _zap_files(g)
+    monkeypatch.setattr(pptoas, "load_data", lambda fn, **kw: files[fn])
+    monkeypatch.setattr(pptoas, "_MJD", _MJD)
+    meta = tmp_path / "meta.txt"
+    meta.write_text("".join(n + "\n" for n in files))
+    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+    gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    gt.get_TOAs(quiet=True)
+    nfile = int(g["nfile"])
+    for ic, (snr_t, rchi_t, it) in enumerate(g["calls"]):
+        gt.get_channels_to_zap(SNR_threshold=snr_t, rchi2_threshold=rchi_t,
+                               iterate=bool(it))
+        for f in range(nfile):
+            for s in range(int(g["nsub"])):
+                np.testing.assert_allclose(
+                    gt.channel_red_chi2s[ic * nfile + f][s],
+                    g["chi2"][ic][f][s], rtol=1e-5, atol=0)
+                assert [int(v) for v in gt.zap_channels[ic * nfile + f][s]] \
+                    == g["zap"][ic][f][s], (ic, f, s)
+    port, model, ok, freqs, noise = gt.show_fit("zap1.fits", isub=1,
+                                                show=False, return_fit=True)
+    assert port.shape == model.shape == (int(g["nchan"]), int(g["nbin"]))
+    bad = np.setdiff1d(np.arange(int(g["nchan"])), ok)
+    assert np.all(port[bad] == 0.0)

@@ -165,3 +165,36 @@ def test_oracle_align_archives_matches_reference():
     scale = np.abs(ref).max()
     np.testing.assert_allclose(port[0], ref, rtol=0, atol=1e-6 * scale)
     np.testing.assert_array_equal(tw[:, 0] > 0, c["out_weights"] > 0)
+
+
+def test_oracle_channels_to_zap_matches_reference():
+    """get_channels_to_zap (pptoas.py:1266-1343): the oracle's channel chi^2
+    (show_fit + get_red_chi2) and selection, fed the reference's own fitted
+    parameters, reproduce the reference's chi^2s and zap lists exactly."""
+    import oracle.ppfit_oracle as OO
+    g = G.zap()
+    nsub, nchan, nbin = int(g["nsub"]), int(g["nchan"]), int(g["nbin"])
+    P = float(g["P"])
+    freqs = g["freqs"]
+    model = _gmodel_portrait(nchan, nbin, freqs, P)
+    D = 0.000241 ** -1
+    for f in range(int(g["nfile"])):
+        sub = g["f%d_subints" % f].astype(float)
+        w = g["f%d_weights" % f]
+        for s in range(nsub):
+            ok = np.where(w[s] != 0)[0]
+            df = g["out_doppler_fs"][f][s]
+            DM = g["out_DMs"][f][s] / df
+            nu_DM, nu_GM, _ = g["out_nu_refs"][f][s]
+            ph = g["out_phis"][f][s] + D * DM * (freqs[ok] ** -2 -
+                                                   nu_DM ** -2) / P
+            chi = OO.channel_red_chi2s(sub[s, ok], ph, model[ok],
+                                       g["out_scales"][f][s][ok],
+                                       g["f%d_noise" % f][s][ok], nbin - 2)
+            for ic, (snr_t, rchi_t, it) in enumerate(g["calls"]):
+                np.testing.assert_allclose(chi, g["chi2"][ic][f][s],
+                                           rtol=1e-9, atol=0)
+                bad = OO.select_zap_channels(
+                    g["chi2"][ic][f][s], list(ok), g["out_channel_snrs"][f][s],
+                    snr_t, rchi_t, bool(it))
+                assert bad == g["zap"][ic][f][s], (ic, f, s)

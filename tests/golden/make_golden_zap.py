@@ -140,6 +140,39 @@ def run_zap():
     out["out_chi2_n"] = np.array(chi_n, dtype=np.int64)
     out["out_zap"] = np.array(zap, dtype=np.int64)
     out["out_zap_n"] = np.array(zap_n, dtype=np.int64)
+    out.update(run_ppzap(files, gt))
+    return out
+
+
+def run_ppzap(files, gt):
+    """ppzap.py: the noise-median zapper (get_zap_channels, ppzap.py:23-53)
+    over each archive, and print_paz_cmds (ppzap.py:56-106) for the
+    model-based zap lists and the noise-based ones, all flag combinations."""
+    with contextlib.redirect_stdout(io.StringIO()):
+        import ppzap
+    out = {}
+    zl = []
+    for nstd in (1.0, 3.0):
+        for name in sorted(files):
+            zl.append(ppzap.get_zap_channels(files[name], nstd=nstd))
+    flat, nz = [], []
+    for a in zl:
+        for s in a:
+            flat.extend(int(v) for v in s)
+            nz.append(len(s))
+    out["ppzap_noise_zap"] = np.array(flat, dtype=np.int64)
+    out["ppzap_noise_zap_n"] = np.array(nz, dtype=np.int64)
+    ok_files = list(np.array(gt.datafiles)[gt.ok_idatafiles])
+    lines = []
+    for zap_list in (gt.zap_channels[:2], zl[:2]):
+        for all_subs in (False, True):
+            for modify in (False, True):
+                buf = io.StringIO()
+                with contextlib.redirect_stdout(buf):
+                    ppzap.print_paz_cmds(ok_files, zap_list,
+                                         all_subs=all_subs, modify=modify)
+                lines.append(buf.getvalue())
+    out["ppzap_paz_out"] = np.array(lines)
     return out
 
 

@@ -746,3 +746,11 @@ def test_channels_to_zap_matches_reference(monkeypatch, tmp_path):
     assert port.shape == model.shape == (int(g["nchan"]), int(g["nbin"]))
     bad = np.setdiff1d(np.arange(int(g["nchan"])), ok)
     assert np.all(port[bad] == 0.0)
+    # the ppzap.py command line, model-based branch: get_TOAs +
+    # get_channels_to_zap(8, 1.3, iterate) -> paz commands (to a file),
+    # identical to the reference's print_paz_cmds of its own zap lists
+    from pulseportraiture_amd import ppzap
+    paz = tmp_path / "paz.txt"
+    assert ppzap.main(["-d", str(meta), "-m", gm, "-o", str(paz),
+                       "--quiet"]) == 0
+    assert paz.read_text() == str(g["ppzap_paz_out"][0])

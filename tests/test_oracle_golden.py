@@ -198,3 +198,40 @@ def test_oracle_channels_to_zap_matches_reference():
                     g["chi2"][ic][f][s], list(ok), g["out_channel_snrs"][f][s],
                     snr_t, rchi_t, bool(it))
                 assert bad == g["zap"][ic][f][s], (ic, f, s)
+
+
+def test_ppzap_host_logic_matches_reference(tmp_path):
+    """ppzap.get_zap_channels (noise-median iteration, ppzap.py:23-53) and
+    print_paz_cmds (ppzap.py:56-106) against the reference's own output on
+    the zap archives: identical channel lists and identical paz text."""
+    import contextlib
+    import io
+    from pulseportraiture_amd import ppzap
+    from pulseportraiture_amd.pplib import DataBunch
+    g = G.zap()
+    nsub, nfile = int(g["nsub"]), int(g["nfile"])
+    zl = []
+    for nstd in (1.0, 3.0):
+        for f in range(nfile):
+            w = g["f%d_weights" % f]
+            d = DataBunch(ok_isubs=np.arange(nsub),
+                          ok_ichans=[np.where(w[i] != 0)[0]
+                                     for i in range(nsub)],
+                          noise_stds=g["f%d_noise" % f][:, None])
+            zl.append(ppzap.get_zap_channels(d, nstd=nstd))
+    flat = [int(v) for a in zl for s in a for v in s]
+    assert flat == list(g["ppzap_noise_zap"])
+    assert [len(s) for a in zl for s in a] == list(g["ppzap_noise_zap_n"])
+    files = ["zap0.fits", "zap1.fits"]
+    outs = iter(g["ppzap_paz_out"])
+    for zap_list in (g["zap"][0], zl[:2]):
+        for all_subs in (False, True):
+            for modify in (False, True):
+                buf = io.StringIO()
+                with contextlib.redirect_stdout(buf):
+                    ppzap.print_paz_cmds(files, zap_list, all_subs=all_subs,
+                                         modify=modify)
+                assert buf.getvalue() == str(next(outs))
+    out = tmp_path / "paz.txt"
+    ppzap.print_paz_cmds(files, zl[:2], outfile=str(out), quiet=True)
+    assert out.read_text() == str(g["ppzap_paz_out"][5])

@@ -220,6 +220,23 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin,
                           const double *noise, int32_t Ns, double lo,
                           double hi, double *out, void *stream);
 
+/* Gaussian-component model portraits: pplib.gen_gaussian_portrait
+ * (pplib.py:886-963, join_ichans = []) as called by pplib.read_model
+ * (pplib.py:2971-3057) for every sub-integration of GetTOAs.get_TOAs
+ * (pptoas.py:392-419) and get_narrowband_TOAs.  One launch builds nport
+ * portraits (one per distinct frequency set), each row by
+ * gen_gaussian_profile / gaussian_profile (pplib.py:801-883) and, when
+ * tau != 0, convolved with scattering_portrait_FT (pplib.py:4245-4260).
+ * model_code: 3 chars '0' (power law) / '1' (linear) for loc, wid, amp
+ * (anything else: PPF_EINVAL, the reference's KeyError).  params:
+ * [nport][2 + 6*ngauss] = DC, tau [bin], then per component loc, m_loc,
+ * wid, m_wid, amp, m_amp; scattering_index, nu_ref: [nport];
+ * freqs: [nport][nchan]; out: [nport][nchan][nbin] f64 (device). */
+int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin,
+                             int32_t ngauss, const char *model_code, const double *params,
+                             const double *scattering_index, const double *freqs,
+                             const double *nu_ref, double *out, void *stream);
+
 /* Synthetic sub-integrations for benchmarks/tests (make_fake_pulsar minus
  * PSRCHIVE, pplib.py:3355-3493): out[s][n] = rotate(model[n], -phi[s],
  * -DM[s], P[s], freqs[n], nu_ref) + N(0, noise) with a counter-based RNG

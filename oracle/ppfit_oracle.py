@@ -18,7 +18,8 @@ __all__ = [
     "guess_fit_freq", "channel_terms", "objective", "gradient", "hessian",
     "fit_portrait_full", "fit_portrait", "rotate_rows", "rotate_data",
     "fit_phase_shift", "nu_zeros", "get_toas_archive", "align_archives",
-    "channel_red_chi2s", "select_zap_channels",
+    "channel_red_chi2s", "select_zap_channels", "gaussian_profile",
+    "gen_gaussian_portrait",
 ]
 
 DCONST = 0.000241 ** -1          # pplib.py:64-67 (Dconst = Dconst_trad)
@@ -799,3 +800,78 @@ def select_zap_channels(red_chi2s, ok_ichans, channel_snrs, SNR_threshold,
             added = bool(len(bad) - old)
             old = len(bad)
     return bad
+
+
+# ---------------------------------------------------------------------------
+# Gaussian-component model portraits (the checker of ppf_gauss_portrait_batch)
+# ---------------------------------------------------------------------------
+def _evolve(freqs, nu_ref, value, evol, code):
+    """evolve_parameter (pplib.py:1032-1084): '0' power_law_evolution
+    (pplib.py:1000-1014), '1' linear_evolution (pplib.py:1017-1029)."""
+    nchan = len(freqs)
+    if code == "0":
+        return np.exp(np.outer(np.log(freqs) - np.log(nu_ref), evol) +
+                      np.outer(np.ones(nchan), np.log(value)))
+    if code == "1":
+        return np.outer(freqs - nu_ref, evol) + \
+            np.outer(np.ones(nchan), value)
+    raise KeyError(code)
+
+
+def gaussian_profile(nbin, loc, wid):
+    """gaussian_profile(norm=False, abs_wid=False, zeroout=True)
+    (pplib.py:801-856): unit-peak wrapped Gaussian, truncated at |z| >= 20;
+    the peak factor uses the wrapped bin centre at the first argmax and the
+    unwrapped loc (pplib.py:847-849)."""
+    if not wid > 0.0:
+        return np.zeros(nbin, "d")
+    sigma = wid / (2 * np.sqrt(2 * np.log(2)))
+    mean = loc % 1.0
+    x = get_bin_centers(nbin)
+    if mean < 0.5:
+        x = np.where(np.greater(x, mean + 0.5), x - 1.0, x)
+    else:
+        x = np.where(np.less(x, mean - 0.5), x + 1.0, x)
+    zs = (x - mean) / sigma
+    ok = np.compress(np.fabs(zs) < 20.0, np.arange(nbin))
+    prof = np.zeros(nbin, "d")
+    np.put(prof, ok, np.exp(-0.5 * np.take(zs, ok) ** 2.0) /
+           (sigma * np.sqrt(2 * np.pi)))
+    if np.max(abs(prof)) == 0.0:
+        return prof
+    imax = prof.argmax()
+    z = (x[imax] - loc) / sigma
+    return np.exp(-0.5 * z ** 2.0) / prof[imax] * prof
+
+
+def gen_gaussian_portrait(model_code, params, scattering_index, phases, freqs,
+                          nu_ref):
+    """gen_gaussian_portrait (pplib.py:886-963) with join_ichans = []: per
+    channel gen_gaussian_profile (pplib.py:859-883, DC then components in
+    order), then the scattering convolution by scattering_portrait_FT
+    (pplib.py:951-957, 4245-4260; complex128 where the reference's
+    'complex_' alias no longer exists)."""
+    params = np.asarray(params, dtype=float)
+    tau = params[1]
+    nbin, nchan = len(phases), len(freqs)
+    freqs = np.asarray(freqs, dtype=float)
+    L = _evolve(freqs, nu_ref, params[2::6], params[3::6], model_code[0])
+    W = _evolve(freqs, nu_ref, params[4::6], params[5::6], model_code[1])
+    A = _evolve(freqs, nu_ref, params[6::6], params[7::6], model_code[2])
+    port = np.empty([nchan, nbin])
+    for ichan in range(nchan):
+        prof = np.zeros(nbin, dtype="d") + params[0]
+        for ig in range(L.shape[1]):
+            prof += A[ichan, ig] * gaussian_profile(nbin, L[ichan, ig],
+                                                    W[ichan, ig])
+        port[ichan] = prof
+    if tau != 0.0:
+        taus = float(tau) / nbin * (freqs / nu_ref) ** scattering_index
+        nharm = nbin // 2 + 1
+        B = np.ones([nchan, nharm], dtype=np.complex128)
+        k = np.arange(nharm)
+        for ichan in range(nchan):
+            if taus[ichan] != 0.0:
+                B[ichan] = (1.0 + 2 * np.pi * 1.0j * k * taus[ichan]) ** -1
+        port = np.fft.irfft(B * np.fft.rfft(port, axis=-1), axis=-1)
+    return port

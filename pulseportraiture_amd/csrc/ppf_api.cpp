@@ -538,6 +538,39 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     return PPF_OK;
 }
 
+int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin,
+                             int32_t ngauss, const char *model_code, const double *params,
+                             const double *scattering_index, const double *freqs,
+                             const double *nu_ref, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (nport < 0 || nchan < 1 || ngauss < 0 ||
+        (nport > 0 && (!params || !scattering_index || !freqs || !nu_ref || !out)))
+        return fail(ctx, PPF_EINVAL, "bad gauss_portrait arguments");
+    if (!model_code) return fail(ctx, PPF_EINVAL, "model_code is NULL");
+    ppf::GaussArgs a{};
+    for (int i = 0; i < 3; ++i) {
+        const char c = model_code[i];
+        if (c != '0' && c != '1')   // evolve_parameter's KeyError (pplib.py:1082-1084)
+            return fail(ctx, PPF_EINVAL, "model_code '%.3s': digit %d must be '0' or '1'",
+                        model_code, i);
+        a.code[i] = c - '0';
+    }
+    if (nport == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T, *T2;
+    int rc = twiddles(ctx, nbin, st, &T, &T2);
+    if (rc) return rc;
+    a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2);
+    a.ngauss = ngauss; a.npar = 2 + 6 * ngauss;
+    a.params = params; a.scat_index = scattering_index; a.freqs = freqs; a.nu_ref = nu_ref;
+    a.T = T; a.T2 = T2; a.out = out;
+    if ((e = ppf::launch_gauss_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_gauss_port");
+    return PPF_OK;
+}
+
 int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, const double *model,
                     const double *freqs, const double *phi, const double *DM, const double *P,
                     double nu_ref, double noise, uint64_t seed, int64_t first_sub,

@@ -172,6 +172,19 @@ struct SynthArgs {
     void *out;
 };
 
+// pplib.gen_gaussian_portrait (pplib.py:886-963) per (portrait, channel) row
+struct GaussArgs {
+    int nport, nchan, nbin, log2N, ngauss, npar;
+    int code[3];                 // evolution code per (loc, wid, amp): 0 power law, 1 linear
+    const double *params;        // [nport][npar]: dc, tau [bin], ngauss x (loc, mloc, wid, mwid, amp, mamp)
+    const double *scat_index;    // [nport]
+    const double *freqs;         // [nport][nchan]
+    const double *nu_ref;        // [nport]
+    const double2 *T, *T2;
+    double *out;                 // [nport][nchan][nbin]
+};
+hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st);
+
 hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);

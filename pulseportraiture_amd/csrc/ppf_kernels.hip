@@ -690,6 +690,146 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
 }
 
 // ===========================================================================
+// k_gauss_port: pplib.gen_gaussian_portrait (pplib.py:886-963, join_ichans
+// = []), one workgroup per (portrait, channel) row.  Per component: the
+// evolved loc/wid/amp (evolve_parameter pplib.py:1032-1084), the wrapped,
+// truncated Gaussian of gaussian_profile (pplib.py:801-856) with its unit-peak
+// factor taken at the first argmax (a block reduction), accumulated into the
+// LDS row in component order as gen_gaussian_profile does (pplib.py:859-883).
+// A non-zero tau then convolves the row with the one-sided exponential
+// (rfft * 1/(1 + 2 pi i k tau_n) -> irfft, pplib.py:951-957, 4212-4260).
+// FP contraction is off so each product/sum rounds as NumPy's does.
+// ===========================================================================
+__device__ __forceinline__ double gp_evolve(double f, double nu_ref, double v, double e, int code) {
+#pragma clang fp contract(off)
+    if (code == 0) return exp((log(f) - log(nu_ref)) * e + 1.0 * log(v));   // power_law_evolution
+    return (f - nu_ref) * e + 1.0 * v;                                    // linear_evolution
+}
+
+__device__ __forceinline__ double gp_bin_center(int j, int nbin) {
+#pragma clang fp contract(off)
+    // np.linspace(1/(2 nbin), 1 - 1/(2 nbin), nbin) (get_bin_centers, pplib.py:694-707)
+    const double lo = 1.0 / (double)(nbin * 2), hi = 1.0 - 1.0 / (double)(nbin * 2);
+    if (j == nbin - 1) return hi;
+    const double step = (hi - lo) / (double)(nbin - 1);
+    return (double)j * step + lo;
+}
+
+// unnormalised retval of gaussian_profile at bin j (0 outside |z| < 20);
+// *xw receives the wrapped bin centre
+__device__ __forceinline__ double gp_raw(int j, int nbin, double mean, double sigma, double *xw) {
+#pragma clang fp contract(off)
+    double x = gp_bin_center(j, nbin);
+    if (mean < 0.5) { if (x > mean + 0.5) x = x - 1.0; }
+    else if (x < mean - 0.5) x = x + 1.0;
+    *xw = x;
+    const double z = (x - mean) / sigma;
+    if (!(fabs(z) < 20.0)) return 0.0;
+    return exp(-0.5 * (z * z)) / (sigma * 2.5066282746310002);   // sqrt(2 pi)
+}
+
+// NumPy's complex reciprocal (loops CDOUBLE_reciprocal) of 1 + i b
+__device__ __forceinline__ double2 scat_recip(double b) {
+#pragma clang fp contract(off)
+    if (fabs(b) <= 1.0) {
+        const double r = b / 1.0, d = 1.0 + b * r;
+        return cmk(1.0 / d, -r / d);
+    }
+    const double r = 1.0 / b, d = 1.0 * r + b;
+    return cmk(r / d, -1.0 / d);
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    __shared__ double red[kWaves * 2];
+    double *row = reinterpret_cast<double *>(lds);
+    const int nbin = a.nbin, N = nbin >> 1;
+    const int p = blockIdx.x / a.nchan, n = blockIdx.x % a.nchan;
+    const double *prm = a.params + (int64_t)p * a.npar;
+    const double f = a.freqs[(int64_t)p * a.nchan + n], nu_ref = a.nu_ref[p];
+    const double dc = prm[0];
+    for (int j = threadIdx.x; j < nbin; j += kBlock) row[j] = dc;   // zeros + DC
+    const double fwhm = 2.0 * sqrt(2.0 * log(2.0));
+    for (int g = 0; g < a.ngauss; ++g) {
+        const double *c = prm + 2 + 6 * g;
+        const double L = gp_evolve(f, nu_ref, c[0], c[1], a.code[0]);
+        const double W = gp_evolve(f, nu_ref, c[2], c[3], a.code[1]);
+        const double A = gp_evolve(f, nu_ref, c[4], c[5], a.code[2]);
+        if (!(W > 0.0)) {   // wid <= 0 (zeroout) or NaN: amp * zeros
+            for (int j = threadIdx.x; j < nbin; j += kBlock) row[j] = row[j] + A * 0.0;
+            continue;
+        }
+        const double sigma = W / fwhm;
+        double mean = fmod(L, 1.0);                  // Python/NumPy L % 1.0
+        if (mean != 0.0 && mean < 0.0) mean += 1.0;
+        // first argmax of the unnormalised profile
+        double lmax = -1.0, xw;
+        int lidx = nbin;
+        for (int j = threadIdx.x; j < nbin; j += kBlock) {
+            const double r = gp_raw(j, nbin, mean, sigma, &xw);
+            if (r > lmax) { lmax = r; lidx = j; }
+        }
+        double v[1] = {lmax};
+        block_max<1>(v, red);
+        const double gmax = v[0];
+        double vi[1] = {lmax == gmax ? -(double)lidx : -(double)nbin};
+        block_max<1>(vi, red);
+        const int imax = (int)(-vi[0]);
+        double fact = 1.0;                            // all-zero profile: returned as is
+        if (gmax != 0.0) {
+            double xi;
+            (void)gp_raw(imax, nbin, mean, sigma, &xi);
+            const double zz = (xi - L) / sigma;
+            fact = exp(-0.5 * (zz * zz)) / gmax;
+        }
+        for (int j = threadIdx.x; j < nbin; j += kBlock) {
+            const double r = gp_raw(j, nbin, mean, sigma, &xw);
+            row[j] = row[j] + A * (fact * r);
+        }
+    }
+    const double tau = prm[1];
+    if (tau != 0.0) {
+        // taus = (tau / nbin) * (freqs / nu_ref)**alpha; B_k = 1 / (1 + 2 pi i k tau_n)
+        const double tn = tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]);
+        __syncthreads();
+        lds_fft(lds, a.log2N, a.T, false);
+        double2 Xk[KMAX], Xn[KMAX];
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < N) {
+                double2 X1 = rfft_bin(lds, N, a.T2, k);
+                double2 X2 = rfft_bin(lds, N, a.T2, N - k);
+                if (tn != 0.0) {
+                    X1 = cmul(X1, scat_recip((2.0 * kPi * (double)k) * tn));
+                    X2 = cmul(X2, scat_recip((2.0 * kPi * (double)(N - k)) * tn));
+                }
+                if (k == 0) { X1.y = 0.0; X2.y = 0.0; }   // irfft keeps DC, Nyquist real parts
+                Xk[i] = X1;
+                Xn[i] = X2;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        }
+        __syncthreads();
+        lds_fft(lds, a.log2N, a.T, true);
+        const double sc = 1.0 / (double)N;
+        double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
+        for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
+        return;
+    }
+    __syncthreads();
+    double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
+    for (int j = threadIdx.x; j < N; j += kBlock) o[j] = lds[j];
+}
+
+// ===========================================================================
 // host-side launchers
 // ===========================================================================
 static inline int log2i(int n) {
@@ -776,6 +916,19 @@ hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
     size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
     hipLaunchKernelGGL(k_guess, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
+    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    dim3 g((unsigned)((int64_t)a.nport * a.nchan)), b(kBlock);
+    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+        case 1: hipLaunchKernelGGL(k_gauss_port<1>, g, b, lds, st, a); break;
+        case 2: hipLaunchKernelGGL(k_gauss_port<2>, g, b, lds, st, a); break;
+        case 4: hipLaunchKernelGGL(k_gauss_port<4>, g, b, lds, st, a); break;
+        case 8: hipLaunchKernelGGL(k_gauss_port<8>, g, b, lds, st, a); break;
+        case 16: hipLaunchKernelGGL(k_gauss_port<16>, g, b, lds, st, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st) {

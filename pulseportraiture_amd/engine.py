@@ -275,6 +275,39 @@ def phase_shift_batch(data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
     return out
 
 
+def gauss_portraits(model_code, params, scattering_index, freqs, nu_ref, nbin,
+                    dev=None):
+    """Gaussian-component model portraits (pplib.gen_gaussian_portrait,
+    pplib.py:886-963) on the device: params [nport, 2 + 6 ngauss] (DC, tau
+    [bin], per component loc, m_loc, wid, m_wid, amp, m_amp),
+    scattering_index [nport], freqs [nport, nchan], nu_ref [nport] ->
+    float64 [nport, nchan, nbin]."""
+    dev = device(dev)
+    code = str(model_code)
+    if len(code) != 3 or any(c not in "01" for c in code):
+        raise KeyError(code)     # evolve_parameter's dictionary lookup
+    prm = to_dev(params, dev, torch.float64)
+    if prm.dim() == 1:
+        prm = prm.unsqueeze(0)
+    nport, npar = prm.shape
+    if npar < 2 or (npar - 2) % 6:
+        raise ValueError("params must hold 2 + 6*ngauss values per portrait")
+    f = to_dev(freqs, dev, torch.float64).reshape(nport, -1).contiguous()
+    nchan = f.shape[1]
+    si = to_dev(np.broadcast_to(np.asarray(scattering_index, dtype=float),
+                                (nport,)), dev, torch.float64).contiguous()
+    nr = to_dev(np.broadcast_to(np.asarray(nu_ref, dtype=float), (nport,)),
+                dev, torch.float64).contiguous()
+    out = torch.empty((nport, nchan, int(nbin)), dtype=torch.float64,
+                      device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_gauss_portrait_batch(
+        ctx, nport, nchan, int(nbin), (npar - 2) // 6, code.encode(),
+        _p(prm), _p(si), _p(f), _p(nr), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
 def synth(model, freqs, phi, DM, P, nu_ref, noise, seed, out_dtype=torch.float32,
           dev=None, first=0):
     """Synthetic sub-integrations [nsub, nchan, nbin] on the device."""

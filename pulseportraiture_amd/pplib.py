@@ -121,69 +121,34 @@ def scattering_portrait_FT(taus, nbin, binshift=binshift):
     return out
 
 
-# -------------------------------------------- Gaussian models (host, once) --
-def _evolve(freqs, nu_ref, value, evol, code):
-    """evolve_parameter (pplib.py:1032-1084): '0' power law, '1' linear."""
-    if code == "0":
-        return np.exp(np.outer(np.log(freqs) - np.log(nu_ref), evol) +
-                      np.outer(np.ones(len(freqs)), np.log(value)))
-    if code == "1":
-        return np.outer(freqs - nu_ref, evol) + \
-            np.outer(np.ones(len(freqs)), value)
-    raise KeyError(code)
-
-
+# ------------------------------------------ Gaussian models (device) --------
 def gaussian_profile(nbin, loc, wid, norm=False, abs_wid=False, zeroout=True):
-    """pplib.py:801-856: unit-peak (or unit-area) wrapped Gaussian."""
+    """pplib.py:801-856 (unit peak, zeroout): one row of k_gauss_port with
+    the linear evolution code at nu = nu_ref, which passes loc, wid and the
+    unit amplitude through exactly."""
+    if norm or not zeroout:
+        raise NotImplementedError("gaussian_profile(norm=True / zeroout="
+                                  "False) is outside the accelerated path")
     if abs_wid:
         wid = abs(wid)
-    if wid == 0.0 or (wid < 0.0 and zeroout):
-        return np.zeros(nbin, "d")
-    sigma = wid / (2 * np.sqrt(2 * np.log(2)))
-    mean = loc % 1.0
-    x = get_bin_centers(nbin)
-    if mean < 0.5:
-        x = np.where(x > mean + 0.5, x - 1.0, x)
-    else:
-        x = np.where(x < mean - 0.5, x + 1.0, x)
-    z = (x - mean) / sigma
-    ok = np.fabs(z) < 20.0
-    prof = np.zeros(nbin, "d")
-    prof[ok] = np.exp(-0.5 * z[ok] ** 2.0) / (sigma * np.sqrt(2 * np.pi))
-    if norm or np.max(abs(prof)) == 0.0:
-        return prof
-    imax = prof.argmax()
-    zz = (x[imax] - loc) / sigma
-    return np.exp(-0.5 * zz ** 2.0) / prof[imax] * prof
+    params = [0.0, 0.0, loc, 0.0, wid, 0.0, 1.0, 0.0]
+    return gen_gaussian_portrait("111", params, 0.0, np.zeros(nbin), [1.0],
+                                 1.0)[0]
 
 
 def gen_gaussian_portrait(model_code, params, scattering_index, phases, freqs,
                           nu_ref, join_ichans=[], P=None):
-    """pplib.py:886-963 for join_ichans == [] (host, once per archive)."""
+    """pplib.py:886-963 for join_ichans == [], built on the device by
+    ppf_gauss_portrait_batch (k_gauss_port)."""
     if len(join_ichans):
         raise NotImplementedError("join_ichans (ppgauss only) is out of scope")
+    from . import engine
     params = np.asarray(params, dtype=float)
-    dc, tau = params[0], params[1]
-    locs, mlocs = params[2::6], params[3::6]
-    wids, mwids = params[4::6], params[5::6]
-    amps, mamps = params[6::6], params[7::6]
-    nbin, nchan = len(phases), len(freqs)
-    L = _evolve(freqs, nu_ref, locs, mlocs, model_code[0])
-    W = _evolve(freqs, nu_ref, wids, mwids, model_code[1])
-    A = _evolve(freqs, nu_ref, amps, mamps, model_code[2])
-    port = np.empty([nchan, nbin])
-    for ichan in range(nchan):
-        prof = np.zeros(nbin) + dc
-        for ig in range(len(locs)):
-            prof = prof + A[ichan, ig] * gaussian_profile(nbin, L[ichan, ig],
-                                                          W[ichan, ig])
-        port[ichan] = prof
-    if tau != 0.0:
-        taus = scattering_times(float(tau) / nbin, scattering_index, freqs,
-                                nu_ref)
-        port = np.fft.irfft(scattering_portrait_FT(taus, nbin) *
-                            np.fft.rfft(port, axis=-1), axis=-1)
-    return port
+    out = engine.gauss_portraits(model_code, params[None, :],
+                                 [scattering_index],
+                                 np.asarray(freqs, dtype=float)[None, :],
+                                 [nu_ref], len(phases))
+    return out[0].cpu().numpy()
 
 
 def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):

@@ -92,34 +92,38 @@ class GetTOAs(object):
 
     # ------------------------------------------------------------------
     def _models(self, d, ok_isubs, fit_scat, quiet):
-        """Model portrait per sub-integration (pptoas.py:385-419), built once
-        per distinct frequency set (host precompute)."""
+        """Model portrait per sub-integration (pptoas.py:385-419): the
+        .gmodel is parsed once (read_model, pplib.py:2971-3057) and every
+        distinct (frequency set, TAU [bin]) portrait of the archive is built
+        in ONE ppf_gauss_portrait_batch launch (k_gauss_port)."""
         if self.is_FITS_model:
             raise NotImplementedError("FITS (archive) templates need PSRCHIVE")
-        cache, models, index = {}, [], []
+        (self.model_name, code, nu_ref, self.ngauss, gparams, _mff, alpha,
+         _mfa) = read_model(self.modelfile, quiet=True)
+        if fit_scat:
+            (self.model_code, self.model_nu_ref, self.gparams,
+             self.alpha) = code, nu_ref, gparams, alpha
+        nbin = len(d.phases)
+        cache, prms, freqs, index = {}, [], [], []
         for isub in ok_isubs:
-            key = d.freqs[isub].tobytes()
+            p = np.copy(gparams)
+            if fit_scat:
+                p[1] = 0.0                 # unscattered template (pptoas.py:408-417)
+            elif p[1] != 0.0:
+                p[1] *= nbin / d.Ps[isub]  # read_model's TAU [s] -> [bin]
+            key = (d.freqs[isub].tobytes(), float(p[1]))
             if key not in cache:
-                if not fit_scat:
-                    self.model_name, self.ngauss, model = read_model(
-                        self.modelfile, d.phases, d.freqs[isub], d.Ps[isub],
-                        quiet=True)
-                else:
-                    self.model_name, self.ngauss, _ = read_model(
-                        self.modelfile, d.phases, d.freqs[isub], d.Ps[isub],
-                        quiet=True)
-                    (self.model_name, self.model_code, self.model_nu_ref,
-                     self.ngauss, self.gparams, _mff, self.alpha,
-                     _mfa) = read_model(self.modelfile, quiet=True)
-                    unscat = np.copy(self.gparams)
-                    unscat[1] = 0.0
-                    model = gen_gaussian_portrait(self.model_code, unscat, 0.0,
-                                                  d.phases, d.freqs[isub],
-                                                  self.model_nu_ref)
-                cache[key] = len(models)
-                models.append(model)
+                cache[key] = len(prms)
+                prms.append(p)
+                freqs.append(np.asarray(d.freqs[isub], dtype=float))
             index.append(cache[key])
-        return np.array(models), np.array(index, dtype=np.int32)
+        if not prms:
+            return np.zeros((0, len(d.freqs[0]), nbin)), \
+                np.zeros(0, dtype=np.int32)
+        models = engine.gauss_portraits(
+            code, np.stack(prms), 0.0 if fit_scat else alpha,
+            np.stack(freqs), nu_ref, nbin).cpu().numpy()
+        return models, np.array(index, dtype=np.int32)
 
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None,
                  bary=True, fit_DM=True, fit_GM=False, fit_scat=False,

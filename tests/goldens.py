@@ -191,3 +191,17 @@ def zap():
         zp.append(zz)
     c["chi2"], c["zap"] = chi, zp
     return c
+
+
+def gauss():
+    """tests/golden/gauss.npz (make_golden_gauss.py): the reference's
+    gen_gaussian_portrait / gaussian_profile / read_model outputs."""
+    z = _load("gauss.npz")
+    return Case({k: z[k] for k in z.files})
+
+
+def gauss_case(g, name):
+    return dict(code=str(g[name + "__code"]), params=g[name + "__params"],
+                alpha=float(g[name + "__alpha"]),
+                nu_ref=float(g[name + "__nu_ref"]),
+                freqs=g[name + "__freqs"], out=g[name + "__out"])

@@ -754,3 +754,67 @@ def test_channels_to_zap_matches_reference(monkeypatch, tmp_path):
     assert ppzap.main(["-d", str(meta), "-m", gm, "-o", str(paz),
                        "--quiet"]) == 0
     assert paz.read_text() == str(g["ppzap_paz_out"][0])
+
+
+# ------------------------------------------------ device model templates ---
+# x max|portrait|: exp/log/pow and FFT rounding differ from NumPy's by an
+# ulp; a 1-ulp change of an evolved loc moves a sub-bin Gaussian
+# (sigma = 1.7e-4 rot in mixed_scat_48x1024) by ~ulp/sigma, i.e. ~1e-12
+GAUSS_ATOL = 1e-11
+
+
+def test_gauss_portraits_match_reference(ppl, tmp_path):
+    """k_gauss_port (ppf_gauss_portrait_batch) against the reference's own
+    gen_gaussian_portrait / gaussian_profile / read_model outputs
+    (tests/golden/make_golden_gauss.py), one portrait per call and all
+    same-shape portraits in one batched launch."""
+    from pulseportraiture_amd import engine
+    g = G.gauss()
+    devs = {}
+    for name in g["cases"]:
+        c = G.gauss_case(g, str(name))
+        nbin = c["out"].shape[1]
+        out = ppl.gen_gaussian_portrait(c["code"], c["params"], c["alpha"],
+                                        np.zeros(nbin), c["freqs"],
+                                        c["nu_ref"])
+        devs[str(name)] = np.abs(out - c["out"]).max() / \
+            np.abs(c["out"]).max()
+        # zeroed rows / bins stay exactly zero where the reference's are
+        if c["params"][1] == 0.0:
+            assert np.array_equal(out == 0.0, c["out"] == 0.0), name
+    print("relative max deviation per case:", devs)
+    assert max(devs.values()) <= GAUSS_ATOL, devs
+    for i in range(int(g["nprof"])):
+        nbin, loc, wid = g["prof%d__args" % i]
+        ref = g["prof%d__out" % i]
+        got = ppl.gaussian_profile(int(nbin), loc, wid)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=GAUSS_ATOL)
+    # batch: three portraits of one shape (different freqs, nu_ref, tau)
+    c = G.gauss_case(g, "example_64x512")
+    nbin = c["out"].shape[1]
+    prm = np.stack([c["params"]] * 3)
+    prm[1, 1] = 5.0
+    prm[2, 0] = 0.3
+    freqs = np.stack([c["freqs"], c["freqs"][::-1], c["freqs"] * 0.5])
+    batch = engine.gauss_portraits(c["code"], prm, [c["alpha"]] * 3, freqs,
+                                   [c["nu_ref"], 1500.0, 700.0], nbin)
+    batch = batch.cpu().numpy()
+    import oracle as O
+    for i, nr in enumerate([c["nu_ref"], 1500.0, 700.0]):
+        ref = O.gen_gaussian_portrait(c["code"], prm[i], c["alpha"],
+                                      np.zeros(nbin), freqs[i], nr)
+        np.testing.assert_allclose(batch[i], ref, rtol=0,
+                                   atol=GAUSS_ATOL * np.abs(ref).max())
+    # read_model with a TAU line: parse, TAU [s] -> [bin], device portrait
+    gm = tmp_path / "tau.gmodel"
+    gm.write_text(str(g["readmodel__text"]))
+    ref = g["readmodel__out"]
+    _, ngauss, model = ppl.read_model(str(gm), ppl.get_bin_centers(ref.shape[1]),
+                                      g["readmodel__freqs"],
+                                      float(g["readmodel__P"]), quiet=True)
+    assert ngauss == 2
+    np.testing.assert_allclose(model, ref, rtol=0,
+                               atol=GAUSS_ATOL * np.abs(ref).max())
+    with pytest.raises(KeyError):     # evolve_parameter's unknown code
+        ppl.gen_gaussian_portrait("020", c["params"], -4.0, np.zeros(nbin),
+                                  c["freqs"], c["nu_ref"])

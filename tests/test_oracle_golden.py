@@ -127,26 +127,26 @@ def test_get_toas_oracle_vs_reference():
 
 def _gmodel_portrait(nchan, nbin, freqs, P):
     """The example.gmodel portrait GetTOAs builds per sub-integration
-    (read_model at full precision, pptoas.py:396-399), regenerated host-side."""
+    (read_model at full precision, pptoas.py:396-399), regenerated by the
+    oracle's gen_gaussian_portrait."""
     from pulseportraiture_amd import pplib as PL
+    import oracle as O
     import os
     gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
-    _, _, model = PL.read_model(gm, PL.get_bin_centers(nbin), freqs, P,
-                                quiet=True)
-    return model
+    (_, code, nu_ref, _, params, _, alpha, _) = PL.read_model(gm, quiet=True)
+    params[1] *= nbin / P                     # read_model's TAU [s] -> [bin]
+    return O.gen_gaussian_portrait(code, params, alpha, np.zeros(nbin),
+                                   freqs, nu_ref)
 
 
-def test_host_gmodel_matches_reference_model():
-    """Host .gmodel portrait generation (pplib.read_model mirror) against the
-    reference's own portraits stored (float32-rounded) in the golden cases."""
-    from pulseportraiture_amd import pplib as PL
-    import os
-    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+def test_oracle_gmodel_matches_reference_model():
+    """The oracle's .gmodel portrait generation against the reference's own
+    portraits stored (float32-rounded) in the golden cases."""
     for name in ("pd_64x512", "pd_128x1024", "pd_512x2048"):
         c = G.full_case(name)
         nbin = c["model"].shape[1]
-        _, _, model = PL.read_model(gm, PL.get_bin_centers(nbin), c["freqs"],
-                                    float(c["P"]), quiet=True)
+        model = _gmodel_portrait(c["model"].shape[0], nbin, c["freqs"],
+                                 float(c["P"]))
         ref = c["model"].astype(np.float64)
         ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
         assert np.all(np.abs(model - ref) <= ulp + 1e-12)
@@ -235,3 +235,34 @@ def test_ppzap_host_logic_matches_reference(tmp_path):
     out = tmp_path / "paz.txt"
     ppzap.print_paz_cmds(files, zl[:2], outfile=str(out), quiet=True)
     assert out.read_text() == str(g["ppzap_paz_out"][5])
+
+
+def test_oracle_gaussian_portraits_match_reference(tmp_path):
+    """The oracle's gen_gaussian_portrait / gaussian_profile reproduce the
+    reference's own outputs bit for bit (both evolution codes, wrapped and
+    out-of-range locs, widths through zero, scattering), and read_model's
+    parse + TAU scaling feeds it the reference's parameters."""
+    import oracle as O
+    from pulseportraiture_amd import pplib as PL
+    g = G.gauss()
+    for name in g["cases"]:
+        c = G.gauss_case(g, str(name))
+        nbin = c["out"].shape[1]
+        out = O.gen_gaussian_portrait(c["code"], c["params"], c["alpha"],
+                                      np.zeros(nbin), c["freqs"], c["nu_ref"])
+        np.testing.assert_array_equal(out, c["out"])
+    for i in range(int(g["nprof"])):
+        nbin, loc, wid = g["prof%d__args" % i]
+        np.testing.assert_array_equal(O.gaussian_profile(int(nbin), loc, wid),
+                                      g["prof%d__out" % i])
+    gm = tmp_path / "tau.gmodel"
+    gm.write_text(str(g["readmodel__text"]))
+    (_, code, nu_ref, ngauss, params, _, alpha, _) = PL.read_model(str(gm),
+                                                                   quiet=True)
+    ref = g["readmodel__out"]
+    nbin, P = ref.shape[1], float(g["readmodel__P"])
+    assert ngauss == 2 and params[1] != 0.0
+    params[1] *= nbin / P
+    out = O.gen_gaussian_portrait(code, params, alpha, np.zeros(nbin),
+                                  g["readmodel__freqs"], nu_ref)
+    np.testing.assert_array_equal(out, ref)

@@ -127,6 +127,8 @@ struct AlignArgs {
 };
 int align_groups(int nsub, int nchan);
 hipError_t launch_align(const AlignArgs &a, hipStream_t st);
+bool align_wave_supported(int log2N);                                   // nbin 256..2048
+hipError_t launch_align_part_w(const AlignArgs &a, hipStream_t st);     // wave-per-row partials
 
 // per-row reduced chi^2 of (rotated data - scale * model) (the channel test
 // of pptoas.get_channels_to_zap, pptoas.py:1266-1343 via show_fit 1375-1480)

@@ -12,6 +12,7 @@
 //                   streaming pass over X; then zero-covariance frequencies,
 //                   output transform, O(nchan) Schur covariance, scales, S/N
 // Standalone kernels: k_rotate, k_noise, k_phase_shift, k_synth.
+#include <cstdlib>
 #include <type_traits>
 
 #include "ppf_device.hpp"
@@ -1044,16 +1045,24 @@ __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
 hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
     const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 gp((unsigned)((int64_t)a.ngroup * a.nchan)), gf((unsigned)a.nchan), b(kBlock);
+    // wave-per-row partials where the register FFT covers nbin; the
+    // block-FFT k_align_part otherwise (PPF_ALIGN_BLOCK=1 forces it)
+    static const bool force_block = getenv("PPF_ALIGN_BLOCK") && atoi(getenv("PPF_ALIGN_BLOCK"));
+    const bool wave = !force_block && align_wave_supported(a.log2N);
+    if (wave) {
+        hipError_t e = launch_align_part_w(a, st);
+        if (e != hipSuccess) return e;
+    }
     switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
-        case 1: hipLaunchKernelGGL(k_align_part<1>, gp, b, lds, st, a);
+        case 1: if (!wave) hipLaunchKernelGGL(k_align_part<1>, gp, b, lds, st, a);
                 hipLaunchKernelGGL(k_align_fin<1>, gf, b, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_align_part<2>, gp, b, lds, st, a);
+        case 2: if (!wave) hipLaunchKernelGGL(k_align_part<2>, gp, b, lds, st, a);
                 hipLaunchKernelGGL(k_align_fin<2>, gf, b, lds, st, a); break;
-        case 4: hipLaunchKernelGGL(k_align_part<4>, gp, b, lds, st, a);
+        case 4: if (!wave) hipLaunchKernelGGL(k_align_part<4>, gp, b, lds, st, a);
                 hipLaunchKernelGGL(k_align_fin<4>, gf, b, lds, st, a); break;
-        case 8: hipLaunchKernelGGL(k_align_part<8>, gp, b, lds, st, a);
+        case 8: if (!wave) hipLaunchKernelGGL(k_align_part<8>, gp, b, lds, st, a);
                 hipLaunchKernelGGL(k_align_fin<8>, gf, b, lds, st, a); break;
-        case 16: hipLaunchKernelGGL(k_align_part<16>, gp, b, lds, st, a);
+        case 16: if (!wave) hipLaunchKernelGGL(k_align_part<16>, gp, b, lds, st, a);
                  hipLaunchKernelGGL(k_align_fin<16>, gf, b, lds, st, a); break;
         default: return hipErrorInvalidValue;
     }

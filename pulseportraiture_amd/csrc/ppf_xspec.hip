@@ -642,6 +642,131 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// k_align_part_w: ppalign accumulation (ppalign.py:236-247) with one row per
+// wave.  Block = (channel n, group g of sub-ints) of kXW waves; wave w takes
+// the group's sub-ints s0 + w, s0 + w + kXW, ... in order: register radix
+// FFT of the row (next row in flight), real post-pass, times
+// w exp(2 pi i k phase) (phasors by recurrence from exp(2 pi i lane phase),
+// step exp(2 pi i 64 phase)), summed in registers.  The waves' sums are then
+// added in wave order through LDS (fixed order: bitwise reproducible) and
+// written as the group partial that k_align_fin reduces and inverts.
+// ===========================================================================
+template <int LOG2N, int DT>
+__global__ __launch_bounds__(64 * kXW) void k_align_part_w(AlignArgs a) {
+    using P = wfft::Plan<LOG2N>;
+    constexpr int N = P::N, R = P::R, NP = N / 128;
+    constexpr int SL = xspec_slw<LOG2N>();
+    constexpr int SMID = SL - 2, SW = SL - 1;         // harmonic N/2, weight sum
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *buf = lds + wave * SL;
+    const int n = blockIdx.x % a.nchan, g = blockIdx.x / a.nchan;
+    const int per = (a.nsub + a.ngroup - 1) / a.ngroup;
+    const int s0 = g * per, s1 = min(a.nsub, s0 + per);
+    const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    const RowT *rows = reinterpret_cast<const RowT *>(a.in);
+    double2 Alo[NP], Ahi[NP], Am = cmk(0.0, 0.0);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Alo[i] = Ahi[i] = cmk(0.0, 0.0);
+    double wtot = 0.0;
+    RowT zr[R];
+    auto next_live = [&](int s) {      // rows with w == 0 are skipped (uniform per wave)
+        while (s < s1 && a.weights[(int64_t)s * a.nchan + n] == 0.0) s += kXW;
+        return s;
+    };
+    auto fetch = [&](int s) {
+        const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
+#pragma unroll
+        for (int q = 0; q < R; ++q) zr[q] = src[lane + 64 * q];
+    };
+    int s = next_live(s0 + wave);
+    if (s < s1) fetch(s);
+    while (s < s1) {
+        const int64_t row = (int64_t)s * a.nchan + n;
+        const double w = a.weights[row], ph = a.phases[row];
+        wtot += w;
+        double2 x[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+        const int sn = next_live(s + kXW);
+        if (sn < s1) fetch(sn);                        // next row in flight during this FFT
+        wfft::fft_row<LOG2N>(x, buf, a.T, lane);
+        const double2 Es = cexp2pi(64.0 * ph);
+        double2 E = cexp2pi((double)lane * ph);                        // k = lane + 64 i
+        double2 Eh = cmul(cexp2pi((double)N * ph), cconj(E));           // k = N - lane - 64 i
+        double2 wt = w_seed;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int klo = lane + 64 * i;
+            double2 Dlo, Dhi;
+            rfft_pair<LOG2N>(buf, klo, wt, Dlo, Dhi);
+            wt = cmul(wt, w_step);
+            Alo[i] = cadd(Alo[i], cscale(cmul(Dlo, E), w));
+            Ahi[i] = cadd(Ahi[i], cscale(cmul(Dhi, Eh), w));
+            E = cmul(E, Es);
+            Eh = cmul(Eh, cconj(Es));
+        }
+        if (lane == 0) {
+            const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
+            Am = cadd(Am, cscale(cmul(cmk(zm.x, -zm.y), cexp2pi((double)(N / 2) * ph)), w));
+        }
+        s = sn;
+    }
+    // this wave's sums into its buffer: k -> pad(k), N - k -> pad(N - k)
+    // (k = 0: N -> pad(N / 2)), N / 2 -> SMID, weight sum -> SW
+    wfft::wave_sync();
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int klo = lane + 64 * i;
+        buf[wfft::pad<LOG2N>(klo)] = Alo[i];
+        buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(N - klo)] = Ahi[i];
+    }
+    if (lane == 0) {
+        buf[SMID] = Am;
+        buf[SW] = cmk(wtot, 0.0);
+    }
+    __syncthreads();
+    double2 *Pp = a.part + ((int64_t)g * a.nchan + n) * (N + 1);
+    for (int k = threadIdx.x; k <= N; k += 64 * kXW) {
+        const int slot = k == N ? wfft::pad<LOG2N>(N / 2) : (k == N / 2 ? SMID : wfft::pad<LOG2N>(k));
+        double2 acc = lds[slot];
+#pragma unroll
+        for (int w2 = 1; w2 < kXW; ++w2) acc = cadd(acc, lds[w2 * SL + slot]);
+        Pp[k] = acc;
+    }
+    if (threadIdx.x == 0) {
+        double wsum = lds[SW].x;
+        for (int w2 = 1; w2 < kXW; ++w2) wsum += lds[w2 * SL + SW].x;
+        a.wpart[(int64_t)g * a.nchan + n] = wsum;
+    }
+}
+
+template <int L2, int DT>
+static void launch_align_w_t(const AlignArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)kXW * xspec_slw<L2>() * sizeof(double2);
+    hipLaunchKernelGGL((k_align_part_w<L2, DT>), dim3((unsigned)((int64_t)a.ngroup * a.nchan)),
+                       dim3(64 * kXW), lds, st, a);
+}
+
+bool align_wave_supported(int log2N) { return log2N >= 7 && log2N <= 10; }
+
+hipError_t launch_align_part_w(const AlignArgs &a, hipStream_t st) {
+    switch (a.log2N * 2 + a.dtype) {
+        case 14: launch_align_w_t<7, 0>(a, st); break;
+        case 15: launch_align_w_t<7, 1>(a, st); break;
+        case 16: launch_align_w_t<8, 0>(a, st); break;
+        case 17: launch_align_w_t<8, 1>(a, st); break;
+        case 18: launch_align_w_t<9, 0>(a, st); break;
+        case 19: launch_align_w_t<9, 1>(a, st); break;
+        case 20: launch_align_w_t<10, 0>(a, st); break;
+        case 21: launch_align_w_t<10, 1>(a, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_btab(int N, double *Bt, hipStream_t st) {
     hipLaunchKernelGGL(k_btab, dim3((unsigned)((N / 2 * 16 + 255) / 256)), dim3(256), 0, st, N, Bt);
     return hipGetLastError();

@@ -177,38 +177,63 @@ def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
     per-row rotation phases and weights of ppalign.py:222-247."""
     S = R.n
     nchan = model_port.shape[0]
-    phases = np.zeros((S, nchan))
-    weights = np.zeros((S, nchan))
+    f64 = torch.float64
     multi = np.where(R.nchanx > 1)[0]
+    # the rows' constant inputs stay resident across iterations
+    dc = R.__dict__.setdefault("_dev_inputs", {})
+    if dc.get("multi") is None or not np.array_equal(dc["multi"], multi):
+        dc.clear()
+        dc["multi"] = multi
+        dc["freqs"] = torch.as_tensor(R.freqs[multi], dtype=f64, device=dev)
+        dc["P"] = torch.as_tensor(R.P[multi], dtype=f64, device=dev)
+        dc["errs"] = torch.as_tensor(R.errs[multi], dtype=f64, device=dev)
+        dc["mask"] = torch.as_tensor(R.mask[multi], dtype=torch.uint8,
+                                     device=dev)
+        dc["gw"] = torch.as_tensor(R.gw[multi], dtype=f64, device=dev)
+        dc["DM"] = torch.as_tensor(R.DM_guess[multi], dtype=f64, device=dev)
+        init = np.zeros((len(multi), 5))
+        init[:, 1] = R.DM_guess[multi]
+        dc["init"] = torch.as_tensor(init, dtype=f64, device=dev)
+        dc["nu_fits"] = torch.as_tensor(
+            np.repeat(R.nu_fit[multi, None], 3, axis=1), dtype=f64,
+            device=dev)
+        dc["nu_outs"] = torch.full((len(multi), 3), float("nan"), dtype=f64,
+                                   device=dev)
+    phases = torch.zeros((S, nchan), dtype=f64, device=dev)
+    weights = torch.zeros((S, nchan), dtype=f64, device=dev)
     if len(multi):
         rows = R.data[:, 0] if len(multi) == S else \
             R.data[torch.as_tensor(multi, device=dev), 0]
-        init = np.zeros((len(multi), 5))
-        init[:, 1] = R.DM_guess[multi]
         flags = [1, int(bool(fit_dm)), 0, 0, 0]
         res = engine.fit_batch(
-            rows, model_port, R.freqs[multi], R.P[multi], init,
-            flags, nu_fits=np.repeat(R.nu_fit[multi, None], 3, axis=1),
-            nu_outs=np.full((len(multi), 3), np.nan), errs=R.errs[multi],
-            chan_mask=R.mask[multi], log10_tau=False, is_toa=True,
-            guess=True, guess_weights=R.gw[multi],
-            guess_DM=R.DM_guess[multi], guess_Ns=nbin, dev=dev)
-        r = engine.results_numpy(res)
+            rows, model_port, dc["freqs"], dc["P"], dc["init"],
+            flags, nu_fits=dc["nu_fits"], nu_outs=dc["nu_outs"],
+            errs=dc["errs"], chan_mask=dc["mask"], log10_tau=False,
+            is_toa=True, guess=True, guess_weights=dc["gw"],
+            guess_DM=dc["DM"], guess_Ns=nbin, dev=dev)
         I = _lib.RESULT_INDEX
-        st = r["results"][:, I["status"]].astype(np.int64)
+        r = res["results"]
+        st = r[:, I["status"]].to(torch.int64).cpu().numpy()
         bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
         if len(bad):
             from .pplib import _raise_status
             _raise_status(int(st[bad[0]]))
-        phi = r["results"][:, I["params"]][:, 0]
-        DM = r["results"][:, I["params"]][:, 1]
-        nu_ref = r["results"][:, I["nu_out"]][:, 0]
-        ok = R.mask[multi] != 0
-        fr = R.freqs[multi]
-        ph = phi[:, None] + (Dconst * DM / R.P[multi])[:, None] * (
+        phi = r[:, I["params"]][:, 0]
+        DM = r[:, I["params"]][:, 1]
+        nu_ref = r[:, I["nu_out"]][:, 0]
+        ok = dc["mask"] != 0
+        fr = dc["freqs"]
+        ph = phi[:, None] + (Dconst * DM / dc["P"])[:, None] * (
             fr ** -2.0 - (nu_ref ** -2.0)[:, None])
-        phases[multi] = np.where(ok, ph, 0.0)
-        weights[multi] = np.where(ok, r["scales"] / R.errs[multi] ** 2, 0.0)
+        zero = torch.zeros((), dtype=f64, device=dev)
+        ph = torch.where(ok, ph, zero)
+        wt = torch.where(ok, res["scales"] / dc["errs"] ** 2, zero)
+        if len(multi) == S:
+            phases, weights = ph, wt
+        else:
+            mi = torch.as_tensor(multi, device=dev)
+            phases[mi] = ph
+            weights[mi] = wt
     for s in np.where(R.nchanx == 1)[0]:      # 1-channel hack (ppalign.py:231-236)
         m = int(np.where(R.mask[s])[0][0])
         x = R.data[s, 0, m].double().cpu().numpy()

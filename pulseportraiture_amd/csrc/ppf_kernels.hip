@@ -208,10 +208,36 @@ __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int 
                              double hi, double *sh /*LDS >= 2*Ns+8*/, double *fval, int *nfev) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double step = (Ns != 1) ? (hi - lo) / (double)(Ns - 1) : 1.0;
-    for (int j = wave; j < Ns; j += kWaves) {
-        double ph = (double)j * step + lo;
-        double f = wave_fps_eval(xm, nharm, ph, inv_err2);
-        if (lane == 0) sh[j] = f;
+    if (Ns >= 2 * kBlock) {
+        // large grids (ppalign: Ns = nbin): one point per lane, two points
+        // in flight; harmonics broadcast from LDS, phasor e^{2 pi i k ph} by
+        // recurrence, re-seeded exactly every 64 harmonics
+        for (int j0 = threadIdx.x; j0 < Ns; j0 += 2 * kBlock) {
+            const int j1 = j0 + kBlock;
+            const double ph0 = (double)j0 * step + lo;
+            const double ph1 = (double)(j1 < Ns ? j1 : j0) * step + lo;
+            const double2 W0 = cexp2pi(ph0), W1 = cexp2pi(ph1);
+            double acc0 = 0.0, acc1 = 0.0;
+            for (int kb = 0; kb < nharm; kb += 64) {
+                double2 E0 = cexp2pi((double)kb * ph0), E1 = cexp2pi((double)kb * ph1);
+                const int ke = min(nharm, kb + 64);
+                for (int k = kb; k < ke; ++k) {
+                    const double2 x = xm[k];
+                    acc0 = fma(x.x, E0.x, fma(-x.y, E0.y, acc0));
+                    acc1 = fma(x.x, E1.x, fma(-x.y, E1.y, acc1));
+                    E0 = cmul(E0, W0);
+                    E1 = cmul(E1, W1);
+                }
+            }
+            sh[j0] = -acc0 * inv_err2;
+            if (j1 < Ns) sh[j1] = -acc1 * inv_err2;
+        }
+    } else {
+        for (int j = wave; j < Ns; j += kWaves) {
+            double ph = (double)j * step + lo;
+            double f = wave_fps_eval(xm, nharm, ph, inv_err2);
+            if (lane == 0) sh[j] = f;
+        }
     }
     __syncthreads();
     if (wave == 0) {

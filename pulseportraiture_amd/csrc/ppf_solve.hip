@@ -892,10 +892,122 @@ enum { NZ_MAX = 16 };
 // ===========================================================================
 // k_postfit: one workgroup per sub-integration
 // ===========================================================================
-__global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
+// zero-covariance frequencies from the channel sums c[] (thread 0 of
+// k_postfit): the closed forms and np.roots cases of get_nu_zeros
+// (pptoaslib.py:776-950).  Out of line so that its root-finder locals do not
+// weigh on k_postfit's per-channel loops.
+__device__ __noinline__ void nz_solve(const double *c, int nzcase, int option, double nu_mean,
+                                      double *nz, int *no_root_out) {
+    double num, den;
+    bool no_root = false;
+    switch (nzcase) {
+        case 0x3: nz[0] = pow(c[0] / c[1], -0.5); break;
+        case 0x5: nz[1] = pow(c[0] / c[1], -0.25); break;
+        case 0x18: nz[2] = exp(c[0] / c[1]); break;
+        case 0xb: {
+            double H13 = c[16], H33 = c[17];
+            num = H13 * c[0] - H33 * c[1];
+            den = H13 * c[2] - H33 * c[3];
+            nz[0] = pow(num / den, -0.5);
+            break;
+        }
+        case 0x7: {
+            if (option == 0 || option == 1) {
+                double A = c[0], B = c[1], C = c[2], D = c[3], E = c[4], F = c[5], G = c[6],
+                       H = c[7];
+                double co[7] = {A * C - E * G, 0.0, E * H - A * D, 0.0, F * G - B * C, 0.0,
+                                B * D - F * H};
+                double roots[8];
+                int nr = poly_real_roots(co, 6, roots);
+                double best = 0.0, bd = 1e300;
+                bool any = false;
+                for (int i = 0; i < nr; ++i)
+                    if (roots[i] > 0.0 && fabs(nu_mean - roots[i]) < bd) {
+                        bd = fabs(nu_mean - roots[i]); best = roots[i]; any = true;
+                    }
+                if (any) { nz[0] = nz[1] = best; } else no_root = true;
+            }
+            break;
+        }
+        case 0x1b: {
+            double T[4][4];
+            int q = 12;
+            for (int i = 0; i < 4; ++i)
+                for (int j = i; j < 4; ++j) { T[i][j] = T[j][i] = c[q]; ++q; }
+            double H11 = T[0][0], H22 = T[1][1], H33 = T[2][2], H44 = T[3][3];
+            double H12 = T[0][1], H13 = T[0][2], H14 = T[0][3], H23 = T[1][2],
+                   H34 = T[2][3];
+            num = (H34 * H34 - H33 * H44) * c[0] + (H13 * H44 - H14 * H34) * c[1] +
+                  (H14 * H33 - H13 * H34) * c[2];
+            den = (H34 * H34 - H33 * H44) * c[3] + (H13 * H44 - H14 * H34) * c[4] +
+                  (H14 * H33 - H13 * H34) * c[5];
+            nz[0] = pow(num / den, -0.5);
+            num = (H13 * H22 - H12 * H23) * c[6] + (H11 * H23 - H12 * H13) * c[7] +
+                  (H12 * H12 - H11 * H22) * c[8];
+            den = (H13 * H22 - H12 * H23) * c[9] + (H11 * H23 - H12 * H13) * c[10] +
+                  (H12 * H12 - H11 * H22) * c[11];
+            nz[2] = exp(num / den);
+            break;
+        }
+        case 0xf: {
+            if (option == 0 || option == 1) {
+                double H14 = c[16], H44 = c[17];
+                double A = c[0], aa = c[1], B = c[2], b = c[3], C = c[4], cc = c[5],
+                       D = c[6], d = c[7], E = c[8], e = c[9], F = c[10], f = c[11];
+                double co[6];
+                int deg;
+                if (option == 0) {
+                    co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
+                            H14 * A * D;
+                    co[1] = -A * A * b - H44 * C * d - H14 * E * f + H44 * b * E + A * C * f +
+                            H14 * A * d;
+                    co[2] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
+                            (A * cc + aa * C) * F + H14 * aa * D;
+                    co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
+                            (A * cc + aa * C) * f - H14 * aa * d;
+                    co[4] = aa * aa * B - aa * cc * F;
+                    co[5] = -aa * aa * b + aa * cc * f;
+                    deg = 5;
+                } else {
+                    co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
+                            H14 * A * D;
+                    co[1] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
+                            (A * cc + aa * C) * F + H14 * aa * D;
+                    co[2] = -(A * A * b - aa * aa * B) - H44 * C * d - H14 * E * f +
+                            H44 * b * E + (A * C * f - aa * cc * F) + H14 * A * d;
+                    co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
+                            (A * cc + aa * C) * f - H14 * aa * d;
+                    co[4] = -aa * aa * b + aa * cc * f;
+                    deg = 4;
+                }
+                double roots[8];
+                int nr = poly_real_roots(co, deg, roots);
+                double best = 0.0, bd = 1e300;
+                bool any = false;
+                for (int i = 0; i < nr; ++i)
+                    if (roots[i] > 0.0) {
+                        double rr = sqrt(roots[i]);
+                        if (fabs(nu_mean - rr) < bd) { bd = fabs(nu_mean - rr); best = rr; any = true; }
+                    }
+                if (any) { nz[0] = nz[1] = best; } else no_root = true;
+            }
+            break;
+        }
+        default: break;
+    }
+    *no_root_out = no_root ? 1 : 0;
+}
+
+#ifdef PPF_POSTFIT_WPE
+#define PPF_POSTFIT_ATTR __attribute__((amdgpu_waves_per_eu(PPF_POSTFIT_WPE)))
+#else
+#define PPF_POSTFIT_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
     __shared__ double red[kWaves * 32];
     __shared__ double sh_Xinv[25];
     __shared__ double sh_misc[16];
+    __shared__ double sh_acc[NZ_MAX + 8];
     const int s = blockIdx.x, tid = threadIdx.x;
     const TRState &S = a.state[s];
     ppf_result *res = a.results + s;
@@ -1059,103 +1171,10 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
         }
         block_sum<NZ_MAX + 8>(accv, red);
         if (tid == 0) {
-            const double *c = accv;
-            double num, den;
-            switch (nzcase) {
-                case 0x3: nz[0] = pow(c[0] / c[1], -0.5); break;
-                case 0x5: nz[1] = pow(c[0] / c[1], -0.25); break;
-                case 0x18: nz[2] = exp(c[0] / c[1]); break;
-                case 0xb: {
-                    double H13 = c[16], H33 = c[17];
-                    num = H13 * c[0] - H33 * c[1];
-                    den = H13 * c[2] - H33 * c[3];
-                    nz[0] = pow(num / den, -0.5);
-                    break;
-                }
-                case 0x7: {
-                    if (a.option == 0 || a.option == 1) {
-                        double A = c[0], B = c[1], C = c[2], D = c[3], E = c[4], F = c[5], G = c[6],
-                               H = c[7];
-                        double co[7] = {A * C - E * G, 0.0, E * H - A * D, 0.0, F * G - B * C, 0.0,
-                                        B * D - F * H};
-                        double roots[8];
-                        int nr = poly_real_roots(co, 6, roots);
-                        double best = 0.0, bd = 1e300;
-                        bool any = false;
-                        for (int i = 0; i < nr; ++i)
-                            if (roots[i] > 0.0 && fabs(nu_mean - roots[i]) < bd) {
-                                bd = fabs(nu_mean - roots[i]); best = roots[i]; any = true;
-                            }
-                        if (any) { nz[0] = nz[1] = best; } else no_root = true;
-                    }
-                    break;
-                }
-                case 0x1b: {
-                    double T[4][4];
-                    int q = 12;
-                    for (int i = 0; i < 4; ++i)
-                        for (int j = i; j < 4; ++j) { T[i][j] = T[j][i] = c[q]; ++q; }
-                    double H11 = T[0][0], H22 = T[1][1], H33 = T[2][2], H44 = T[3][3];
-                    double H12 = T[0][1], H13 = T[0][2], H14 = T[0][3], H23 = T[1][2],
-                           H34 = T[2][3];
-                    num = (H34 * H34 - H33 * H44) * c[0] + (H13 * H44 - H14 * H34) * c[1] +
-                          (H14 * H33 - H13 * H34) * c[2];
-                    den = (H34 * H34 - H33 * H44) * c[3] + (H13 * H44 - H14 * H34) * c[4] +
-                          (H14 * H33 - H13 * H34) * c[5];
-                    nz[0] = pow(num / den, -0.5);
-                    num = (H13 * H22 - H12 * H23) * c[6] + (H11 * H23 - H12 * H13) * c[7] +
-                          (H12 * H12 - H11 * H22) * c[8];
-                    den = (H13 * H22 - H12 * H23) * c[9] + (H11 * H23 - H12 * H13) * c[10] +
-                          (H12 * H12 - H11 * H22) * c[11];
-                    nz[2] = exp(num / den);
-                    break;
-                }
-                case 0xf: {
-                    if (a.option == 0 || a.option == 1) {
-                        double H14 = c[16], H44 = c[17];
-                        double A = c[0], aa = c[1], B = c[2], b = c[3], C = c[4], cc = c[5],
-                               D = c[6], d = c[7], E = c[8], e = c[9], F = c[10], f = c[11];
-                        double co[6];
-                        int deg;
-                        if (a.option == 0) {
-                            co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
-                                    H14 * A * D;
-                            co[1] = -A * A * b - H44 * C * d - H14 * E * f + H44 * b * E + A * C * f +
-                                    H14 * A * d;
-                            co[2] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
-                                    (A * cc + aa * C) * F + H14 * aa * D;
-                            co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
-                                    (A * cc + aa * C) * f - H14 * aa * d;
-                            co[4] = aa * aa * B - aa * cc * F;
-                            co[5] = -aa * aa * b + aa * cc * f;
-                            deg = 5;
-                        } else {
-                            co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F -
-                                    H14 * A * D;
-                            co[1] = -2 * A * aa * B - H44 * cc * D - H14 * e * F + H44 * B * e +
-                                    (A * cc + aa * C) * F + H14 * aa * D;
-                            co[2] = -(A * A * b - aa * aa * B) - H44 * C * d - H14 * E * f +
-                                    H44 * b * E + (A * C * f - aa * cc * F) + H14 * A * d;
-                            co[3] = 2 * A * aa * b + H44 * cc * d + H14 * e * f - H44 * b * e -
-                                    (A * cc + aa * C) * f - H14 * aa * d;
-                            co[4] = -aa * aa * b + aa * cc * f;
-                            deg = 4;
-                        }
-                        double roots[8];
-                        int nr = poly_real_roots(co, deg, roots);
-                        double best = 0.0, bd = 1e300;
-                        bool any = false;
-                        for (int i = 0; i < nr; ++i)
-                            if (roots[i] > 0.0) {
-                                double rr = sqrt(roots[i]);
-                                if (fabs(nu_mean - rr) < bd) { bd = fabs(nu_mean - rr); best = rr; any = true; }
-                            }
-                        if (any) { nz[0] = nz[1] = best; } else no_root = true;
-                    }
-                    break;
-                }
-                default: break;
-            }
+            for (int i = 0; i < NZ_MAX + 8; ++i) sh_acc[i] = accv[i];
+            int nr_flag = 0;
+            nz_solve(sh_acc, nzcase, a.option, nu_mean, nz, &nr_flag);
+            no_root = nr_flag != 0;
             sh_misc[4] = nz[0]; sh_misc[5] = nz[1]; sh_misc[6] = nz[2];
             sh_misc[7] = no_root ? 1.0 : 0.0;
         }
@@ -1224,9 +1243,11 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
         for (int i2 = 0; i2 < nf; ++i2)
             for (int j2 = 0; j2 < nf; ++j2) Xm[i2][j2] = full[idx[i2]][idx[j2]];
         if (!invert_small(Xm, Xi, nf)) sing = 1;
+        // scattered to parameter positions (zeros for fixed parameters), so
+        // the per-channel loops below index it with compile-time constants
         for (int i2 = 0; i2 < 25; ++i2) sh_Xinv[i2] = 0.0;
         for (int i2 = 0; i2 < nf; ++i2)
-            for (int j2 = 0; j2 < nf; ++j2) sh_Xinv[i2 * 5 + j2] = Xi[i2][j2];
+            for (int j2 = 0; j2 < nf; ++j2) sh_Xinv[idx[i2] * 5 + idx[j2]] = Xi[i2][j2];
         sh_misc[8] = (double)sing;
     }
     __syncthreads();
@@ -1247,11 +1268,17 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
         double dC[5], dS[5], d2C[5][5], d2S[5][5];
         chan_derivs(st, fc, dC, dS, d2C, d2S);
         const double C = st[0], S = st[6], an = C / S;
+        // U X^-1 U over the fitted parameters in order (fixed ones add
+        // exact zeros)
         double U[5];
-        for (int i2 = 0; i2 < nf; ++i2) U[i2] = -2.0 * (dC[idx[i2]] - an * dS[idx[i2]]);
+#pragma unroll
+        for (int i2 = 0; i2 < 5; ++i2) U[i2] = (flagmask >> i2 & 1) ? -2.0 * (dC[i2] - an * dS[i2]) : 0.0;
         double quad = 0.0;
-        for (int i2 = 0; i2 < nf; ++i2)
-            for (int j2 = 0; j2 < nf; ++j2) quad += U[i2] * Xinv[i2][j2] * U[j2];
+#pragma unroll
+        for (int i2 = 0; i2 < 5; ++i2)
+#pragma unroll
+            for (int j2 = 0; j2 < 5; ++j2)
+                if ((flagmask >> i2 & 1) && (flagmask >> j2 & 1)) quad += U[i2] * Xinv[i2][j2] * U[j2];
         const double cinv = 1.0 / (2.0 * S);
         double var = 2.0 * (cinv + quad * cinv * cinv);
         double serr = (a.mode == PPF_MODE_LEGACY2) ? pow(S, -0.5) : sqrt(var);
@@ -1267,8 +1294,8 @@ __global__ __launch_bounds__(kBlock) void k_postfit(SolveArgs a) {
         double *cov = a.covariance + (int64_t)s * 25;
         for (int i2 = 0; i2 < 25; ++i2) cov[i2] = 0.0;
         for (int i2 = 0; i2 < nf; ++i2) {
-            for (int j2 = 0; j2 < nf; ++j2) cov[i2 * 5 + j2] = 2.0 * Xinv[i2][j2];
-            pe[idx[i2]] = sqrt(2.0 * Xinv[i2][i2]);
+            for (int j2 = 0; j2 < nf; ++j2) cov[i2 * 5 + j2] = 2.0 * sh_Xinv[idx[i2] * 5 + idx[j2]];
+            pe[idx[i2]] = sqrt(2.0 * sh_Xinv[idx[i2] * 5 + idx[i2]]);
         }
         double params[5] = {phi_out, x[1], x[2], tau_out, x[4]};
         for (int i2 = 0; i2 < 5; ++i2) { res->params[i2] = params[i2]; res->param_errs[i2] = pe[i2]; }

@@ -43,8 +43,10 @@ def parse():
                     help="sub-integrations per GPU")
     ap.add_argument("--nchan", type=int, default=512)
     ap.add_argument("--nbin", type=int, default=2048)
-    ap.add_argument("--chunk", type=int, default=2500,
-                    help="sub-integrations per ppf_fit_batch call")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="sub-integrations per ppf_fit_batch call (default: "
+                    "all of a GPU's sub-ints for phase+DM, 2500 for full, "
+                    "100 for scat)")
     ap.add_argument("--fit", default="phase+DM",
                     choices=["phase+DM", "full", "scat", "align"],
                     help="phase+DM: configs[1] (the metric); full: configs[2] "
@@ -214,6 +216,8 @@ def main():
     ctx = _lib.context(dev.index)
     lib.ppf_set_profiling(ctx, 1)
     ws = None
+    if args.chunk is None:
+        args.chunk = {"phase+DM": count, "full": 2500, "scat": 100}[args.fit]
     chunks = [(c0, min(count, c0 + args.chunk))
               for c0 in range(0, count, args.chunk)]
 

@@ -54,6 +54,9 @@ def parse():
                     "scattering; scat: configs[4] fit (phi, DM, tau, alpha), "
                     "CHIME-like band; align: configs[3] ppalign iteration "
                     "(--nsub archives, default shape 256 x 1024)")
+    ap.add_argument("--zap-frac", type=float, default=0.0,
+                    help="fraction of channels masked (zapped) in every "
+                    "sub-int, as GetTOAs passes its ok_ichans (default 0)")
     ap.add_argument("--cpu-sample", type=int, default=48,
                     help="sub-integrations for the CPU baseline (0: skip)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
@@ -212,6 +215,13 @@ def main():
     nu_outs_t = torch.full((count, 3), float("nan"), dtype=f64, device=dev)
     gw_t = torch.ones((count, nchan), dtype=f64, device=dev)
     gdm_t = torch.full((count,), synth.DM0, dtype=f64, device=dev)
+    mask_t = None
+    if args.zap_frac > 0.0:      # the same channels zapped in every sub-int
+        zrng = np.random.default_rng(20250217)
+        keep = np.ones(nchan, np.uint8)
+        keep[zrng.choice(nchan, int(round(args.zap_frac * nchan)),
+                         replace=False)] = 0
+        mask_t = torch.as_tensor(np.tile(keep, (count, 1)), device=dev)
     lib = _lib.load()
     ctx = _lib.context(dev.index)
     lib.ppf_set_profiling(ctx, 1)
@@ -231,7 +241,8 @@ def main():
                 flags_t[sl], nu_fits=nu_fits_t[sl], nu_outs=nu_outs_t[sl],
                 log10_tau=scat_fit,
                 guess=True, guess_weights=gw_t[sl], guess_DM=gdm_t[sl],
-                guess_Ns=100, dev=dev, workspace=ws)
+                guess_Ns=100, chan_mask=None if mask_t is None else mask_t[sl],
+                dev=dev, workspace=ws)
             ws = res["workspace"]
             outs.append(res["results"])
         results = torch.cat(outs, 0)
@@ -338,6 +349,7 @@ def main():
                             (FIT["tau"], FIT["nu_tau"])),
                            nsub_per_gpu=args.nsub,
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
+                           zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),
                roofline=roof, stage_ms=stages, kernels=kernels,

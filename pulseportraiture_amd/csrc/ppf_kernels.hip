@@ -496,15 +496,31 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double wsum = sh[0], cnt = sh[1];
     lds_fft(z, a.log2N, a.T, false);
     double pw[1] = {0.0};
-    for (int k = tid; k <= N; k += kBlock) {
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const int lane = tid & 63;
+    // uniform trip count: the mask ballots below need every lane active
+    for (int k0 = 0; k0 <= N; k0 += kBlock) {
+        const int k = k0 + tid;
+        const bool kv = k <= N;
+        // mean model profile of the usable channels: the batch sum minus the
+        // masked channels' rows in increasing channel order (the masked
+        // channels of each 64-channel group found with one ballot)
+        double2 M = kv ? a.Msum[(int64_t)mi * nharm + k] : cmk(0.0, 0.0);
+        if (mask) {
+            for (int n0 = 0; n0 < a.nchan; n0 += 64) {
+                const int nl = n0 + lane;
+                unsigned long long bits = __ballot(nl < a.nchan && !mask[nl]);
+                while (bits) {
+                    const int b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    if (kv) M = csub(M, Mm[(int64_t)(n0 + b) * nharm + k]);
+                }
+            }
+        }
+        if (!kv) continue;
         double2 R = cscale(rfft_bin(z, N, a.T2, k), 1.0 / wsum);
-        const int mi = a.model_index ? a.model_index[s] : 0;
-        const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
-        const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-        double2 M = a.Msum[(int64_t)mi * nharm + k];
-        if (mask)
-            for (int n = 0; n < a.nchan; ++n)
-                if (!mask[n]) M = csub(M, Mm[(int64_t)n * nharm + k]);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
             double u = kTwoPi * (double)k * a.guess_tau[s];

@@ -77,7 +77,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, MP,
+    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, MP, KC,
         needx, Bt, total;
     int nblk, cb, cbd, nblkd;
 };
@@ -106,6 +106,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.mres = o;  o += align256(sizeof(double) * nsub * 2 * nchan);
     L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.MP = o;    o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
+    L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.needx = o; o += align256(nsub);
     L.Bt = o;    o += align256(sizeof(double) * (nharm - 1) / 2 * 16);
     if (d->guess) {
@@ -272,6 +273,9 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     if ((e = ppf::launch_model_pow_t(Mft, d->nchan, nharm, d->nmodel, (double *)(ws + L.MP), st)) !=
         hipSuccess)
         return hip_fail(ctx, e, "k_model_pow_t");
+    if ((e = ppf::launch_model_cut((const double *)(ws + L.MP), d->nchan, nharm, d->nmodel,
+                                   (int32_t *)(ws + L.KC), st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_model_cut");
     if ((e = ppf::launch_model_pow(Mft, d->nchan, nharm, d->nmodel, Mpow, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_model_pow");
     // moment-mode sub-ints (no scattering) never need the cross spectrum in
@@ -336,6 +340,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.nsub = d->nsub; sa.nchan = d->nchan; sa.nbin = d->nbin;
     sa.X = xa.X; sa.Mft = Mft; sa.model_index = d->model_index; sa.chan = xa.chan;
     sa.MP = (const double *)(ws + L.MP);
+    sa.KC = (const int32_t *)(ws + L.KC);
     sa.freqs = d->freqs; sa.P = d->P; sa.mask = d->chan_mask; sa.init = d->init;
     sa.fit_flags = d->fit_flags; sa.nu_fits = d->nu_fits; sa.nu_outs = d->nu_outs;
     sa.log10_tau = d->log10_tau; sa.option = d->option; sa.is_toa = d->is_toa; sa.mode = d->mode;

@@ -81,6 +81,7 @@ struct SolveArgs {
     int nsub, nchan, nbin;
     const double2 *X, *Mft;
     const double *MP;            // [nmodel][N+1][nchan] |M_nk|^2 (k = 0: 0)
+    const int32_t *KC;           // [nmodel][nchan] harmonics that matter (k_model_cut)
     const int32_t *model_index;
     const double *chan;
     const double *freqs, *P;
@@ -215,6 +216,10 @@ hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
+// per (model, channel): 1 + the last harmonic with |M_k|^2 > kCutRel max_k |M_k|^2
+constexpr double kCutRel = 1e-28;   // |M_k| < 1e-14 max|M|: below the template's own FFT rounding floor
+hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, int32_t *KC,
+                            hipStream_t st);
 hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmodel, double *MP,
                               hipStream_t st);
 

@@ -298,7 +298,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 #pragma unroll
     for (int i = 0; i < 21; ++i) acc[i] = 0.0;
     const int n = blk * kPassChans + threadIdx.x;
-    if (n < a.nchan && (!mask || mask[n])) {
+    const bool use_n = n < a.nchan && (!mask || mask[n]);
+    // harmonics the wave sums: up to the largest cutoff of its channels
+    // (k_model_cut; wave-uniform so the loads stay coalesced)
+    const int kend = (int)wave_max(use_n ? (double)a.KC[(int64_t)mi * a.nchan + n] : 1.0);
+    if (use_n) {
         const double nu = fr[n];
         const double phin = th[0] + kDconst * th[1] * (pow(nu, -2.0) - nuDM2) / g.P +
                             kDconst * kDconst * th[2] * (pow(nu, -4.0) - nuGM4) / g.P;
@@ -335,9 +339,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
         auto ldg = [&](int kb, double2 (&xo)[KB], double (&po)[KB]) {
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
-                const int k = min(kb + u, nharm - 1);
+                const int k = min(kb + u, kend - 1);
                 // past the last harmonic: zero terms (no branch in the group)
-                const bool in = kb + u < nharm;
+                const bool in = kb + u < kend;
                 const double2 xl = Xc[k * xs];
                 xo[u] = in ? xl : cmk(0.0, 0.0);
                 if (SCAT) {
@@ -347,10 +351,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
             }
         };
         ldg(0, xv, pv);
-        if (KB < nharm) ldg(KB, xn, pn);
+        if (KB < kend) ldg(KB, xn, pn);
         double2 E = cmk(1.0, 0.0);
-        for (int kb = 0; kb < nharm; kb += KB) {
-            if (kb + 2 * KB < nharm) ldg(kb + 2 * KB, xn2, pn2);
+        for (int kb = 0; kb < kend; kb += KB) {
+            if (kb + 2 * KB < kend) ldg(kb + 2 * KB, xn2, pn2);
             if ((kb & 63) == 0) E = cexp2pi((double)kb * phin);   // exact seed every 64
 #pragma unroll
             for (int u = 0; u < KB; ++u) {

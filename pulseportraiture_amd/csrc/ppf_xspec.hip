@@ -836,6 +836,42 @@ hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmod
     return hipGetLastError();
 }
 
+// Harmonic cutoff per (model, channel): KC = 1 + the last k with
+// |M_k|^2 > rel * max_k |M_k|^2 (>= 1).  Every term of the pass sums beyond
+// it carries |M_k| < 1e-14 max |M| (rel = kCutRel = 1e-28) -- the level of
+// a float64 template's own FFT rounding floor; summed over the dropped
+// harmonics these terms change C, C', C'' and S by < 1e-12 relative -- so
+// k_pass stops there (the example template at 512 x 2048: median 226 of
+// 1025 harmonics; at 16384 x 1024 over 400-800 MHz the narrow component
+// reaches Nyquist and nothing is cut).
+// rel < 0 (PPF_NO_HCUT=1): KC = nharm.
+__global__ __launch_bounds__(256) void k_model_cut(const double *MP, int nchan, int nharm, int nmodel,
+                                                   double rel, int32_t *KC) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)nmodel * nchan) return;
+    const int m = (int)(i / nchan), n = (int)(i % nchan);
+    const double *p = MP + (int64_t)m * nharm * nchan + n;
+    int kc = nharm;
+    if (rel >= 0.0) {
+        double mx = 0.0;
+        for (int k = 0; k < nharm; ++k) mx = fmax(mx, p[(int64_t)k * nchan]);
+        const double thr = rel * mx;
+        kc = 1;
+        for (int k = nharm - 1; k >= 1; --k)
+            if (p[(int64_t)k * nchan] > thr) { kc = k + 1; break; }
+    }
+    KC[i] = kc;
+}
+
+hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, int32_t *KC,
+                            hipStream_t st) {
+    static const bool off = getenv("PPF_NO_HCUT") && atoi(getenv("PPF_NO_HCUT"));
+    const int64_t n = (int64_t)nmodel * nchan;
+    hipLaunchKernelGGL(k_model_cut, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, MP, nchan,
+                       nharm, nmodel, off ? -1.0 : kCutRel, KC);
+    return hipGetLastError();
+}
+
 hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out,
                             hipStream_t st) {
     dim3 g((unsigned)((nharm + 15) / 16), (unsigned)nmodel);

@@ -370,6 +370,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ma.mom = (double *)sa.mom;
     ma.Bt = (const double *)(ws + L.Bt);
     ma.kc = kc; ma.errs = d->errs; ma.Mpow = Mpow; ma.mres = sa.mres; ma.nmodel = d->nmodel;
+    ma.KC = (const int32_t *)(ws + L.KC);
     if (fused && (e = ppf::launch_btab(d->nbin / 2, (double *)(ws + L.Bt), st)) != hipSuccess)
         return hip_fail(ctx, e, "k_btab");
     // trust-region iterations.  Scattering fits: each iteration = one

@@ -59,6 +59,7 @@ struct XmomArgs {
     const double *errs;          // [nsub][nchan] or null
     const double *Mpow;          // [nmodel][nchan]
     double *mres;                // [nsub][2][nchan] centre residual phi_c,n - s_n/nbin
+    const int32_t *KC;           // [nchan] harmonic cutoff of the (single) model, or null
 };
 
 struct GuessArgs {

@@ -519,10 +519,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         mstore();                         // this round no longer reads mrow
 
         f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0;
+        // folded pairs (k, N - k) with k >= KC_n hold only harmonics whose
+        // model amplitude is below 1e-14 of its peak (k_model_cut): the
+        // needed range [0, KC_n) is spread over the eight waves instead
+        int kpw = KPW, kw0 = k0;
+        if constexpr (SH) {
+            const int kn = a.KC ? a.KC[n] : NH;
+            if (kn < N / 2) {
+                kpw = min(KPW, ((kn + 4 * XW - 1) / (4 * XW)) * 4);
+                kw0 = wave * kpw;
+            }
+        }
 #ifndef G_NOMFMA
 #pragma unroll 4
         for (int t = 0; t < KPW / 4; ++t) {
-            const int k = k0 + 4 * t + kk;
+            if (t >= (kpw >> 2)) break;                       // wave-uniform
+            const int k = kw0 + 4 * t + kk;
             const int se = wfft::pad<LOG2N>(k);
             const int so = k == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(N - k);
             // B[k][j] = v_k^j, v = u_k^2 (same arithmetic as k_btab)

@@ -289,7 +289,18 @@ def main():
     dsum_unit = nchan * nbin * 4 + nblkd * nbin * 8 + nblkd * 16
     #  k_xspec_w (scattering fits: the cross spectrum X streamed by every
     #   evaluation): read the rows, write X (complex128) and 4 scalars/channel
-    xspec_unit = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
+    #   X is written only below the harmonic cutoff of each aligned
+    #   64-channel group (k_model_cut, |M_k|^2 > 1e-28 max |M|^2; DESIGN.md
+    #   section 3), so the X bytes count those harmonics
+    mp = np.abs(np.fft.rfft(np.asarray(batch["model"], dtype=np.float64),
+                            axis=1)) ** 2
+    mp[:, 0] = 0.0
+    above = mp > 1e-28 * mp.max(axis=1, keepdims=True)
+    kc = np.where(above.any(axis=1),
+                  nharm - np.argmax(above[:, ::-1], axis=1), 1)
+    kw = np.array([kc[g:g + 64].max() for g in range(0, nchan, 64)])
+    xh = int(sum(kw[i] * min(64, nchan - 64 * i) for i in range(len(kw))))
+    xspec_unit = nchan * nbin * 4 + xh * 16 + 4 * nchan * 8
     L2N = (nbin // 4).bit_length()
     kern = {
         "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,

@@ -302,6 +302,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // moments are taken from X (k_moments)
     const bool fused = wave && use_moments;
     xa.needx = fused ? needx : nullptr;
+    // fused: only k_pass reads X, and only below its channels' cutoffs
+    xa.KC = fused ? (const int32_t *)(ws + L.KC) : nullptr;
     if (wave) {
         if ((e = ppf::launch_xspec_wave(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec_w");
     } else {

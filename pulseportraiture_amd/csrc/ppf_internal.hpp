@@ -30,6 +30,8 @@ struct XspecArgs {
     // fit runs on moments (k_xmom) are skipped.
     const double *Mpow;
     const uint8_t *needx;        // [nsub]
+    const int32_t *KC;           // [nmodel][nchan] harmonic cutoff (k_model_cut) or null: X is
+                                 // written only below the cutoff of each 64-channel group
 };
 
 // k_dsum: GetTOAs guess profile, time-domain dedispersion (pptoas.py:461-464)

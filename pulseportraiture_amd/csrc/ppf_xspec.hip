@@ -126,6 +126,13 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     // 8 rows' X are left in the wave buffers and written out together, 8
     // channels x 16 B = one 128-B line per harmonic.
     double2 *Xs = a.X + (int64_t)s * NH * a.nchan;
+    // harmonics k_pass reads for this block's channels: the largest cutoff
+    // of the aligned 64-channel group (a k_pass wave) containing them
+    int kw = NH;
+    if (a.KC) {
+        const int nn = (cbase & ~63) + lane;
+        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
+    }
 
     auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
     RowT zr[R];
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
             if (nc < cend) {
                 const bool ok = !mask || mask[nc];
                 const double2 *b = lds + c * SL;
-                for (int k = threadIdx.x >> 3; k < NH; k += 64 * kXW / 8) {
+                for (int k = threadIdx.x >> 3; k < kw; k += 64 * kXW / 8) {
                     const int slot = k == N ? wfft::pad<LOG2N>(N / 2)
                                             : (k == N / 2 ? XNYQ : wfft::pad<LOG2N>(k));
                     Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);

@@ -332,6 +332,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.kc = kc; ga.nblkd = L.nblkd; ga.Ns = d->guess_Ns; ga.mask = d->chan_mask;
         ga.freqs = d->freqs; ga.P = d->P; ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau;
         ga.nu_fits = d->nu_fits; ga.gP = da.gP; ga.gw = da.gw; ga.T = T; ga.T2 = T2;
+        ga.KC = (const int32_t *)(ws + L.KC);
         ga.x0 = (double *)(ws + L.x0); ga.Msum = msum; ga.Mft = Mft;
         ga.model_index = d->model_index;
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");

@@ -76,6 +76,7 @@ struct GuessArgs {
     const double2 *Msum;         // [nmodel][N+1]
     const double2 *Mft;
     const int32_t *model_index;
+    const int32_t *KC;           // [nmodel][nchan] harmonic cutoff (k_model_cut) or null
 };
 
 struct TRState;

@@ -534,7 +534,16 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     block_sum<1>(pw, red);
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
     const double err = sig * sqrt((double)a.nbin / 2.0);
-    const double phase = brute_fmin(xm, nharm, 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
+    // the mean model has no harmonic above the largest channel cutoff
+    // (k_model_cut): the FFTFIT sums stop there
+    double kmx[1] = {1.0};
+    if (a.KC)
+        for (int n = tid; n < a.nchan; n += kBlock)
+            kmx[0] = fmax(kmx[0], (double)a.KC[(int64_t)mi * a.nchan + n]);
+    else
+        kmx[0] = (double)nharm;
+    block_max<1>(kmx, red);
+    const double phase = brute_fmin(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
                                     nullptr);
     // nu_mean of the usable channels (block reduction: 16384-channel
     // portraits made a serial loop here cost ~0.2 ms per sub-int)

@@ -818,3 +818,69 @@ def test_gauss_portraits_match_reference(ppl, tmp_path):
     with pytest.raises(KeyError):     # evolve_parameter's unknown code
         ppl.gen_gaussian_portrait("020", c["params"], -4.0, np.zeros(nbin),
                                   c["freqs"], c["nu_ref"])
+
+
+# ------------------------------------------------------ harmonic cutoff ---
+def _cut_fraction(model):
+    """Fraction of harmonics k_model_cut keeps (numpy restatement of its
+    rule: last k with |M_k|^2 > 1e-28 max |M|^2, k = 0 excluded)."""
+    mp = np.abs(np.fft.rfft(model, axis=1)) ** 2
+    mp[:, 0] = 0.0
+    above = mp > 1e-28 * mp.max(axis=1, keepdims=True)
+    kc = mp.shape[1] - np.argmax(above[:, ::-1], axis=1)
+    return kc.mean() / mp.shape[1]
+
+
+@pytest.mark.parametrize("flags", [[1, 1, 0, 0, 0], [1, 1, 1, 1, 1]])
+def test_harmonic_cutoff_fits_match_oracle(flags):
+    """The example template at 1100-1900 MHz x 2048 bins has no model power
+    above ~1e-14 of its peak past harmonic ~430, so the device sums stop
+    there (k_model_cut; DESIGN.md section 4, deviation 7) while the oracle
+    sums all 1025 harmonics: the phase+DM moment path (with the device guess)
+    and the full scattering fit agree with the oracle to 0.01 sigma and
+    chi2_red to 1e-8."""
+    import oracle as O
+    from pulseportraiture_amd import engine, synth, _lib
+    from pulseportraiture_amd.pplib import guess_fit_freq, phase_transform
+    nsub, nchan, nbin = 2, 128, 2048
+    scat = flags[3] == 1
+    b = synth.make_batch(nsub, nchan, nbin, first=515,
+                         tau=2e-3 if scat else 0.0,
+                         nu_tau=1500.0 if scat else None)
+    assert _cut_fraction(b["model"]) < 0.5          # the cut is active
+    nu_fit = guess_fit_freq(b["freqs"])
+    init = np.zeros((nsub, 5))
+    init[:, 1] = synth.DM0
+    if scat:
+        for i in range(nsub):
+            init[i, 0] = phase_transform(b["phi_true"][i], b["DM_true"][i],
+                                         b["nu_ref"], nu_fit, b["P"][i],
+                                         mod=True)
+        init[:, 3] = np.log10(1.0 / nbin)
+        init[:, 4] = synth.GMODEL_ALPHA
+    res = engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags,
+        nu_fits=np.full((nsub, 3), nu_fit), log10_tau=scat,
+        guess=not scat, guess_weights=np.ones((nsub, nchan)),
+        guess_DM=np.full(nsub, synth.DM0))
+    r = engine.results_numpy(res)
+    I = _lib.RESULT_INDEX
+    for i in range(nsub):
+        R = r["results"][i]
+        x0 = list(init[i])
+        if not scat:
+            x0[0] = R[I["x_fit_phi"]]      # start the oracle at the device's
+        data = b["data"][i].double().cpu().numpy()   # converged phase
+        ref = O.fit_portrait_full(data, b["model"], x0, b["P"][i], b["freqs"],
+                                  nu_fits=(nu_fit,) * 3, fit_flags=flags,
+                                  log10_tau=scat)
+        got = dict(params=R[I["params"]], nu_DM=R[I["nu_out"]][0],
+                   nu_GM=R[I["nu_out"]][1], nu_tau=R[I["nu_out"]][2])
+        refd = dict(params=ref["params"], param_errs=ref["param_errs"],
+                    nu_DM=ref["nu_DM"], nu_GM=ref["nu_GM"],
+                    nu_tau=ref["nu_tau"])
+        dev = G.param_deviation_sigma(got, refd, b["P"][i], scat)
+        assert dev.max() < SIG, (i, dev)
+        assert abs(R[I["red_chi2"]] / ref["red_chi2"] - 1) < RCHI2
+        np.testing.assert_allclose(R[I["param_errs"]], ref["param_errs"],
+                                   rtol=1e-4)

@@ -282,10 +282,10 @@ def gauss_portraits(model_code, params, scattering_index, freqs, nu_ref, nbin,
     [bin], per component loc, m_loc, wid, m_wid, amp, m_amp),
     scattering_index [nport], freqs [nport, nchan], nu_ref [nport] ->
     float64 [nport, nchan, nbin]."""
-    dev = device(dev)
     code = str(model_code)
     if len(code) != 3 or any(c not in "01" for c in code):
         raise KeyError(code)     # evolve_parameter's dictionary lookup
+    dev = device(dev)
     prm = to_dev(params, dev, torch.float64)
     if prm.dim() == 1:
         prm = prm.unsqueeze(0)

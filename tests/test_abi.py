@@ -63,3 +63,19 @@ def test_poly_real_roots_matches_np_roots(seed):
     got = np.sort(_lib.poly_real_roots(c))
     assert len(got) == len(ref)
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
+
+
+def test_gauss_portrait_entry_validates_without_gpu():
+    """ppf_gauss_portrait_batch rejects a NULL context, and the Python
+    wrapper raises evolve_parameter's KeyError for an unknown evolution
+    code before touching any device (pplib.py:1082-1084)."""
+    import ctypes
+    import pytest
+    from pulseportraiture_amd import _lib, engine
+    lib = _lib.load()
+    rc = lib.ppf_gauss_portrait_batch(None, 1, 1, 64, 1, b"000", None, None,
+                                      None, None, None, None)
+    assert rc != 0
+    with pytest.raises(KeyError):
+        engine.gauss_portraits("0x0", np.zeros((1, 8)), [0.0], [[1.0]],
+                               [1.0], 64)

@@ -11,6 +11,11 @@ running the reference itself in the build container
 (``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``,
 ``tests/test_oracle_golden.py``).
 
+The Gaussian-template generator (gen_gaussian_portrait / gaussian_profile,
+pplib.py:801-963) is restated here too, as the checker of the device
+template kernel; it reproduces the reference's outputs bit for bit
+(tests/golden/make_golden_gauss.py -> gauss.npz).
+
 Third-party arithmetic restated / reused (as the reference uses it):
 NumPy 2.2.6 ``numpy.fft`` (pocketfft), SciPy 1.15.3 ``optimize.minimize``
 (trust-ncg, TNC) and ``optimize.brute`` + ``fmin``.

@@ -45,8 +45,8 @@ def parse():
     ap.add_argument("--nbin", type=int, default=2048)
     ap.add_argument("--chunk", type=int, default=None,
                     help="sub-integrations per ppf_fit_batch call (default: "
-                    "all of a GPU's sub-ints for phase+DM, 2500 for full, "
-                    "100 for scat)")
+                    "all of a GPU's sub-ints; scattering fits: at most ~150 "
+                    "GB of cross spectrum per call)")
     ap.add_argument("--fit", default="phase+DM",
                     choices=["phase+DM", "full", "scat", "align"],
                     help="phase+DM: configs[1] (the metric); full: configs[2] "
@@ -227,7 +227,11 @@ def main():
     lib.ppf_set_profiling(ctx, 1)
     ws = None
     if args.chunk is None:
-        args.chunk = {"phase+DM": count, "full": 2500, "scat": 100}[args.fit]
+        # one ppf_fit_batch call per GPU per step, unless the cross spectrum
+        # of the scattering fits (nchan nharm 16 B per sub-int) would pass
+        # ~150 GB of the 288 GB HBM
+        args.chunk = count if not scat_fit else max(1, min(
+            count, int(150e9 // (nchan * nharm * 16))))
     chunks = [(c0, min(count, c0 + args.chunk))
               for c0 in range(0, count, args.chunk)]
 

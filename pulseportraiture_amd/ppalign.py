@@ -237,7 +237,10 @@ def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
     for s in np.where(R.nchanx == 1)[0]:      # 1-channel hack (ppalign.py:231-236)
         m = int(np.where(R.mask[s])[0][0])
         x = R.data[s, 0, m].double().cpu().numpy()
-        fr = fit_phase_shift(x, model_port[m], R.errs[s, m], Ns=nbin)
+        mrow = model_port[m]
+        if isinstance(mrow, torch.Tensor):
+            mrow = mrow.cpu().numpy()
+        fr = fit_phase_shift(x, mrow, R.errs[s, m], Ns=nbin)
         phases[s, m] = fr.phase          # DM = data.DM at nu_ref = freqs[0]: 0
         weights[s, m] = fr.scale / R.errs[s, m] ** 2
     return phases, weights
@@ -305,11 +308,11 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
             _dist.allreduce_sum_(out, wsum)
         good = wsum > 0
         out[:, good] /= wsum[good][None, :, None]
-        aligned_port = out.cpu().numpy()
-        total_weights = np.outer(wsum.cpu().numpy(), np.ones(nbin))
-        model_port = aligned_port[0]
+        model_port = out[0]             # the next template stays in HBM
         niter -= 1
         count += 1
+    aligned_port = out.cpu().numpy()
+    total_weights = np.outer(wsum.cpu().numpy(), np.ones(nbin))
     if norm in ("mean", "max", "prof", "rms", "abs"):
         for ipol in range(npol):
             aligned_port[ipol] = normalize_portrait(aligned_port[ipol], norm,

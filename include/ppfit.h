@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PPF_ABI_VERSION 1
+#define PPF_ABI_VERSION 2
 
 enum ppf_error {
     PPF_OK = 0,
@@ -52,7 +52,16 @@ enum ppf_status {
                                 the reference raises ValueError here         */
     PPF_ST_SINGULAR = 0x200, /* singular covariance (LinAlgError)            */
     PPF_ST_NONFINITE = 0x400,/* non-finite objective encountered             */
-    PPF_ST_NOFIT = 0x800     /* no parameter to fit / no usable channel      */
+    PPF_ST_NOFIT = 0x800,    /* no parameter to fit / no usable channel      */
+    PPF_ST_NOSPACE = 0x1000  /* the fit streams the cross spectrum but the
+                                workspace holds fewer X slots (x_subints)    */
+};
+
+/* ppf_fit_desc.options bits */
+enum ppf_option {
+    PPF_OPT_NO_HCUT = 1      /* sum every harmonic: no per-channel cutoff of
+                                the harmonics whose template power is below
+                                1e-28 of the channel's peak */
 };
 
 enum ppf_mode {
@@ -123,6 +132,17 @@ typedef struct ppf_fit_desc {
     double *covariance;           /* [nsub][5][5], fit block in leading corner */
     void *workspace;
     size_t workspace_bytes;
+    /* ABI 2 */
+    int32_t x_subints;            /* cross-spectrum (X) slots the workspace
+                                     holds: the number of sub-ints whose fit
+                                     streams X (scattering fits: fit_flags[3]
+                                     or [4] set, or a nonzero initial tau).
+                                     <= 0: nsub.  Sub-ints past it end with
+                                     PPF_ST_NOSPACE.  Off the fused phase+DM
+                                     path (nbin outside 256..2048) every
+                                     sub-int streams X and nsub slots are
+                                     always reserved. */
+    int32_t options;              /* ppf_option bits                           */
 } ppf_fit_desc;
 
 int ppf_abi_version(void);

@@ -624,14 +624,20 @@ def fit_phase_shift(data, model, noise=None, bounds=(-0.5, 0.5), Ns=100):
 # ---------------------------------------------------------------------------
 def get_toas_archive(subints, models, freqs, weights, SNRs, Ps, DM_stored,
                      doppler_factors, ok_isubs=None, noise_stds=None,
-                     fit_flags=(1, 1, 0, 0, 0), bary=True, DM0=None):
+                     fit_flags=(1, 1, 0, 0, 0), bary=True, DM0=None,
+                     tau_guess=0.0, alpha_guess=-4.0, log10_tau=True):
     """subints [nsub, nchan, nbin]; models [nsub, nchan, nbin] (or one
-    [nchan, nbin] shared); weights / SNRs [nsub, nchan]."""
+    [nchan, nbin] shared); weights / SNRs [nsub, nchan].  With a scattering
+    fit (fit_flags[3] or [4]) the guesses follow pptoas.py:467-492: tau_guess
+    [rot] at nu_fit scatters the mean model profile of the phase guess, and
+    with log10_tau a zero tau_guess becomes log10(1 / nbin)."""
     nsub, nchan, nbin = subints.shape
     if ok_isubs is None:
         ok_isubs = np.arange(nsub)
     out = {k: np.zeros(nsub) for k in ("phis", "phi_errs", "DMs", "DM_errs",
-                                       "red_chi2s", "snrs", "GMs")}
+                                       "red_chi2s", "snrs", "GMs", "taus",
+                                       "alphas")}
+    out["param_errs"] = np.zeros((nsub, 5))
     out["nu_refs"] = np.zeros((nsub, 3))
     out["nu_fits"] = np.zeros((nsub, 3))
     out["scales"] = np.zeros((nsub, nchan))
@@ -649,24 +655,36 @@ def get_toas_archive(subints, models, freqs, weights, SNRs, Ps, DM_stored,
         nu_fit = guess_fit_freq(freqsx, SNRs[isub, ok])
         rot = rotate_data(portx, 0.0, DM_stored, P, freqsx, nu_mean)
         rot_prof = np.average(rot, axis=0, weights=weights[isub, ok])
-        phi_guess = fit_phase_shift(rot_prof, modelx.mean(axis=0),
-                                    Ns=100)["phase"]
+        scat = bool(fit_flags[3] or fit_flags[4])
+        mprof = modelx.mean(axis=0)
+        tg, ag = 0.0, 0.0
+        if scat:
+            tg, ag = float(tau_guess), float(alpha_guess)
+            B = _scat_B(np.array([tg]), nbin // 2 + 1)[0]
+            mprof = np.fft.irfft(B * np.fft.rfft(mprof), n=nbin)
+        phi_guess = fit_phase_shift(rot_prof, mprof, Ns=100)["phase"]
         phi_guess = phase_transform(phi_guess, DM_stored, nu_mean, nu_fit, P,
                                     mod=True)
+        lt = bool(log10_tau) and scat
+        if lt:
+            tg = np.log10(tg if tg != 0.0 else 1.0 / nbin)
         flags = list(fit_flags)
         if len(freqsx) == 1:
             flags = [1, 0, 0, 0, 0]
-        r = fit_portrait_full(portx, modelx, [phi_guess, DM_stored, 0.0, 0.0,
-                                              0.0], P, freqsx,
+        r = fit_portrait_full(portx, modelx, [phi_guess, DM_stored, 0.0, tg,
+                                              ag], P, freqsx,
                               [nu_fit] * 3, [None] * 3, errs, flags,
-                              log10_tau=False)
+                              log10_tau=lt)
         df = doppler_factors[isub] if bary else 1.0
         DM = r["DM"] * df if flags[1] else r["DM"]
         out["phis"][isub] = r["phi"]
         out["phi_errs"][isub] = r["phi_err"]
         out["DMs"][isub] = DM
         out["DM_errs"][isub] = r["DM_err"]
-        out["GMs"][isub] = r["GM"]
+        out["GMs"][isub] = r["GM"] * df ** 3 if flags[2] else r["GM"]
+        out["taus"][isub] = r["tau"]
+        out["alphas"][isub] = r["alpha"]
+        out["param_errs"][isub] = r["param_errs"]
         out["red_chi2s"][isub] = r["red_chi2"]
         out["snrs"][isub] = r["snr"]
         out["nu_refs"][isub] = [r["nu_DM"], r["nu_GM"], r["nu_tau"]]

@@ -19,6 +19,9 @@ PPF_F32, PPF_F64 = 0, 1
 PPF_MODE_FULL, PPF_MODE_LEGACY2 = 0, 1
 ST_SUCCESS, ST_MAXITER, ST_CONVERGED, ST_LINALG = 0, 1, 2, 3
 ST_NO_ROOT, ST_SINGULAR, ST_NONFINITE, ST_NOFIT = 0x100, 0x200, 0x400, 0x800
+ST_NOSPACE = 0x1000
+OPT_NO_HCUT = 1           # ppf_fit_desc.options
+ABI_VERSION = 2
 
 # ppf_result: 32 doubles (include/ppfit.h)
 RESULT_FIELDS = (
@@ -59,6 +62,7 @@ class FitDesc(ctypes.Structure):
         ("results", _vp), ("scales", _vp), ("scale_errs", _vp),
         ("channel_snrs", _vp), ("covariance", _vp), ("workspace", _vp),
         ("workspace_bytes", ctypes.c_size_t),
+        ("x_subints", _i32), ("options", _i32),       # ABI 2
     ]
 
 
@@ -121,7 +125,7 @@ def load():
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
-            if lib.ppf_abi_version() != 1 or \
+            if lib.ppf_abi_version() != ABI_VERSION or \
                     lib.ppf_sizeof_fit_desc() != ctypes.sizeof(FitDesc) or \
                     lib.ppf_sizeof_result() != 8 * RESULT_DOUBLES:
                 raise RuntimeError("libppfit ABI mismatch (rebuild with make)")

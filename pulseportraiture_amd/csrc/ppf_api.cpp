@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 
 #include "../../include/ppfit.h"
@@ -18,6 +19,7 @@ struct ppf_ctx {
     int device;
     std::string err;
     std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
+    std::mutex tw_mu;              // guards tw (calls from several host threads)
     bool prof = false;
     static constexpr int kRing = 256;
     // [0..4]: stage boundaries; [5, 6]: the first moment pass (k_xmom_g,
@@ -61,6 +63,7 @@ int noise_kc(int nharm, int frac) {
 }
 
 int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const double2 **T2) {
+    std::lock_guard<std::mutex> lock(ctx->tw_mu);
     auto it = ctx->tw.find(nbin);
     if (it == ctx->tw.end()) {
         const int N = nbin / 2;
@@ -69,6 +72,10 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
         if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(twiddles)");
         e = ppf::launch_twiddles(N, p, p + N, st);
         if (e != hipSuccess) return hip_fail(ctx, e, "k_twiddles");
+        // the table is cached for calls on ANY stream: finish it before it
+        // is published (one-time cost per nbin)
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize(twiddles)");
         it = ctx->tw.emplace(nbin, p).first;
     }
     *T = it->second;
@@ -78,8 +85,10 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 
 struct FitLayout {
     size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, MP, KC,
-        needx, Bt, total;
+        needx, xslot, Bt, total;
     int nblk, cb, cbd, nblkd;
+    int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
+    int xcap;     // X slots
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -90,11 +99,13 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
+    L.fused = ppf::xspec_wave_supported(ilog2(d->nbin / 2), L.cb) ? 1 : 0;
+    L.xcap = (L.fused && d->x_subints > 0 && d->x_subints < d->nsub) ? d->x_subints : d->nsub;
     L.cbd = d->nchan < 128 ? d->nchan : 128;          // k_dsum channel block
     L.nblkd = (d->nchan + L.cbd - 1) / L.cbd;
     size_t o = 0;
     L.M = o;     o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
-    L.X = o;     o += align256(sizeof(double2) * nsub * nchan * nharm);
+    L.X = o;     o += align256(sizeof(double2) * (size_t)L.xcap * nchan * nharm);
     L.chan = o;  o += align256(sizeof(double) * nsub * nchan * 4);
     L.stats = o; o += align256(sizeof(double) * nsub * 2 * nchan * 10);
     L.x0 = o;    o += align256(sizeof(double) * nsub * 8);
@@ -108,6 +119,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.MP = o;    o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
     L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.needx = o; o += align256(nsub);
+    L.xslot = o; o += align256(sizeof(int32_t) * nsub);
     L.Bt = o;    o += align256(sizeof(double) * (nharm - 1) / 2 * 16);
     if (d->guess) {
         L.gP = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * (size_t)d->nbin);
@@ -274,17 +286,19 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         hipSuccess)
         return hip_fail(ctx, e, "k_model_pow_t");
     if ((e = ppf::launch_model_cut((const double *)(ws + L.MP), d->nchan, nharm, d->nmodel,
-                                   (int32_t *)(ws + L.KC), st)) != hipSuccess)
+                                   (d->options & PPF_OPT_NO_HCUT) != 0, (int32_t *)(ws + L.KC),
+                                   st)) != hipSuccess)
         return hip_fail(ctx, e, "k_model_cut");
     if ((e = ppf::launch_model_pow(Mft, d->nchan, nharm, d->nmodel, Mpow, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_model_pow");
-    // moment-mode sub-ints (no scattering) never need the cross spectrum in
-    // HBM: k_xmom re-FFTs their rows; k_classify marks the others
-    const char *senv = getenv("PPF_SOLVER");
-    const int use_moments = (senv && !strcmp(senv, "pass")) ? 0 : 1;
+    // moment-mode sub-ints (no scattering) on the fused path never need the
+    // cross spectrum in HBM: k_xmom_g re-FFTs their rows; k_classify marks
+    // the others and gives each an X slot
+    const int use_moments = 1;
     uint8_t *needx = (uint8_t *)(ws + L.needx);
-    if ((e = ppf::launch_classify(d->nsub, d->fit_flags, d->init, d->log10_tau, use_moments, needx,
-                                  st)) != hipSuccess)
+    int32_t *xslot = (int32_t *)(ws + L.xslot);
+    if ((e = ppf::launch_classify(d->nsub, d->fit_flags, d->init, d->log10_tau, L.fused, L.xcap,
+                                  needx, xslot, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_classify");
     mark(1);
 
@@ -296,8 +310,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.errs = d->errs; xa.freqs = d->freqs; xa.P = d->P; xa.T = T; xa.T2 = T2;
     xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);
     xa.Mpow = Mpow;
-    const char *xenv = getenv("PPF_XSPEC");
-    const bool wave = ppf::xspec_wave_supported(xa.log2N, xa.cb) && !(xenv && !strcmp(xenv, "block"));
+    xa.xslot = xslot;
+    const bool wave = L.fused != 0;
     // fused moment pass (k_xmom) only on the wave-FFT shapes; elsewhere the
     // moments are taken from X (k_moments)
     const bool fused = wave && use_moments;
@@ -363,6 +377,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
     sa.mres = (double *)(ws + L.mres);
+    sa.xslot = xslot;
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
     ppf::XmomArgs ma{};

@@ -32,6 +32,7 @@ struct XspecArgs {
     const uint8_t *needx;        // [nsub]
     const int32_t *KC;           // [nmodel][nchan] harmonic cutoff (k_model_cut) or null: X is
                                  // written only below the cutoff of each 64-channel group
+    const int32_t *xslot;        // [nsub] X slot of each sub-int (k_classify), or null: slot = s
 };
 
 // k_dsum: GetTOAs guess profile, time-domain dedispersion (pptoas.py:461-464)
@@ -107,6 +108,7 @@ struct SolveArgs {
     double2 *mom;                // [nsub][2][nchan][kMoments]
     double *dphi;                // [nsub][nchan][2]: d phi_n / d(DM, GM)
     double *mres;                // [nsub][2][nchan]: moment-centre residual per channel
+    const int32_t *xslot;        // [nsub] X slot (k_classify; -1 none, -2 no room) or null
 };
 
 struct RotateArgs {
@@ -202,7 +204,7 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);
 hipError_t launch_xmom(const XmomArgs &a, bool full, hipStream_t st);
 hipError_t launch_btab(int N, double *Bt, hipStream_t st);
 hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
-                           int moments, uint8_t *needx, hipStream_t st);
+                           int fused, int xcap, uint8_t *needx, int32_t *xslot, hipStream_t st);
 hipError_t launch_model_pow(const double2 *Mft, int nchan, int nharm, int nmodel, double *out,
                             hipStream_t st);
 hipError_t launch_model_sum(const double2 *Mft, int nchan, int nharm, int nmodel, double2 *out,
@@ -222,8 +224,8 @@ hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 // per (model, channel): 1 + the last harmonic with |M_k|^2 > kCutRel max_k |M_k|^2
 constexpr double kCutRel = 1e-28;   // |M_k| < 1e-14 max|M|: below the template's own FFT rounding floor
-hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, int32_t *KC,
-                            hipStream_t st);
+hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, bool off,
+                            int32_t *KC, hipStream_t st);
 hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmodel, double *MP,
                               hipStream_t st);
 

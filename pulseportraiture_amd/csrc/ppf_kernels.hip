@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
         if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
         else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)(2 * N)) * sqrt_half_nbin;
         const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-        double2 *Xrow = a.X + (int64_t)s * NH * a.nchan + n;   // X[s][k][n]
+        double2 *Xrow = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan + n;   // X[slot][k][n]
         const int64_t xs = a.nchan;
         double mpow[1] = {0.0};
         // pass 2: cross spectrum (D recomputed from the LDS spectrum)
@@ -1097,9 +1097,8 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
     const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 gp((unsigned)((int64_t)a.ngroup * a.nchan)), gf((unsigned)a.nchan), b(kBlock);
     // wave-per-row partials where the register FFT covers nbin; the
-    // block-FFT k_align_part otherwise (PPF_ALIGN_BLOCK=1 forces it)
-    static const bool force_block = getenv("PPF_ALIGN_BLOCK") && atoi(getenv("PPF_ALIGN_BLOCK"));
-    const bool wave = !force_block && align_wave_supported(a.log2N);
+    // block-FFT k_align_part otherwise
+    const bool wave = align_wave_supported(a.log2N);
     if (wave) {
         hipError_t e = launch_align_part_w(a, st);
         if (e != hipSuccess) return e;

@@ -140,16 +140,46 @@ __device__ void wave_gates(const double *lnr, const uint8_t *mask, int nchan, do
 }
 
 // k_classify: which sub-ints need the cross spectrum X in HBM (scattering
-// fits, which k_pass streams; or every fit when the moment solver is off).
-// Same test as k_tr_init's `scat`.
-__global__ void k_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
-                           int moments, uint8_t *needx) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsub) return;
-    const double x3 = init[(int64_t)s * 5 + 3];
-    const double tau0 = log10_tau ? pow(10.0, x3) : x3;
-    const bool scat = fit_flags[(int64_t)s * 5 + 3] || fit_flags[(int64_t)s * 5 + 4] || tau0 != 0.0;
-    needx[s] = (!moments || scat) ? 1 : 0;
+// fits, which k_pass streams; every fit when the moments are taken from X,
+// i.e. off the fused k_xmom_g path), and X's slot for each of them: the
+// slots are the order of those sub-ints (one workgroup, a running
+// exclusive scan), so the workspace holds X only for the sub-ints that use
+// it.  Past the caller's xcap: slot -2, and k_tr_init fails the fit with
+// PPF_ST_NOSPACE.  Same scattering test as k_tr_init's `scat`.
+constexpr int kClassifyBlock = 1024;
+__global__ __launch_bounds__(kClassifyBlock) void k_classify(int nsub, const int32_t *fit_flags,
+                                                             const double *init, int log10_tau,
+                                                             int fused, int xcap, uint8_t *needx,
+                                                             int32_t *xslot) {
+    __shared__ int wtot[kClassifyBlock / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int base_slot = 0;
+    for (int s0 = 0; s0 < nsub; s0 += kClassifyBlock) {
+        const int s = s0 + tid;
+        int need = 0;
+        if (s < nsub) {
+            const double x3 = init[(int64_t)s * 5 + 3];
+            const double tau0 = log10_tau ? pow(10.0, x3) : x3;
+            const bool scat =
+                fit_flags[(int64_t)s * 5 + 3] || fit_flags[(int64_t)s * 5 + 4] || tau0 != 0.0;
+            need = (!fused || scat) ? 1 : 0;
+        }
+        const unsigned long long bal = __ballot(need);
+        const int below = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wtot[wave] = __popcll(bal);
+        __syncthreads();
+        int off = base_slot;
+        for (int w = 0; w < wave; ++w) off += wtot[w];
+        int chunk = 0;
+        for (int w = 0; w < kClassifyBlock / 64; ++w) chunk += wtot[w];
+        if (s < nsub) {
+            const int slot = off + below;
+            needx[s] = (need && slot < xcap) ? 1 : 0;
+            xslot[s] = need ? (slot < xcap ? slot : -2) : -1;
+        }
+        base_slot += chunk;
+        __syncthreads();
+    }
 }
 
 // ===========================================================================
@@ -215,6 +245,9 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         if (nf == 0 || cnt == 0.0) {
             S.phase = PH_DONE;
             S.status = PPF_ST_NOFIT;
+        } else if (a.xslot && a.xslot[s] == -2) {
+            S.phase = PH_DONE;               // needs X, but the workspace has no slot
+            S.status = PPF_ST_NOSPACE;
         } else {
             S.phase = PH_INIT;
         }
@@ -307,7 +340,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
         const double phin = th[0] + kDconst * th[1] * (pow(nu, -2.0) - nuDM2) / g.P +
                             kDconst * kDconst * th[2] * (pow(nu, -4.0) - nuGM4) / g.P;
         const double2 W = cexp2pi(phin);
-        const double2 *Xc = a.X + (int64_t)s * nharm * a.nchan + n;
+        const double2 *Xc = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * nharm * a.nchan + n;
         const double *Pc = a.MP + (int64_t)mi * nharm * a.nchan + n;
         const int64_t xs = a.nchan;
         double aa = 0.0, inv_e2 = 0.0;
@@ -639,7 +672,8 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
         phin = c0 + c1 * dp[0] + c2 * dp[1];
         if (kk == 0) a.mres[((int64_t)s * 2 + q) * a.nchan + n] = 0.0;   // exact centre
     }
-    const double2 *Xr = a.X + (int64_t)s * nharm * a.nchan + (valid ? n : 0);   // X[s][k][n]
+    const double2 *Xr = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * nharm * a.nchan +
+                         (valid ? n : 0);   // X[slot][k][n]
     const double2 W4 = cexp2pi(4.0 * phin);
     f64x4 dre0 = {0.0, 0.0, 0.0, 0.0}, dre1 = dre0, dim0 = dre0, dim1 = dre0;
     double2 E = cmk(1.0, 0.0);
@@ -1015,10 +1049,10 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
     const int s = blockIdx.x, tid = threadIdx.x;
     const TRState &S = a.state[s];
     ppf_result *res = a.results + s;
-    if (S.status == PPF_ST_NOFIT) {
+    if (S.status == PPF_ST_NOFIT || S.status == PPF_ST_NOSPACE) {
         if (tid == 0) {
             for (int i = 0; i < 32; ++i) reinterpret_cast<double *>(res)[i] = 0.0;
-            res->status = PPF_ST_NOFIT;
+            res->status = S.status;
             res->phi_guess = S.phi_guess;
         }
         for (int n = tid; n < a.nchan; n += kBlock) {
@@ -1333,9 +1367,9 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
 // launchers
 // ===========================================================================
 hipError_t launch_classify(int nsub, const int32_t *fit_flags, const double *init, int log10_tau,
-                           int moments, uint8_t *needx, hipStream_t st) {
-    hipLaunchKernelGGL(k_classify, dim3((unsigned)((nsub + 255) / 256)), dim3(256), 0, st, nsub,
-                       fit_flags, init, log10_tau, moments, needx);
+                           int fused, int xcap, uint8_t *needx, int32_t *xslot, hipStream_t st) {
+    hipLaunchKernelGGL(k_classify, dim3(1), dim3(kClassifyBlock), 0, st, nsub, fit_flags, init,
+                       log10_tau, fused, xcap, needx, xslot);
     return hipGetLastError();
 }
 

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
 
     int s, cb;
     block_map(a.xcd_swizzle, a.nblk, s, cb);
-    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int
+    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
     // rounds: in round r wave w takes channel cb*CB + r*kXW + w
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
     const int nround = (a.cb + kXW - 1) / kXW;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     // X[s][k][n] (harmonic-major: k_pass lanes are channels).  Each round the
     // 8 rows' X are left in the wave buffers and written out together, 8
     // channels x 16 B = one 128-B line per harmonic.
-    double2 *Xs = a.X + (int64_t)s * NH * a.nchan;
+    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
     // harmonics k_pass reads for this block's channels: the largest cutoff
     // of the aligned 64-channel group (a k_pass wave) containing them
     int kw = NH;
@@ -863,7 +863,7 @@ hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmod
 // k_pass stops there (the example template at 512 x 2048: median 226 of
 // 1025 harmonics; at 16384 x 1024 over 400-800 MHz the narrow component
 // reaches Nyquist and nothing is cut).
-// rel < 0 (PPF_NO_HCUT=1): KC = nharm.
+// rel < 0 (ppf_fit_desc.options PPF_OPT_NO_HCUT): KC = nharm.
 __global__ __launch_bounds__(256) void k_model_cut(const double *MP, int nchan, int nharm, int nmodel,
                                                    double rel, int32_t *KC) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -882,9 +882,8 @@ __global__ __launch_bounds__(256) void k_model_cut(const double *MP, int nchan, 
     KC[i] = kc;
 }
 
-hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, int32_t *KC,
-                            hipStream_t st) {
-    static const bool off = getenv("PPF_NO_HCUT") && atoi(getenv("PPF_NO_HCUT"));
+hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, bool off,
+                            int32_t *KC, hipStream_t st) {
     const int64_t n = (int64_t)nmodel * nchan;
     hipLaunchKernelGGL(k_model_cut, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, MP, nchan,
                        nharm, nmodel, off ? -1.0 : kCutRel, KC);

@@ -91,3 +91,21 @@ def allreduce_sum_(*tensors):
     for t in tensors:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return tensors
+
+
+def raise_if_any_failed(err, device=None):
+    """Collective error check: every rank calls this with its own exception
+    (or None) BEFORE the next collective, so a failure on one rank raises on
+    every rank instead of leaving the others blocked in that collective."""
+    if not is_dist():
+        if err is not None:
+            raise err
+        return
+    t = torch.tensor([1.0 if err is not None else 0.0], dtype=torch.float64,
+                     device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if err is not None:
+        raise err
+    if t.item() > 0.0:
+        raise RuntimeError("another rank failed (its exception is raised "
+                           "there)")

@@ -54,14 +54,42 @@ def _data_dtype(x):
         torch.float64
 
 
+def _host(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def x_subints(fit_flags, init, log10_tau, nsub):
+    """Sub-ints whose fit streams the cross spectrum X (k_classify's test,
+    restated on the host): scattering flags set, or a nonzero initial tau
+    (10**tau with log10_tau, pptoaslib.py:271-276)."""
+    fl = _host(fit_flags).reshape(-1, 5)
+    if fl.shape[0] == 1:
+        fl = np.repeat(fl, nsub, axis=0)
+    x3 = _host(init).reshape(nsub, 5)[:, 3]
+    with np.errstate(over="ignore"):
+        tau0 = 10.0 ** x3 if log10_tau else x3
+    return int(np.count_nonzero((fl[:, 3] != 0) | (fl[:, 4] != 0) |
+                                (tau0 != 0.0)))
+
+
 def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               nu_outs=None, errs=None, chan_mask=None, model_index=None,
               log10_tau=False, option=0, is_toa=True, mode=_lib.PPF_MODE_FULL,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
-              guess_Ns=100, guess_tau=None, dev=None, workspace=None):
+              guess_Ns=100, guess_tau=None, dev=None, workspace=None,
+              n_x=None, no_hcut=False, max_workspace=None):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
+
+    n_x: cross-spectrum slots (sub-ints whose fit streams X); None computes
+    it from fit_flags / init (x_subints).  no_hcut: sum every harmonic
+    (PPF_OPT_NO_HCUT).  max_workspace: workspace budget in bytes (default
+    half the free device memory); a batch needing more is fitted in
+    consecutive chunks of sub-ints (a sub-int's result does not depend on
+    the batch it is in).
 
     Returns a dict of device tensors: results [nsub, 32] (see
     _lib.RESULT_INDEX), scales/scale_errs/channel_snrs [nsub, nchan],
@@ -78,7 +106,6 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     if model_t.shape[1:] != (nchan, nbin):
         raise ValueError("model shape %s != [*, %d, %d]" %
                          (tuple(model_t.shape), nchan, nbin))
-    nmodel = model_t.shape[0]
     freqs_t = to_dev(freqs, dev, f64).reshape(-1)
     if freqs_t.numel() == nchan:
         freqs_t = freqs_t.repeat(nsub)
@@ -112,35 +139,104 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
         gdm_t = to_dev(guess_DM, dev, f64).reshape(-1)
         if gdm_t.numel() == 1:
             gdm_t = gdm_t.repeat(nsub)
+    per_sub = dict(data=data_t, freqs=freqs_t, P=P_t, init=init_t,
+                   flags=flags_t, nu_fits=nu_fits_t, nu_outs=nu_outs_t,
+                   errs=errs_t, mask=mask_t, mi=mi_t, gw=gw_t, gdm=gdm_t,
+                   gtau=gtau_t)
+    if n_x is None:
+        n_x = x_subints(flags_t, init_t, log10_tau, nsub)
+    xsel = None
+    cfg = dict(model=model_t, log10_tau=log10_tau, option=option,
+               is_toa=is_toa, mode=mode, max_iter=max_iter, guess=guess,
+               guess_Ns=guess_Ns, no_hcut=no_hcut)
+    lib = _lib.load()
+    need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
+    if max_workspace is None:
+        free, _ = torch.cuda.mem_get_info(dev)
+        max_workspace = free // 2
+    if need <= max_workspace or nsub == 1:
+        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
+    # chunks of equal size whose workspace fits the budget
+    per = max(1, int(nsub * max_workspace // max(need, 1)))
+    while per > 1 and _workspace_bytes(lib, per_sub, 0, per, per, cfg) > \
+            max_workspace:
+        per //= 2
+    if xsel is None:
+        fl = _host(flags_t)
+        x3 = _host(init_t)[:, 3]
+        with np.errstate(over="ignore"):
+            tau0 = 10.0 ** x3 if log10_tau else x3
+        xsel = (fl[:, 3] != 0) | (fl[:, 4] != 0) | (tau0 != 0.0)
+    outs, ws = [], None
+    for c0 in range(0, nsub, per):
+        c1 = min(nsub, c0 + per)
+        r = _fit_slice(lib, dev, per_sub, c0, c1,
+                       int(np.count_nonzero(xsel[c0:c1])), cfg, ws)
+        ws = r["workspace"]
+        outs.append(r)
+    out = {k: torch.cat([o[k] for o in outs], 0)
+           for k in ("results", "scales", "scale_errs", "channel_snrs",
+                     "covariance")}
+    out["workspace"] = ws
+    out["_keep"] = tuple(o["_keep"] for o in outs)
+    return out
+
+
+def _desc(per_sub, c0, c1, n_x, cfg):
+    """ppf_fit_desc of sub-ints [c0, c1) (pointers into the device tensors;
+    outputs left NULL)."""
+    sl = slice(c0, c1)
+
+    def pp(t):
+        return None if t is None else _p(t[sl])
+    data_t = per_sub["data"]
+    nchan, nbin = data_t.shape[1:]
+    model_t = cfg["model"]
+    d = _lib.FitDesc()
+    d.nsub, d.nchan, d.nbin = c1 - c0, nchan, nbin
+    d.data_dtype = _lib.PPF_F32 if data_t.dtype == torch.float32 else \
+        _lib.PPF_F64
+    d.data, d.model, d.nmodel = pp(data_t), _p(model_t), model_t.shape[0]
+    d.model_index, d.chan_mask = pp(per_sub["mi"]), pp(per_sub["mask"])
+    d.freqs, d.P, d.errs = pp(per_sub["freqs"]), pp(per_sub["P"]), \
+        pp(per_sub["errs"])
+    d.init, d.fit_flags = pp(per_sub["init"]), pp(per_sub["flags"])
+    d.nu_fits, d.nu_outs = pp(per_sub["nu_fits"]), pp(per_sub["nu_outs"])
+    d.log10_tau, d.option = int(bool(cfg["log10_tau"])), int(cfg["option"])
+    d.is_toa = int(bool(cfg["is_toa"]))
+    d.mode, d.max_iter = int(cfg["mode"]), int(cfg["max_iter"])
+    d.guess, d.guess_Ns = int(bool(cfg["guess"])), int(cfg["guess_Ns"])
+    d.guess_weights, d.guess_DM = pp(per_sub["gw"]), pp(per_sub["gdm"])
+    d.guess_tau = pp(per_sub["gtau"])
+    d.x_subints = int(max(n_x, 1)) if n_x < (c1 - c0) else 0
+    d.options = _lib.OPT_NO_HCUT if cfg["no_hcut"] else 0
+    return d
+
+
+def _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg):
+    d = _desc(per_sub, c0, c1, n_x, cfg)
+    nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    if nbytes == 0:
+        raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
+                                  " (nbin must be a power of two in "
+                                  "[32, 8192])" % (d.nsub, d.nchan, d.nbin))
+    return nbytes
+
+
+def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace):
+    f64 = torch.float64
+    nsub = c1 - c0
+    nchan = per_sub["data"].shape[1]
     results = torch.zeros((nsub, _lib.RESULT_DOUBLES), dtype=f64, device=dev)
     scales = torch.zeros((nsub, nchan), dtype=f64, device=dev)
     scale_errs = torch.zeros_like(scales)
     channel_snrs = torch.zeros_like(scales)
     cov = torch.zeros((nsub, 5, 5), dtype=f64, device=dev)
-    d = _lib.FitDesc()
-    d.nsub, d.nchan, d.nbin = nsub, nchan, nbin
-    d.data_dtype = _lib.PPF_F32 if data_t.dtype == torch.float32 else \
-        _lib.PPF_F64
-    d.data, d.model, d.nmodel = _p(data_t), _p(model_t), nmodel
-    d.model_index, d.chan_mask = _p(mi_t), _p(mask_t)
-    d.freqs, d.P, d.errs = _p(freqs_t), _p(P_t), _p(errs_t)
-    d.init, d.fit_flags = _p(init_t), _p(flags_t)
-    d.nu_fits, d.nu_outs = _p(nu_fits_t), _p(nu_outs_t)
-    d.log10_tau, d.option, d.is_toa = int(bool(log10_tau)), int(option), \
-        int(bool(is_toa))
-    d.mode, d.max_iter = int(mode), int(max_iter)
-    d.guess, d.guess_Ns = int(bool(guess)), int(guess_Ns)
-    d.guess_weights, d.guess_DM = _p(gw_t), _p(gdm_t)
-    d.guess_tau = _p(gtau_t)
+    d = _desc(per_sub, c0, c1, n_x, cfg)
     d.results, d.scales, d.scale_errs = _p(results), _p(scales), \
         _p(scale_errs)
     d.channel_snrs, d.covariance = _p(channel_snrs), _p(cov)
-    lib = _lib.load()
-    nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
-    if nbytes == 0:
-        raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
-                                  " (nbin must be a power of two in "
-                                  "[32, 8192])" % (nsub, nchan, nbin))
+    nbytes = _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg)
     if workspace is None or workspace.numel() < nbytes or \
             workspace.device != dev:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -148,8 +244,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     ctx = _lib.context(dev.index)
     _lib.check(lib.ppf_fit_batch(ctx, ctypes.byref(d), _stream(dev)), ctx)
     # keep inputs alive until the stream has consumed them
-    keep = (data_t, model_t, freqs_t, P_t, init_t, flags_t, nu_fits_t,
-            nu_outs_t, errs_t, mask_t, mi_t, gw_t, gdm_t, gtau_t)
+    keep = (cfg["model"],) + tuple(v for v in per_sub.values()
+                                   if v is not None)
     return dict(results=results, scales=scales, scale_errs=scale_errs,
                 channel_snrs=channel_snrs, covariance=cov,
                 workspace=workspace, _keep=keep)

@@ -115,13 +115,23 @@ def _channel_map(data, isub, model_data, same_freqs):
 
 
 class _Rows(object):
-    """Every usable sub-integration of every archive, laid out in MODEL
-    channel order (row s, channel m = the data channel mapped onto model
-    channel m), device-resident."""
+    """Every usable sub-integration of every archive, device-resident.
+
+    The accumulation layout is MODEL channel order (row s, channel m = the
+    data channel mapped onto model channel m): numpy's fancy-index "+=" of
+    ppalign.py:244-247 keeps the LAST of several data channels mapped onto
+    one model channel, so only that one is placed there.  The fit, however,
+    runs over the full ichans list (ppalign.py:198-227: the guess profile,
+    nu_fit and fit_portrait_full all see every data channel, duplicates
+    included): rows without duplicate model channels are fitted in model
+    order against the shared template; rows with duplicates get a second,
+    data-order ("slot") layout whose model rows are gathered from the
+    template by model channel (`dup_*` below)."""
 
     def __init__(self, archives, model_data, npol, dev):
         nchan, nbin = model_data.nchan, model_data.nbin
-        rows, meta = [], []
+        rows, meta, dup = [], [], []
+        exact = True                 # every amplitude survives a float32 trip
         for data in archives:
             try:
                 fd = data.freqs - model_data.freqs
@@ -133,33 +143,50 @@ class _Rows(object):
                 ichans, mch = _channel_map(data, isub, model_data, same)
                 if len(ichans) == 0:
                     continue
-                # numpy fancy-index "+=" keeps the LAST of duplicate model
-                # channels (ppalign.py:244-247): keep that one
                 last = {}
                 for i, m in enumerate(mch):
                     last[int(m)] = i
                 sel = np.array(sorted(last.values()), dtype=int)
-                ich, mch = ichans[sel], mch[sel]
-                x = np.zeros((npol, nchan, nbin), dtype=np.float32)
+                ich, mchl = ichans[sel], mch[sel]
+                x = np.zeros((npol, nchan, nbin))
                 for ipol in range(npol):
-                    x[ipol, mch] = data.subints[isub, ipol, ich]
+                    x[ipol, mchl] = data.subints[isub, ipol, ich]
+                    if exact:
+                        v = np.asarray(data.subints[isub, ipol, ichans])
+                        exact = np.array_equal(
+                            v.astype(np.float32).astype(np.float64), v)
                 freqs = np.ones(nchan) * np.nan
-                freqs[mch] = data.freqs[isub, ich]
+                freqs[mchl] = data.freqs[isub, ich]
                 m = dict(mask=np.zeros(nchan, np.uint8), freqs=freqs,
                          P=float(data.Ps[isub]), DM_guess=float(DM_guess),
                          DM=float(data.DM), errs=np.ones(nchan),
-                         gw=np.zeros(nchan), nchanx=len(ich))
-                m["mask"][mch] = 1
-                m["errs"][mch] = data.noise_stds[isub, 0, ich]
-                m["gw"][mch] = data.weights[isub, ich]
-                m["nu_fit"] = guess_fit_freq(data.freqs[isub, ich],
-                                             data.SNRs[isub, 0, ich])
+                         gw=np.zeros(nchan), nchanx=len(ichans),
+                         dup=len(sel) < len(ichans))
+                m["mask"][mchl] = 1
+                m["errs"][mchl] = data.noise_stds[isub, 0, ich]
+                m["gw"][mchl] = data.weights[isub, ich]
+                # guess_fit_freq over the full ichans (ppalign.py:214)
+                m["nu_fit"] = guess_fit_freq(data.freqs[isub, ichans],
+                                             data.SNRs[isub, 0, ichans])
+                if m["dup"] and len(ichans) > 1:
+                    dup.append(dict(
+                        row=len(rows), mch=np.asarray(mch, dtype=int),
+                        last=sel, x=np.asarray(data.subints[isub, 0, ichans],
+                                               dtype=np.float64),
+                        freqs=np.asarray(data.freqs[isub, ichans], float),
+                        errs=np.asarray(data.noise_stds[isub, 0, ichans],
+                                        float),
+                        gw=np.asarray(data.weights[isub, ichans], float)))
                 rows.append(x)
                 meta.append(m)
         self.n = len(rows)
         self.meta = meta
+        # float32 amplitudes (PSRCHIVE's type) unless some value would not
+        # survive the round trip (e.g. after rm_baseline): then float64
+        self.dtype = np.float32 if exact else np.float64
         if self.n:
-            self.data = torch.as_tensor(np.stack(rows)).to(dev)   # [S, npol, nchan, nbin]
+            self.data = torch.as_tensor(
+                np.stack(rows).astype(self.dtype)).to(dev)  # [S, npol, nchan, nbin]
         fill = np.nanmean([np.nanmean(m["freqs"]) for m in meta]) if meta else 1.0
         self.freqs = np.array([np.where(np.isnan(m["freqs"]), fill, m["freqs"])
                                for m in meta])
@@ -170,15 +197,95 @@ class _Rows(object):
         self.DM_guess = np.array([m["DM_guess"] for m in meta])
         self.nu_fit = np.array([m["nu_fit"] for m in meta])
         self.nchanx = np.array([m["nchanx"] for m in meta])
+        self.dup = np.array([m["dup"] for m in meta], dtype=bool)
+        self.dup_rows = dup
+        self._dup_dev = None
+        if dup:
+            self._dup_layout(dev, fill)
+
+    def _dup_layout(self, dev, fill):
+        """Slot-order inputs of the rows with duplicate model channels:
+        slot j of row d = data channel ichans[j] (model channel mch[j]),
+        padded with masked slots to the longest ichans.  Rows with the same
+        mch list share one gathered model (index `gidx`)."""
+        D = self.dup_rows
+        nchf = max(len(d["mch"]) for d in D)
+        nbin = D[0]["x"].shape[1]
+        x = np.zeros((len(D), nchf, nbin))
+        mask = np.zeros((len(D), nchf), np.uint8)
+        freqs = np.full((len(D), nchf), fill)
+        errs = np.ones((len(D), nchf))
+        gw = np.zeros((len(D), nchf))
+        groups, gidx, midx = {}, [], []
+        for i, d in enumerate(D):
+            n = len(d["mch"])
+            x[i, :n], mask[i, :n] = d["x"], 1
+            freqs[i, :n], errs[i, :n], gw[i, :n] = d["freqs"], d["errs"],                 d["gw"]
+            key = tuple(d["mch"])
+            if key not in groups:
+                groups[key] = len(gidx)
+                gidx.append(np.pad(d["mch"], (0, nchf - n)))
+            midx.append(groups[key])
+        f64 = torch.float64
+        rows = [d["row"] for d in D]
+        init = np.zeros((len(D), 5))
+        init[:, 1] = self.DM_guess[rows]
+        self._dup_dev = dict(
+            x=torch.as_tensor(x.astype(self.dtype)).to(dev),
+            mask=torch.as_tensor(mask, device=dev),
+            freqs=torch.as_tensor(freqs, dtype=f64, device=dev),
+            errs=torch.as_tensor(errs, dtype=f64, device=dev),
+            gw=torch.as_tensor(gw, dtype=f64, device=dev),
+            P=torch.as_tensor(self.P[rows], dtype=f64, device=dev),
+            DM=torch.as_tensor(self.DM_guess[rows], dtype=f64, device=dev),
+            init=torch.as_tensor(init, dtype=f64, device=dev),
+            nu_fits=torch.as_tensor(np.repeat(self.nu_fit[rows, None], 3,
+                                              axis=1), dtype=f64, device=dev),
+            nu_outs=torch.full((len(D), 3), float("nan"), dtype=f64,
+                               device=dev),
+            gidx=torch.as_tensor(np.array(gidx), dtype=torch.int64,
+                                 device=dev),
+            midx=np.array(midx, dtype=np.int32))
+
+
+def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
+    """One batched ppf_fit_batch of `rows` (guess + phase[/DM] fit), the
+    reference's exceptions raised for failed sub-ints."""
+    flags = [1, int(bool(fit_dm)), 0, 0, 0]
+    res = engine.fit_batch(
+        rows, model, dc["freqs"], dc["P"], dc["init"], flags,
+        nu_fits=dc["nu_fits"], nu_outs=dc["nu_outs"], errs=dc["errs"],
+        chan_mask=dc["mask"], model_index=mi, log10_tau=False, is_toa=True,
+        guess=True, guess_weights=dc["gw"], guess_DM=dc["DM"],
+        guess_Ns=nbin, dev=dev)
+    I = _lib.RESULT_INDEX
+    r = res["results"]
+    st = r[:, I["status"]].to(torch.int64).cpu().numpy()
+    bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
+    if len(bad):
+        from .pplib import _raise_status
+        _raise_status(int(st[bad[0]]))
+    phi = r[:, I["params"]][:, 0]
+    DM = r[:, I["params"]][:, 1]
+    nu_ref = r[:, I["nu_out"]][:, 0]
+    ok = dc["mask"] != 0
+    ph = phi[:, None] + (Dconst * DM / dc["P"])[:, None] * (
+        dc["freqs"] ** -2.0 - (nu_ref ** -2.0)[:, None])
+    zero = torch.zeros((), dtype=torch.float64, device=dev)
+    ph = torch.where(ok, ph, zero)
+    wt = torch.where(ok, res["scales"] / dc["errs"] ** 2, zero)
+    return ph, wt
 
 
 def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
     """One batched fit of every row against the current template: the
-    per-row rotation phases and weights of ppalign.py:222-247."""
+    per-row rotation phases and weights of ppalign.py:222-247 (model
+    channel order)."""
     S = R.n
     nchan = model_port.shape[0]
     f64 = torch.float64
-    multi = np.where(R.nchanx > 1)[0]
+    dup = getattr(R, "dup", np.zeros(S, dtype=bool))
+    multi = np.where((R.nchanx > 1) & ~dup)[0]
     # the rows' constant inputs stay resident across iterations
     dc = R.__dict__.setdefault("_dev_inputs", {})
     if dc.get("multi") is None or not np.array_equal(dc["multi"], multi):
@@ -204,36 +311,27 @@ def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
     if len(multi):
         rows = R.data[:, 0] if len(multi) == S else \
             R.data[torch.as_tensor(multi, device=dev), 0]
-        flags = [1, int(bool(fit_dm)), 0, 0, 0]
-        res = engine.fit_batch(
-            rows, model_port, dc["freqs"], dc["P"], dc["init"],
-            flags, nu_fits=dc["nu_fits"], nu_outs=dc["nu_outs"],
-            errs=dc["errs"], chan_mask=dc["mask"], log10_tau=False,
-            is_toa=True, guess=True, guess_weights=dc["gw"],
-            guess_DM=dc["DM"], guess_Ns=nbin, dev=dev)
-        I = _lib.RESULT_INDEX
-        r = res["results"]
-        st = r[:, I["status"]].to(torch.int64).cpu().numpy()
-        bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
-        if len(bad):
-            from .pplib import _raise_status
-            _raise_status(int(st[bad[0]]))
-        phi = r[:, I["params"]][:, 0]
-        DM = r[:, I["params"]][:, 1]
-        nu_ref = r[:, I["nu_out"]][:, 0]
-        ok = dc["mask"] != 0
-        fr = dc["freqs"]
-        ph = phi[:, None] + (Dconst * DM / dc["P"])[:, None] * (
-            fr ** -2.0 - (nu_ref ** -2.0)[:, None])
-        zero = torch.zeros((), dtype=f64, device=dev)
-        ph = torch.where(ok, ph, zero)
-        wt = torch.where(ok, res["scales"] / dc["errs"] ** 2, zero)
+        ph, wt = _fit_rows(rows, model_port, None, dc, fit_dm, nbin, dev)
         if len(multi) == S:
             phases, weights = ph, wt
         else:
             mi = torch.as_tensor(multi, device=dev)
             phases[mi] = ph
             weights[mi] = wt
+    if getattr(R, "_dup_dev", None) is not None:
+        # rows with duplicate model channels: fit in slot order against the
+        # gathered template rows, then place each model channel's LAST slot
+        dd = R._dup_dev
+        mp = torch.as_tensor(np.asarray(model_port) if not isinstance(
+            model_port, torch.Tensor) else model_port, dtype=f64, device=dev)
+        models = mp[dd["gidx"]]                       # [G, nchf, nbin]
+        ph, wt = _fit_rows(dd["x"], models, dd["midx"], dd, fit_dm, nbin,
+                           dev)
+        for i, d in enumerate(R.dup_rows):
+            s, last = d["row"], torch.as_tensor(d["last"], device=dev)
+            m = torch.as_tensor(d["mch"][d["last"]], device=dev)
+            phases[s, m] = ph[i, last]
+            weights[s, m] = wt[i, last]
     for s in np.where(R.nchanx == 1)[0]:      # 1-channel hack (ppalign.py:231-236)
         m = int(np.where(R.mask[s])[0][0])
         x = R.data[s, 0, m].double().cpu().numpy()
@@ -276,35 +374,53 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
     dev = engine.device(dev)
     # archives are read once and kept resident (the reference re-reads them
     # every iteration; the skip tests give the same outcome each time)
-    archives = []
-    for name in datafiles:
-        try:
-            data = _load(name, state, tscrunch, pscrunch, quiet)
-        except RuntimeError:
-            if not quiet:
-                print("%s: cannot load_data().  Skipping it." % name)
-            continue
-        except IndexError:
-            if not quiet:
-                print("%s: has npol = 1.  Skipping it." % name)
-            continue
-        if _usable(data, name, model_data, SNR_cutoff, quiet):
-            archives.append(data)
-    R = _Rows(archives, model_data, npol, dev)
     from . import dist as _dist
+    archives, err = [], None
+    try:
+        for name in datafiles:
+            try:
+                data = _load(name, state, tscrunch, pscrunch, quiet)
+            except RuntimeError:
+                if not quiet:
+                    print("%s: cannot load_data().  Skipping it." % name)
+                continue
+            except IndexError:
+                if not quiet:
+                    print("%s: has npol = 1.  Skipping it." % name)
+                continue
+            if _usable(data, name, model_data, SNR_cutoff, quiet):
+                archives.append(data)
+        R = _Rows(archives, model_data, npol, dev)
+    except Exception as exc:
+        if not comm:
+            raise
+        err = exc
+    if comm:
+        _dist.raise_if_any_failed(err, dev)
     count = 1
     while niter:
         if not quiet:
             print("Doing iteration %d..." % count)
         out = torch.zeros((npol, nchan, nbin), dtype=torch.float64, device=dev)
         wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
-        if R.n:
-            phases, weights = _fit_and_weights(R, model_port, fit_dm, nbin, dev)
-            for ipol in range(npol):
-                w = torch.zeros_like(wsum)
-                engine.align_accum(R.data[:, ipol], phases, weights, out[ipol],
-                                   wsum if ipol == 0 else w, dev=dev)
+        err = None
+        try:
+            if R.n:
+                phases, weights = _fit_and_weights(R, model_port, fit_dm,
+                                                   nbin, dev)
+                for ipol in range(npol):
+                    w = torch.zeros_like(wsum)
+                    engine.align_accum(R.data[:, ipol], phases, weights,
+                                       out[ipol], wsum if ipol == 0 else w,
+                                       dev=dev)
+        except Exception as exc:        # raised on every rank, below
+            if not comm:
+                raise
+            err = exc
         if comm:
+            # a failed rank must not leave the others blocked in the
+            # all-reduce: agree on success first
+            _dist.raise_if_any_failed(err, dev)
             _dist.allreduce_sum_(out, wsum)
         good = wsum > 0
         out[:, good] /= wsum[good][None, :, None]

@@ -1,0 +1,178 @@
+"""Inputs of the full-shape golden cases (tests/golden/full.npz), rebuilt
+from a few stored parameters (TEST INFRASTRUCTURE; no reference import).
+
+make_golden_full.py builds the inputs here, hands them to the REFERENCE and
+stores only its outputs plus a SHA-256 of the inputs; the tests rebuild the
+inputs here and check the hash (see synth_np.py).
+"""
+import os
+
+import numpy as np
+
+import synth_np as S
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+NARROW_GMODEL = os.path.join(HERE, "narrow.gmodel")
+# example.gmodel plus a narrow (FWHM 0.002 rot) component: its power at
+# 2048 bins stays above 1e-28 of the peak up to Nyquist
+NARROW_PARAMS = np.concatenate([S.read_gmodel()[2],
+                                [0.62, 0.0, 0.002, 0.0, 3.0, -1.0]])
+
+
+def write_narrow(path=NARROW_GMODEL):
+    """tests/golden/narrow.gmodel (committed; rewritten only if missing)."""
+    if os.path.exists(path):
+        return
+    code, nu_ref, _, alpha = S.read_gmodel()
+    S.write_gmodel(path, code, nu_ref, NARROW_PARAMS, alpha,
+                   name="PSR_NARROW")
+
+
+FITS = [
+    dict(name="c3_all_512x2048_a", nchan=512, nbin=2048, flags=[1, 1, 1, 1, 1],
+         seed=101, tau=2e-3),
+    dict(name="c3_all_512x2048_b", nchan=512, nbin=2048, flags=[1, 1, 1, 1, 1],
+         seed=102, tau=2e-3),
+    dict(name="c3_pdta_512x2048", nchan=512, nbin=2048, flags=[1, 1, 0, 1, 1],
+         seed=103, tau=2e-3),
+    dict(name="narrow_pd_512x2048", nchan=512, nbin=2048,
+         flags=[1, 1, 0, 0, 0], seed=104, narrow=True),
+    dict(name="pd_64x4096", nchan=64, nbin=4096, flags=[1, 1, 0, 0, 0],
+         seed=105),
+    dict(name="pdta_64x128", nchan=64, nbin=128, flags=[1, 1, 0, 1, 1],
+         seed=106, tau=2e-3),
+]
+
+
+def fit_inputs(c):
+    """(data, model, freqs, P, truth, init, nu_fit) of a fit case, rebuilt
+    identically by the tests (tests/test_gpu_fullshape.py)."""
+    rng = np.random.default_rng(20251016 + c["seed"])
+    nchan, nbin = c["nchan"], c["nbin"]
+    phi = rng.uniform(-0.5, 0.5)
+    dDM = rng.normal(3e-4, 2e-4)
+    P = S.P0 * (1.0 + 1e-6 * rng.normal())
+    phi_guess_off = rng.normal(0, 2e-3)
+    model, freqs = S.template(nchan, nbin, gmodel=NARROW_GMODEL if
+                              c.get("narrow") else None)
+    tau = c.get("tau", 0.0)
+    data = S.subint(c["seed"], model, freqs, phi, S.DM0 + dDM, P, tau=tau)
+    nu_fit = float(_guess_fit_freq(freqs))
+    phi_g = _phase_transform(phi + phi_guess_off, S.DM0, 1500.0, nu_fit, P)
+    scat = c["flags"][3] == 1
+    init = [phi_g, S.DM0, 0.0, np.log10(1.0 / nbin) if scat else 0.0,
+            -4.0 if scat else 0.0]
+    return data, model, freqs, P, np.array([phi, S.DM0 + dDM, 0.0, tau,
+                                            -4.0]), init, nu_fit
+
+
+def _guess_fit_freq(freqs, SNRs=None):
+    nu0 = (freqs.min() + freqs.max()) * 0.5
+    w = (np.ones(len(freqs)) if SNRs is None else SNRs) * freqs ** -2
+    return nu0 + np.sum((freqs - nu0) * w) / np.sum(w)
+
+
+def _phase_transform(phi, DM, nu1, nu2, P):
+    x = phi + S.DCONST * DM / P * (nu2 ** -2 - nu1 ** -2)
+    x = x % 1.0
+    return x - 1.0 if x >= 0.5 else x
+
+
+TOAS = [
+    dict(name="c1", nfile=5, nsub=10, nchan=64, nbin=512, scint=True,
+         seed=201, DM0=True),
+    dict(name="c2", nfile=1, nsub=8, nchan=512, nbin=2048, seed=202),
+    dict(name="narrow", nfile=1, nsub=4, nchan=512, nbin=2048, seed=203,
+         narrow=True),
+]
+
+
+def toa_inputs(c):
+    """Per archive: subints [nsub, nchan, nbin] f32-rounded, weights, SNRs,
+    doppler factors, epochs; plus freqs.  Rebuilt identically by the tests."""
+    rng = np.random.default_rng(20251016 + c["seed"])
+    nchan, nbin, nsub = c["nchan"], c["nbin"], c["nsub"]
+    model, freqs = S.template(nchan, nbin, gmodel=NARROW_GMODEL if
+                              c.get("narrow") else None)
+    files = []
+    for f in range(c["nfile"]):
+        dDM = rng.normal(3e-4, 2e-4)            # example.py: one per archive
+        subs = np.zeros((nsub, nchan, nbin))
+        for s in range(nsub):
+            phi = rng.uniform(-0.5, 0.5)
+            subs[s] = S.subint(c["seed"] * 1000 + f * 100 + s, model, freqs,
+                               phi, S.DM0 + dDM, S.P0, scint=c.get("scint",
+                                                                   False))
+        weights = np.ones((nsub, nchan))
+        if f == 1 or c["nfile"] == 1:           # zap a few channels
+            for s in range(nsub):
+                weights[s, rng.choice(nchan, 3 + s % 4, replace=False)] = 0.0
+        dfs = 1.0 + 1e-4 * rng.normal(size=nsub)
+        epochs = 57202.0 + 20.0 * f + np.arange(nsub) * 60.0 / 86400.0
+        files.append(dict(subints=subs, weights=weights, dfs=dfs,
+                          epochs=epochs, dDM=dDM))
+    return files, freqs
+
+
+ALIGNS = [
+    dict(name="c4", nfile=16, nsub=1, nchan=256, nbin=1024, niter=3,
+         seed=301),
+    dict(name="dup", nfile=4, nsub=2, nchan=32, nbin=256, niter=2, seed=302,
+         tmpl_nchan=16),
+]
+
+
+def align_inputs(c):
+    """(archives, guess template [tmpl_nchan, nbin], data freqs, template
+    freqs) rebuilt identically by the tests."""
+    rng = np.random.default_rng(20251016 + c["seed"])
+    nchan, nbin, nsub = c["nchan"], c["nbin"], c["nsub"]
+    model, freqs = S.template(nchan, nbin)
+    arch = []
+    for f in range(c["nfile"]):
+        subs = np.zeros((nsub, nchan, nbin))
+        for s in range(nsub):
+            phi = rng.uniform(-0.5, 0.5)
+            dDM = rng.normal(3e-4, 2e-4)
+            subs[s] = S.subint(c["seed"] * 1000 + f * 10 + s, model, freqs,
+                               phi, S.DM0 + dDM, S.P0, noise=0.5)
+        weights = np.ones((nsub, nchan))
+        if f == 2:
+            weights[:, rng.choice(nchan, 4, replace=False)] = 0.0
+        arch.append(dict(subints=subs, weights=weights))
+    tn = c.get("tmpl_nchan", nchan)
+    tfreqs = S.channel_freqs(tn)
+    prof = S.f32(arch[0]["subints"].mean(axis=(0, 1)))
+    guess = np.tile(prof, (tn, 1))
+    return arch, guess, freqs, tfreqs
+
+
+# configs[4] (16384 x 1024, CHIME-like 400-800 MHz, phi + DM + tau + alpha):
+# the reference cannot run this width (its dense covariance cube,
+# pptoaslib.py:731, needs 3.5e13 B), so these outputs come from the ORACLE
+# (make_golden_oracle.py), itself pinned to the reference at <= 512 channels
+C5 = [dict(name="c5_a", nchan=16384, nbin=1024, flags=[1, 1, 0, 1, 1],
+           seed=401, tau=5e-3, nu_tau=600.0),
+      dict(name="c5_b", nchan=16384, nbin=1024, flags=[1, 1, 0, 1, 1],
+           seed=402, tau=5e-3, nu_tau=600.0)]
+
+
+def c5_inputs(c):
+    """(data, model, freqs, P, truth, init, nu_fit) of a configs[4] case."""
+    rng = np.random.default_rng(20251016 + c["seed"])
+    nchan, nbin = c["nchan"], c["nbin"]
+    phi = rng.uniform(-0.5, 0.5)
+    dDM = rng.normal(3e-4, 2e-4)
+    P = S.P0
+    model, freqs = S.template(nchan, nbin, lo=400.0, bw=400.0)
+    data = S.subint(c["seed"], model, freqs, phi, S.DM0 + dDM, P,
+                    tau=c["tau"], nu_tau=c["nu_tau"])
+    nu_fit = float(_guess_fit_freq(freqs))
+    # GetTOAs guesses (pptoas.py:467-502): log10 tau = log10(1/nbin),
+    # alpha = -4; the phase guess starts within 1e-3 rot of the truth
+    phi_g = _phase_transform(phi + rng.normal(0, 1e-3), S.DM0, 1500.0,
+                             nu_fit, P)
+    init = [phi_g, S.DM0, 0.0, np.log10(1.0 / nbin), -4.0]
+    return data, model, freqs, P, np.array([phi, S.DM0 + dDM, 0.0, c["tau"],
+                                            -4.0]), init, nu_fit

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_struct_layouts_match():
     lib = _lib.load()
-    assert lib.ppf_abi_version() == 1
+    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 2
     assert lib.ppf_sizeof_fit_desc() == ctypes.sizeof(_lib.FitDesc)
     assert lib.ppf_sizeof_result() == 8 * _lib.RESULT_DOUBLES == 256
 
@@ -41,8 +41,19 @@ def test_workspace_query_and_validation_without_gpu():
     d = _lib.FitDesc()
     d.nsub, d.nchan, d.nbin, d.nmodel = 10, 512, 2048, 1
     nb = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
-    # X alone is nsub*nchan*nharm complex128
+    # X alone is nsub*nchan*nharm complex128 (every sub-int by default)
     assert nb >= 10 * 512 * 1025 * 16
+    # x_subints = 2: only two cross-spectrum slots on the fused phase+DM
+    # path (X was reserved for every sub-int)
+    d.x_subints = 2
+    nb2 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    assert nb - nb2 == 8 * 512 * 1025 * 16
+    # off the fused path (nbin 4096: block FFT, moments taken from X) every
+    # sub-int streams X whatever x_subints says
+    d.nbin = 4096
+    nb3 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    d.x_subints = 0
+    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == nb3
     d.nbin = 1000   # not a power of two
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0
     # a NULL context is rejected before touching the device
@@ -79,3 +90,16 @@ def test_gauss_portrait_entry_validates_without_gpu():
     with pytest.raises(KeyError):
         engine.gauss_portraits("0x0", np.zeros((1, 8)), [0.0], [[1.0]],
                                [1.0], 64)
+
+
+def test_x_subints_host_rule():
+    """engine.x_subints restates k_classify's test: scattering flags, or a
+    nonzero initial tau (10**tau when log10_tau)."""
+    from pulseportraiture_amd import engine
+    flags = np.array([[1, 1, 0, 0, 0], [1, 1, 0, 1, 1], [1, 1, 0, 0, 1],
+                      [1, 1, 0, 0, 0]])
+    init = np.zeros((4, 5))
+    init[3, 3] = 1e-3
+    assert engine.x_subints(flags, init, False, 4) == 3
+    assert engine.x_subints(flags, init, True, 4) == 4       # 10**0 = 1
+    assert engine.x_subints([1, 1, 0, 0, 0], np.zeros((3, 5)), False, 3) == 0

@@ -219,8 +219,13 @@ def bench_align(args):
         DM_guess=np.full(count, synth.DM0),
         nu_fit=np.full(count, guess_fit_freq(b["freqs"])),
         nchanx=np.full(count, nchan))
-    # initial template: archive 0's mean profile tiled
-    prof = b["data"][0].double().mean(dim=0).cpu().numpy()
+    # initial template (the reference notebook's
+    # make_constant_portrait(profile=DataPortrait.prof)): archive 0's mean
+    # profile, dedispersed at DM0 to the band centre, tiled
+    D = 0.000241 ** -1
+    ded = engine.rotate_rows(b["data"][0], D * synth.DM0 * (
+        b["freqs"] ** -2 - 1500.0 ** -2) / b["P"][0])
+    prof = ded.mean(dim=0).cpu().numpy()
     model0 = np.tile(prof, (nchan, 1))
     comm = dist.is_dist()
 

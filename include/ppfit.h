@@ -143,6 +143,11 @@ typedef struct ppf_fit_desc {
                                      sub-int streams X and nsub slots are
                                      always reserved. */
     int32_t options;              /* ppf_option bits                           */
+    int32_t guess_ref;            /* frame of the guess stage's dedispersed
+                                     mean profile: 0 = the mean usable
+                                     frequency, phase then moved to nu_fit
+                                     (GetTOAs, pptoas.py:461-499); 1 = nu_fit
+                                     itself (ppalign, ppalign.py:214-219) */
 } ppf_fit_desc;
 
 int ppf_abi_version(void);

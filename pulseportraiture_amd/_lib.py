@@ -62,7 +62,7 @@ class FitDesc(ctypes.Structure):
         ("results", _vp), ("scales", _vp), ("scale_errs", _vp),
         ("channel_snrs", _vp), ("covariance", _vp), ("workspace", _vp),
         ("workspace_bytes", ctypes.c_size_t),
-        ("x_subints", _i32), ("options", _i32),       # ABI 2
+        ("x_subints", _i32), ("options", _i32), ("guess_ref", _i32),  # ABI 2
     ]
 
 

@@ -333,6 +333,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         da.cbd = L.cbd; da.nblkd = L.nblkd; da.data = d->data; da.mask = d->chan_mask;
         da.freqs = d->freqs; da.P = d->P; da.guess_DM = d->guess_DM;
         da.guess_weights = d->guess_weights;
+        da.guess_ref = d->guess_ref; da.nu_fits = d->nu_fits;
         da.gP = (double *)(ws + L.gP); da.gw = (double *)(ws + L.gw);
         mark(7);
         if ((e = ppf::launch_dsum(da, st)) != hipSuccess) return hip_fail(ctx, e, "k_dsum");
@@ -344,6 +345,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ppf::GuessArgs ga{};
         ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = ilog2(d->nbin / 2);
         ga.kc = kc; ga.nblkd = L.nblkd; ga.Ns = d->guess_Ns; ga.mask = d->chan_mask;
+        ga.guess_ref = d->guess_ref;
         ga.freqs = d->freqs; ga.P = d->P; ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau;
         ga.nu_fits = d->nu_fits; ga.gP = da.gP; ga.gw = da.gw; ga.T = T; ga.T2 = T2;
         ga.KC = (const int32_t *)(ws + L.KC);

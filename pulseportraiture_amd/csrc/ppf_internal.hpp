@@ -38,6 +38,8 @@ struct XspecArgs {
 // k_dsum: GetTOAs guess profile, time-domain dedispersion (pptoas.py:461-464)
 struct DsumArgs {
     int nsub, nchan, nbin, dtype, cbd, nblkd;
+    int guess_ref;               // 1: dedisperse at nu_fits[s][0] (ppalign), 0: at the mean freq
+    const double *nu_fits;       // [nsub][3]
     const void *data;
     const uint8_t *mask;
     const double *freqs, *P, *guess_DM, *guess_weights;
@@ -67,6 +69,7 @@ struct XmomArgs {
 
 struct GuessArgs {
     int nsub, nchan, nbin, log2N, kc, nblkd, Ns;
+    int guess_ref;               // 1: the profile is already at nu_fit (no phase_transform)
     const uint8_t *mask;
     const double *freqs, *P, *guess_DM, *guess_tau, *nu_fits;
     const double *gP;            // [nsub][nblkd][nbin] (k_dsum)

@@ -320,7 +320,11 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
         if (!mask || mask[n]) { v[0] += fr[n]; v[1] += 1.0; }
     block_sum<2>(v, red);
     const double Dg = kDconst * a.guess_DM[s] / a.P[s];
-    const double nu_mean_m2 = pow(v[0] / v[1], -2.0);
+    double nu_mean_m2 = pow(v[0] / v[1], -2.0);
+    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
+        const double nf = a.nu_fits[(int64_t)s * 3];
+        if (nf == nf) nu_mean_m2 = pow(nf, -2.0);
+    }
     const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
     const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)s * a.nchan * nbin;
     double wsum = 0.0, wcnt = 0.0;
@@ -392,7 +396,12 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
     v0 = wave_sum(v0);
     v1 = wave_sum(v1);
     const double Dg = (double)NB * kDconst * a.guess_DM[s] / a.P[s];
-    const double mu = v0 / v1, nu_mean_m2 = 1.0 / (mu * mu);
+    const double mu = v0 / v1;
+    double nu_mean_m2 = 1.0 / (mu * mu);
+    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
+        const double nf = a.nu_fits[(int64_t)s * 3];
+        if (nf == nf) nu_mean_m2 = 1.0 / (nf * nf);
+    }
     const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
     const VecT *rows = reinterpret_cast<const VecT *>(a.data) + (int64_t)s * a.nchan * (NB / VW);
     double acc[J];
@@ -560,9 +569,12 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
         double nu_fit = a.nu_fits[(int64_t)s * 3 + 0];
         if (nu_fit != nu_fit) nu_fit = nu_mean;
         double DM = a.guess_DM[s], P = a.P[s];
-        double out = phase + kDconst * DM * pow(P, -1.0) * (pow(nu_fit, -2.0) - pow(nu_mean, -2.0));
-        if (fabs(out) >= 0.5) out = out - floor(out);   // python % 1
-        if (out >= 0.5) out -= 1.0;
+        double out = phase;
+        if (!a.guess_ref) {     // GetTOAs: phase_transform(..., mod=True)
+            out = phase + kDconst * DM * pow(P, -1.0) * (pow(nu_fit, -2.0) - pow(nu_mean, -2.0));
+            if (fabs(out) >= 0.5) out = out - floor(out);   // python % 1
+            if (out >= 0.5) out -= 1.0;
+        }
         a.x0[(int64_t)s * 8 + 0] = out;
     }
 }

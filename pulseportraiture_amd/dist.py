@@ -109,3 +109,8 @@ def raise_if_any_failed(err, device=None):
     if t.item() > 0.0:
         raise RuntimeError("another rank failed (its exception is raised "
                            "there)")
+
+
+def backend():
+    """The process group's backend ('nccl' = RCCL, 'gloo'), or None."""
+    return dist.get_backend() if dist.is_initialized() else None

@@ -79,14 +79,16 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               log10_tau=False, option=0, is_toa=True, mode=_lib.PPF_MODE_FULL,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
               guess_Ns=100, guess_tau=None, dev=None, workspace=None,
-              n_x=None, no_hcut=False, max_workspace=None):
+              n_x=None, no_hcut=False, max_workspace=None, guess_ref=0):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
 
     n_x: cross-spectrum slots (sub-ints whose fit streams X); None computes
     it from fit_flags / init (x_subints).  no_hcut: sum every harmonic
-    (PPF_OPT_NO_HCUT).  max_workspace: workspace budget in bytes (default
+    (PPF_OPT_NO_HCUT).  guess_ref: frame of the guess profile (0: mean
+    frequency then phase_transform to nu_fit, GetTOAs; 1: nu_fit, ppalign).
+    max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
     the batch it is in).
@@ -148,7 +150,7 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     xsel = None
     cfg = dict(model=model_t, log10_tau=log10_tau, option=option,
                is_toa=is_toa, mode=mode, max_iter=max_iter, guess=guess,
-               guess_Ns=guess_Ns, no_hcut=no_hcut)
+               guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref)
     lib = _lib.load()
     need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
     if max_workspace is None:
@@ -210,6 +212,7 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.guess_tau = pp(per_sub["gtau"])
     d.x_subints = int(max(n_x, 1)) if n_x < (c1 - c0) else 0
     d.options = _lib.OPT_NO_HCUT if cfg["no_hcut"] else 0
+    d.guess_ref = int(cfg["guess_ref"])
     return d
 
 

@@ -257,7 +257,7 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
         nu_fits=dc["nu_fits"], nu_outs=dc["nu_outs"], errs=dc["errs"],
         chan_mask=dc["mask"], model_index=mi, log10_tau=False, is_toa=True,
         guess=True, guess_weights=dc["gw"], guess_DM=dc["DM"],
-        guess_Ns=nbin, dev=dev)
+        guess_Ns=nbin, dev=dev, guess_ref=1)   # ppalign.py:214-219: at nu_fit
     I = _lib.RESULT_INDEX
     r = res["results"]
     st = r[:, I["status"]].to(torch.int64).cpu().numpy()

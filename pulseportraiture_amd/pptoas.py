@@ -10,11 +10,15 @@ corrections, TOA flags, DeltaDM).  Archive I/O stays on PSRCHIVE via
 
 Reference: /root/reference/pptoas.py (file:line cited per block).
 """
+import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
+import torch
 
 from . import _lib, engine
+from . import dist as _dist
 from . import pplib as _pplib
 from .pplib import (DataBunch, file_is_type, guess_fit_freq, read_model,
                     scattering_alpha, write_TOAs, weighted_mean,
@@ -35,6 +39,115 @@ def load_data(filename, **kwargs):
 def _MJD(days):
     import psrchive as pr
     return pr.MJD(days)
+
+
+def _rank_world():
+    """(rank, world) when torch.distributed runs more than one rank."""
+    if _dist.is_dist():
+        import torch.distributed as tdist
+        return tdist.get_rank(), tdist.get_world_size()
+    return 0, 1
+
+
+_WSTREAMS = {}
+_WLOCK = threading.Lock()
+
+
+def _worker_stream(dev):
+    """The fit worker's own HIP stream (one per device)."""
+    with _WLOCK:
+        if dev.index not in _WSTREAMS:
+            _WSTREAMS[dev.index] = torch.cuda.Stream(dev)
+        return _WSTREAMS[dev.index]
+
+
+class _Staged(object):
+    def __init__(self, t, ev):
+        self.t, self.ev = t, ev
+
+    def wait(self):
+        """The uploaded rows, ordered after the upload on the caller's
+        current stream."""
+        if self.ev is not None:
+            cur = torch.cuda.current_stream(self.t.device)
+            cur.wait_event(self.ev)
+            self.t.record_stream(cur)
+        return self.t
+
+    def release(self):
+        self.t = self.ev = None
+
+
+class _Stager(object):
+    """Host data plane of get_TOAs: an archive's rows are copied into one of
+    two pinned host buffers (float32 when every amplitude survives the round
+    trip, as PSRCHIVE stores them) and uploaded asynchronously on a copy
+    stream, so the upload of archive i+1 overlaps the fit of archive i; a
+    buffer is reused only after its previous upload has completed."""
+
+    def __init__(self):
+        self.bufs, self.events, self.k = [None, None], [None, None], 0
+        self.stream = None
+
+    def stage(self, rows):
+        dev = engine.device()
+        rows = np.asarray(rows)
+        if rows.dtype != np.float32:
+            r32 = rows.astype(np.float32)
+            if np.array_equal(r32, rows):
+                rows = r32
+            else:
+                rows = np.asarray(rows, dtype=np.float64)
+        if rows.size == 0:
+            return _Staged(torch.zeros(rows.shape, dtype=torch.float32,
+                                       device=dev), None)
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        need = rows.nbytes
+        if self.bufs[k] is None or self.bufs[k].numel() < need:
+            self.bufs[k] = torch.empty(need, dtype=torch.uint8,
+                                       pin_memory=True)
+        tdt = torch.float32 if rows.dtype == np.float32 else torch.float64
+        host = self.bufs[k][:need].view(tdt).view(rows.shape)
+        np.copyto(host.numpy(), rows)
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(self.stream):
+            t = host.to(dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.events[k] = ev
+        return _Staged(t, ev)
+
+    def close(self):
+        for ev in self.events:
+            if ev is not None:
+                ev.synchronize()
+        self.bufs, self.events = [None, None], [None, None]
+
+
+def _table_width(nchan):
+    return _lib.RESULT_DOUBLES + 3 * nchan + 25
+
+
+def _pack(res):
+    """One row per sub-int: the result record, scales, scale_errs,
+    channel_snrs and the 5x5 covariance (the table all-gathered across
+    ranks)."""
+    n = res["results"].shape[0]
+    return torch.cat([res["results"], res["scales"], res["scale_errs"],
+                      res["channel_snrs"], res["covariance"].reshape(n, 25)],
+                     dim=1)
+
+
+def _unpack(t, nchan):
+    R = _lib.RESULT_DOUBLES
+    return dict(results=t[:, :R], scales=t[:, R:R + nchan],
+                scale_errs=t[:, R + nchan:R + 2 * nchan],
+                channel_snrs=t[:, R + 2 * nchan:R + 3 * nchan],
+                covariance=t[:, R + 3 * nchan:].reshape(-1, 5, 5))
 
 
 class TOA(object):
@@ -172,364 +285,466 @@ class GetTOAs(object):
         datafiles = self.datafiles if datafile is None else [datafile]
         self.tscrunch = tscrunch
         self.add_instrumental_response = add_instrumental_response
-        fit_flags = None    # carried across sub-ints as in pptoas.py:519-529
-        for iarch, datafile in enumerate(datafiles):
-            fit_duration = 0.0
-            try:
-                data = load_data(datafile, dedisperse=False,
-                                 dededisperse=False, tscrunch=tscrunch,
-                                 pscrunch=True, fscrunch=False,
-                                 rm_baseline=rm_baseline, flux_prof=False,
-                                 refresh_arch=False, return_arch=False,
-                                 quiet=quiet)
-                if data.dmc:
-                    if not quiet:
-                        print("%s is dedispersed (dmc = 1).  Reloading it." %
-                              datafile)
-                    data = load_data(datafile, dedisperse=False,
-                                     dededisperse=True, tscrunch=tscrunch,
-                                     pscrunch=True, fscrunch=False,
-                                     rm_baseline=rm_baseline,
-                                     flux_prof=False, refresh_arch=False,
-                                     return_arch=False, quiet=quiet)
-                if np.isnan(data.prof_SNR) or (data.prof_SNR == 0.0):
-                    print("Profile has a nan or zero  snr, must skip")
+        self._ff = [None]   # fit_flags carried across sub-ints (pptoas.py:519-529)
+        ctx = dict(quiet=quiet, tscrunch=tscrunch, fit_scat=fit_scat,
+                   nu_fit_tuple=nu_fit_tuple, nu_ref_tuple=nu_ref_tuple,
+                   bary=bary, print_phase=print_phase, print_flux=print_flux,
+                   print_parangle=print_parangle,
+                   addtnl_toa_flags=addtnl_toa_flags)
+        # Two-stage pipeline (the host data plane): while the device fits
+        # archive i (a worker thread on its own HIP stream; ppf_fit_batch
+        # releases the GIL), this thread loads archive i+1, builds its batch
+        # and starts its upload from pinned memory on a copy stream; then it
+        # does archive i's bookkeeping.  With torch.distributed initialised
+        # (world > 1), every rank fits a contiguous share of each archive's
+        # sub-ints and the full result tables are all-gathered (dist.py).
+        stager = _Stager()
+        pool = ThreadPoolExecutor(max_workers=1)
+        pending = None
+        try:
+            for iarch, datafile in enumerate(datafiles):
+                job = self._prep_archive(iarch, datafile, ctx, stager)
+                if job is None:
                     continue
-                nnan = len(data.SNRs[np.isnan(data.SNRs)])
-                if nnan > 10:
-                    print("More than 10 frequency channels with nan SNR. "
-                          "Skipping it")
-                    continue
-                if nnan > 0:
-                    print("This file has %s frequency channels with a nan SNR"
-                          % nnan)
-                    print(datafile)
-                    for isub in data.ok_isubs:
-                        for ipol in range(data.npol):
-                            oc = np.array(data.ok_ichans[isub])
-                            data.ok_ichans[isub] = oc[~np.isnan(
-                                data.SNRs[isub, ipol][oc])]
-                if not len(data.ok_isubs):
-                    if not quiet:
-                        print("No subints to fit for %s.  Skipping it." %
-                              datafile)
-                    continue
-                self.ok_idatafiles.append(iarch)
-            except RuntimeError:
+                fut = pool.submit(self._fit_archive, job, ctx)
+                if pending is not None:
+                    self._book_archive(pending[0], pending[1].result(), ctx,
+                                       start)
+                pending = (job, fut)
+            if pending is not None:
+                self._book_archive(pending[0], pending[1].result(), ctx, start)
+        finally:
+            pool.shutdown(wait=True)
+            stager.close()
+
+    # ------------------------------------------------------------------
+    def _prep_archive(self, iarch, datafile, ctx, stager):
+        """Load one archive and build its batch (pptoas.py:258-529); None if
+        the archive is skipped."""
+        quiet, tscrunch, fit_scat = ctx["quiet"], ctx["tscrunch"], \
+            ctx["fit_scat"]
+        nu_fit_tuple, nu_ref_tuple, bary = ctx["nu_fit_tuple"], \
+            ctx["nu_ref_tuple"], ctx["bary"]
+        fit_duration = 0.0
+        try:
+            data = load_data(datafile, dedisperse=False,
+                             dededisperse=False, tscrunch=tscrunch,
+                             pscrunch=True, fscrunch=False,
+                             rm_baseline=rm_baseline, flux_prof=False,
+                             refresh_arch=False, return_arch=False,
+                             quiet=quiet)
+            if data.dmc:
                 if not quiet:
-                    print("Cannot load_data(%s).  Skipping it." % datafile)
-                continue
-            d = data
-            nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
-            if d.source is None:
-                d.source = "noname"
-            obs = DataBunch(telescope=d.telescope, backend=d.backend,
-                            frontend=d.frontend)
-            nu_fits_a = list(np.zeros([nsub, 3], dtype=np.float64))
-            nu_refs_a = list(np.zeros([nsub, 3], dtype=np.float64))
-            phis = np.zeros(nsub)
-            phi_errs = np.zeros(nsub)
-            TOAs = np.zeros(nsub, dtype="object")
-            TOA_errs = np.zeros(nsub, dtype="object")
-            DMs, DM_errs = np.zeros(nsub), np.zeros(nsub)
-            GMs, GM_errs = np.zeros(nsub), np.zeros(nsub)
-            taus, tau_errs = np.zeros(nsub), np.zeros(nsub)
-            alphas, alpha_errs = np.zeros(nsub), np.zeros(nsub)
-            scales = np.zeros([nsub, nchan])
-            scale_errs = np.zeros([nsub, nchan])
-            snrs = np.zeros(nsub)
-            channel_snrs = np.zeros([nsub, nchan])
-            profile_fluxes = np.zeros([nsub, nchan])
-            profile_flux_errs = np.zeros([nsub, nchan])
-            fluxes, flux_errs = np.zeros(nsub), np.zeros(nsub)
-            flux_freqs = np.zeros(nsub)
-            red_chi2s = np.zeros(nsub)
-            covariances = np.zeros([nsub, self.nfit, self.nfit])
-            nfevals = np.zeros(nsub, dtype="int")
-            rcs = np.zeros(nsub, dtype="int")
-            MJDs = np.array([d.epochs[isub].in_days() for isub in range(nsub)],
-                            dtype=np.double)
-            DM_stored = d.DM
-            DM0 = DM_stored if self.DM0 is None else self.DM0
-            if not quiet:
-                print("\nEach of the %d TOAs is approximately %.2f s" % (
-                    len(d.ok_isubs), d.integration_length / nsub))
-            ok_isubs = list(d.ok_isubs)
-            nok = len(ok_isubs)
-            models, model_index = self._models(d, ok_isubs, fit_scat, quiet)
-            # ---- gather the batch (pptoas.py:384-529) --------------------
-            mask = np.zeros((nok, nchan), dtype=np.uint8)
-            init = np.zeros((nok, 5))
-            flags_b = np.zeros((nok, 5), dtype=np.int32)
-            nu_fit_b = np.zeros((nok, 3))
-            nu_out_b = np.full((nok, 3), np.nan)
-            guess_tau = np.zeros(nok)
-            for j, isub in enumerate(ok_isubs):
-                ok = np.asarray(d.ok_ichans[isub], dtype=int)
-                mask[j, ok] = 1
-                freqsx = d.freqs[isub, ok]
-                SNRsx = d.SNRs[isub, 0, ok]
-                P = d.Ps[isub]
-                if nu_fit_tuple is None:
-                    nu_fit = guess_fit_freq(freqsx, SNRsx)
-                    nu_fit_DM = nu_fit_GM = nu_fit_tau = nu_fit
-                else:
-                    nu_fit_DM = nu_fit_GM = nu_fit_tuple[0]
-                    nu_fit_tau = nu_fit_tuple[-1]
-                nu_fits_a[isub] = [nu_fit_DM, nu_fit_GM, nu_fit_tau]
-                nu_fit_b[j] = nu_fits_a[isub]
-                if nu_ref_tuple is None:
-                    nu_ref_DM = nu_ref_GM = nu_ref_tau = None
-                else:
-                    nu_ref_DM = nu_ref_GM = nu_ref_tuple[0]
-                    nu_ref_tau = nu_ref_tuple[-1]
-                    if bary and nu_ref_tau:
-                        nu_ref_tau /= d.doppler_factors[isub]
-                nu_refs_a[isub] = [nu_ref_DM, nu_ref_GM, nu_ref_tau]
-                nu_out_b[j] = [np.nan if v is None else v for v in
-                               nu_refs_a[isub]]
-                tau_guess = alpha_guess = 0.0
-                if fit_scat:
-                    if self.scat_guess is not None:
-                        tg_s, tg_ref, alpha_guess = self.scat_guess
-                        tau_guess = (tg_s / P) * (nu_fit_tau / tg_ref) ** \
-                            alpha_guess
-                    else:
-                        alpha_guess = self.alpha if hasattr(self, "alpha") \
-                            else scattering_alpha
-                        tau_guess = (self.gparams[1] / P) * (
-                            nu_fit_tau / self.model_nu_ref) ** alpha_guess \
-                            if hasattr(self, "gparams") else 0.0
-                    guess_tau[j] = tau_guess
-                    if self.log10_tau:
-                        if tau_guess == 0.0:
-                            tau_guess = nbin ** -1
-                        tau_guess = np.log10(tau_guess)
-                init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
-                if len(freqsx) == 1:
-                    fit_flags = [1, 0, 0, 0, 0]
-                    if not quiet:
-                        print("TOA #%d only has 1 frequency channel...fitting "
-                              "for phase only..." % (j + 1))
-                elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
-                    if fit_flags is None:
-                        raise UnboundLocalError(
-                            "local variable 'fit_flags' referenced before "
-                            "assignment (pptoas.py:525)")
-                    fit_flags = list(fit_flags)
-                    fit_flags[2] = 0
-                else:
-                    fit_flags = list(np.copy(self.fit_flags))
-                flags_b[j] = fit_flags
-            data_rows = np.asarray(d.subints)[ok_isubs, 0]
-            d32 = data_rows.astype(np.float32)
-            if np.array_equal(d32.astype(np.float64), data_rows):
-                data_rows = d32      # PSRCHIVE amplitudes are float32
-            t_fit = time.time()
-            res = engine.fit_batch(
-                data_rows, models, d.freqs[ok_isubs], d.Ps[ok_isubs], init,
-                flags_b, nu_fits=nu_fit_b, nu_outs=nu_out_b,
-                errs=np.asarray(d.noise_stds)[ok_isubs, 0],
-                chan_mask=mask, model_index=model_index,
-                log10_tau=self.log10_tau, option=0, is_toa=True, guess=True,
-                guess_weights=np.asarray(d.weights)[ok_isubs],
-                guess_DM=np.full(nok, DM_stored), guess_Ns=100,
-                guess_tau=guess_tau if fit_scat else None)
-            r = engine.results_numpy(res)
-            batch_duration = time.time() - t_fit
-            # ---- per-sub-integration bookkeeping (pptoas.py:567-711) -----
-            for j, isub in enumerate(ok_isubs):
-                fit_flags_j = [int(v) for v in flags_b[j]]
-                ok = mask[j].astype(bool)
-                R = r["results"][j]
-                status = int(R[_lib.RESULT_INDEX["status"]])
-                _nu_zero_messages(fit_flags_j, nu_refs_a[isub])
-                _raise_status(status)
-                if (status & 0xff) not in (0, 1, 2, 4):
-                    _status_message(status & 0xff, datafile + "_%d" % isub)
-                results = unpack_result(
-                    R, r["scales"][j][ok], r["scale_errs"][j][ok],
-                    r["channel_snrs"][j][ok], r["covariance"][j], fit_flags_j,
-                    batch_duration / nok)
-                fit_duration += results.duration
-                P = d.Ps[isub]
-                epoch = d.epochs[isub]
-                results.TOA = epoch + _MJD((results.phi * P + d.backend_delay)
-                                           / (3600 * 24.))
-                results.TOA_err = results.phi_err * P * 1e6
-                if self.bary:
-                    df = d.doppler_factors[isub]
-                    if fit_flags_j[1]:
-                        results.DM *= df
-                    if fit_flags_j[2]:
-                        results.GM *= df ** 3
-                else:
-                    df = 1.0
-                freqsx = d.freqs[isub, ok]
-                if print_flux:
-                    modelx = models[model_index[j]][ok]
-                    if results.tau != 0.0:
-                        tau = 10 ** results.tau if self.log10_tau else \
-                            results.tau
-                        scat_model = np.fft.irfft(scattering_portrait_FT(
-                            scattering_times(tau, results.alpha, freqsx,
-                                             results.nu_tau), nbin) *
-                            np.fft.rfft(modelx, axis=1), axis=1)
-                    else:
-                        scat_model = np.copy(modelx)
-                    smm = scat_model.mean(axis=1)
-                    profile_fluxes[isub, ok] = smm * results.scales
-                    profile_flux_errs[isub, ok] = abs(smm) * results.scale_errs
-                    flux, flux_err = weighted_mean(profile_fluxes[isub, ok],
-                                                   profile_flux_errs[isub, ok])
-                    flux_freq, _ = weighted_mean(freqsx,
-                                                 profile_flux_errs[isub, ok])
-                    fluxes[isub], flux_errs[isub] = flux, flux_err
-                    flux_freqs[isub] = flux_freq
-                nu_refs_a[isub] = [results.nu_DM, results.nu_GM,
-                                   results.nu_tau]
-                phis[isub], phi_errs[isub] = results.phi, results.phi_err
-                TOAs[isub], TOA_errs[isub] = results.TOA, results.TOA_err
-                DMs[isub], DM_errs[isub] = results.DM, results.DM_err
-                GMs[isub], GM_errs[isub] = results.GM, results.GM_err
-                taus[isub], tau_errs[isub] = results.tau, results.tau_err
-                alphas[isub], alpha_errs[isub] = results.alpha, \
-                    results.alpha_err
-                nfevals[isub], rcs[isub] = results.nfeval, results.return_code
-                scales[isub, ok] = results.scales
-                scale_errs[isub, ok] = results.scale_errs
-                snrs[isub] = results.snr
-                channel_snrs[isub, ok] = results.channel_snrs
-                try:
-                    covariances[isub] = results.covariance_matrix
-                except ValueError:
-                    ifit = np.where(fit_flags_j)[0]
-                    for ii, a in enumerate(ifit):
-                        for jj, b in enumerate(ifit):
-                            covariances[isub][a, b] = \
-                                results.covariance_matrix[ii, jj]
-                red_chi2s[isub] = results.red_chi2
-                toa_flags = {}
-                if not fit_flags_j[1]:
-                    results.DM = None
-                    results.DM_err = None
-                if fit_flags_j[2]:
-                    toa_flags["gm"] = results.GM
-                    toa_flags["gm_err"] = results.GM_err
-                if fit_flags_j[3]:
-                    if self.log10_tau:
-                        toa_flags["scat_time"] = 10 ** results.tau * P / df * 1e6
-                        toa_flags["log10_scat_time"] = results.tau + \
-                            np.log10(P / df)
-                        toa_flags["log10_scat_time_err"] = results.tau_err
-                    else:
-                        toa_flags["scat_time"] = results.tau * P / df * 1e6
-                        toa_flags["scat_time_err"] = results.tau_err * P / df \
-                            * 1e6
-                    toa_flags["scat_ref_freq"] = results.nu_tau * df
-                    toa_flags["scat_ind"] = results.alpha
-                if fit_flags_j[4]:
-                    toa_flags["scat_ind_err"] = results.alpha_err
-                toa_flags["be"] = d.backend
-                toa_flags["fe"] = d.frontend
-                toa_flags["f"] = d.frontend + "_" + d.backend
-                toa_flags["nbin"] = nbin
-                toa_flags["nch"] = nchan
-                toa_flags["nchx"] = len(freqsx)
-                toa_flags["bw"] = freqsx.max() - freqsx.min()
-                toa_flags["chbw"] = abs(d.bw) / nchan
-                toa_flags["subint"] = isub
-                toa_flags["tobs"] = d.subtimes[isub]
-                toa_flags["fratio"] = freqsx.max() / freqsx.min()
-                toa_flags["tmplt"] = self.modelfile
-                toa_flags["snr"] = results.snr
-                if nu_ref_tuple is not None and np.all(fit_flags_j[:2]):
-                    toa_flags["phi_DM_cov"] = results.covariance_matrix[0, 1]
-                toa_flags["gof"] = results.red_chi2
-                if print_phase:
-                    toa_flags["phs"] = results.phi
-                    toa_flags["phs_err"] = results.phi_err
-                if print_flux:
-                    toa_flags["flux"] = fluxes[isub]
-                    toa_flags["flux_err"] = flux_errs[isub]
-                    toa_flags["flux_ref_freq"] = flux_freqs[isub]
-                if print_parangle:
-                    toa_flags["par_angle"] = d.parallactic_angles[isub]
-                for k, v in addtnl_toa_flags.items():
-                    toa_flags[k] = v
-                self.TOA_list.append(TOA(datafile, results.nu_DM, results.TOA,
-                                         results.TOA_err, d.telescope,
-                                         d.telescope_code, results.DM,
-                                         results.DM_err, toa_flags))
-            # ---- DeltaDM (pptoas.py:713-729) ------------------------------
-            DeltaDMs = DMs - DM0
-            oks = np.asarray(d.ok_isubs)
-            if np.all(DM_errs[oks]):
-                DM_weights = DM_errs[oks] ** -2
-            else:
-                DM_weights = np.ones(len(DM_errs[oks]))
-            DeltaDM_mean, DeltaDM_var = np.average(DeltaDMs[oks],
-                                                   weights=DM_weights,
-                                                   returned=True)
-            DeltaDM_var = DeltaDM_var ** -1
-            if len(oks) > 1:
-                DeltaDM_var *= np.sum(((DeltaDMs[oks] - DeltaDM_mean) ** 2) *
-                                      DM_weights) / (len(DeltaDMs[oks]) - 1)
-            DeltaDM_err = DeltaDM_var ** 0.5
-            self.order.append(datafile)
-            self.obs.append(obs)
-            self.doppler_fs.append(d.doppler_factors)
-            self.nu0s.append(d.nu0)
-            self.nu_fits.append(nu_fits_a)
-            self.nu_refs.append(nu_refs_a)
-            self.ok_isubs.append(d.ok_isubs)
-            self.epochs.append(d.epochs)
-            self.MJDs.append(MJDs)
-            self.Ps.append(d.Ps)
-            self.phis.append(phis)
-            self.phi_errs.append(phi_errs)
-            self.TOAs.append(TOAs)
-            self.TOA_errs.append(TOA_errs)
-            self.DM0s.append(DM0)
-            self.DMs.append(DMs)
-            self.DM_errs.append(DM_errs)
-            self.DeltaDM_means.append(DeltaDM_mean)
-            self.DeltaDM_errs.append(DeltaDM_err)
-            self.GMs.append(GMs)
-            self.GM_errs.append(GM_errs)
-            self.taus.append(taus)
-            self.tau_errs.append(tau_errs)
-            self.alphas.append(alphas)
-            self.alpha_errs.append(alpha_errs)
-            self.scales.append(scales)
-            self.scale_errs.append(scale_errs)
-            self.snrs.append(snrs)
-            self.channel_snrs.append(channel_snrs)
-            self.profile_fluxes.append(profile_fluxes)
-            self.profile_flux_errs.append(profile_flux_errs)
-            self.fluxes.append(fluxes)
-            self.flux_errs.append(flux_errs)
-            self.flux_freqs.append(flux_freqs)
-            self.covariances.append(covariances)
-            self.red_chi2s.append(red_chi2s)
-            self.nfevals.append(nfevals)
-            self.rcs.append(rcs)
-            self.fit_durations.append(fit_duration)
-            if not quiet:
-                print("--------------------------")
+                    print("%s is dedispersed (dmc = 1).  Reloading it." %
+                          datafile)
+                data = load_data(datafile, dedisperse=False,
+                                 dededisperse=True, tscrunch=tscrunch,
+                                 pscrunch=True, fscrunch=False,
+                                 rm_baseline=rm_baseline,
+                                 flux_prof=False, refresh_arch=False,
+                                 return_arch=False, quiet=quiet)
+            if np.isnan(data.prof_SNR) or (data.prof_SNR == 0.0):
+                print("Profile has a nan or zero  snr, must skip")
+                return None
+            nnan = len(data.SNRs[np.isnan(data.SNRs)])
+            if nnan > 10:
+                print("More than 10 frequency channels with nan SNR. "
+                      "Skipping it")
+                return None
+            if nnan > 0:
+                print("This file has %s frequency channels with a nan SNR"
+                      % nnan)
                 print(datafile)
-                print("~%.4f sec/TOA" % (fit_duration / len(d.ok_isubs)))
-                print("Med. TOA error is %.3f us" % (np.median(
-                    phi_errs[oks]) * d.Ps.mean() * 1e6))
-            tot_duration = time.time() - start
-            if not quiet and len(self.ok_isubs):
-                print("--------------------------")
-                print("Total time: %.2f sec, ~%.4f sec/TOA" % (
-                    tot_duration,
-                    tot_duration / np.array(list(map(len, self.ok_isubs))
-                                            ).sum()))
-        if not already_warned:
-            pass
+                for isub in data.ok_isubs:
+                    for ipol in range(data.npol):
+                        oc = np.array(data.ok_ichans[isub])
+                        data.ok_ichans[isub] = oc[~np.isnan(
+                            data.SNRs[isub, ipol][oc])]
+            if not len(data.ok_isubs):
+                if not quiet:
+                    print("No subints to fit for %s.  Skipping it." %
+                          datafile)
+                return None
+            self.ok_idatafiles.append(iarch)
+        except RuntimeError:
+            if not quiet:
+                print("Cannot load_data(%s).  Skipping it." % datafile)
+            return None
+        d = data
+        nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
+        if d.source is None:
+            d.source = "noname"
+        obs = DataBunch(telescope=d.telescope, backend=d.backend,
+                        frontend=d.frontend)
+        nu_fits_a = list(np.zeros([nsub, 3], dtype=np.float64))
+        nu_refs_a = list(np.zeros([nsub, 3], dtype=np.float64))
+        MJDs = np.array([d.epochs[isub].in_days() for isub in range(nsub)],
+                        dtype=np.double)
+        DM_stored = d.DM
+        DM0 = DM_stored if self.DM0 is None else self.DM0
+        if not quiet:
+            print("\nEach of the %d TOAs is approximately %.2f s" % (
+                len(d.ok_isubs), d.integration_length / nsub))
+        ok_isubs = list(d.ok_isubs)
+        nok = len(ok_isubs)
+        models, model_index = self._models(d, ok_isubs, fit_scat, quiet)
+        # ---- gather the batch (pptoas.py:384-529) --------------------
+        mask = np.zeros((nok, nchan), dtype=np.uint8)
+        init = np.zeros((nok, 5))
+        flags_b = np.zeros((nok, 5), dtype=np.int32)
+        nu_fit_b = np.zeros((nok, 3))
+        nu_out_b = np.full((nok, 3), np.nan)
+        guess_tau = np.zeros(nok)
+        for j, isub in enumerate(ok_isubs):
+            ok = np.asarray(d.ok_ichans[isub], dtype=int)
+            mask[j, ok] = 1
+            freqsx = d.freqs[isub, ok]
+            SNRsx = d.SNRs[isub, 0, ok]
+            P = d.Ps[isub]
+            if nu_fit_tuple is None:
+                nu_fit = guess_fit_freq(freqsx, SNRsx)
+                nu_fit_DM = nu_fit_GM = nu_fit_tau = nu_fit
+            else:
+                nu_fit_DM = nu_fit_GM = nu_fit_tuple[0]
+                nu_fit_tau = nu_fit_tuple[-1]
+            nu_fits_a[isub] = [nu_fit_DM, nu_fit_GM, nu_fit_tau]
+            nu_fit_b[j] = nu_fits_a[isub]
+            if nu_ref_tuple is None:
+                nu_ref_DM = nu_ref_GM = nu_ref_tau = None
+            else:
+                nu_ref_DM = nu_ref_GM = nu_ref_tuple[0]
+                nu_ref_tau = nu_ref_tuple[-1]
+                if bary and nu_ref_tau:
+                    nu_ref_tau /= d.doppler_factors[isub]
+            nu_refs_a[isub] = [nu_ref_DM, nu_ref_GM, nu_ref_tau]
+            nu_out_b[j] = [np.nan if v is None else v for v in
+                           nu_refs_a[isub]]
+            tau_guess = alpha_guess = 0.0
+            if fit_scat:
+                if self.scat_guess is not None:
+                    tg_s, tg_ref, alpha_guess = self.scat_guess
+                    tau_guess = (tg_s / P) * (nu_fit_tau / tg_ref) ** \
+                        alpha_guess
+                else:
+                    alpha_guess = self.alpha if hasattr(self, "alpha") \
+                        else scattering_alpha
+                    tau_guess = (self.gparams[1] / P) * (
+                        nu_fit_tau / self.model_nu_ref) ** alpha_guess \
+                        if hasattr(self, "gparams") else 0.0
+                guess_tau[j] = tau_guess
+                if self.log10_tau:
+                    if tau_guess == 0.0:
+                        tau_guess = nbin ** -1
+                    tau_guess = np.log10(tau_guess)
+            init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
+            if len(freqsx) == 1:
+                fit_flags = [1, 0, 0, 0, 0]
+                if not quiet:
+                    print("TOA #%d only has 1 frequency channel...fitting "
+                          "for phase only..." % (j + 1))
+            elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
+                if fit_flags is None:
+                    raise UnboundLocalError(
+                        "local variable 'fit_flags' referenced before "
+                        "assignment (pptoas.py:525)")
+                fit_flags = list(fit_flags)
+                fit_flags[2] = 0
+            else:
+                fit_flags = list(np.copy(self.fit_flags))
+            flags_b[j] = fit_flags
+        rank, world = _rank_world()
+        first, count = _dist.shard(nok, rank, world)
+        rows = np.asarray(d.subints)[ok_isubs[first:first + count], 0] \
+            if count else np.zeros((0, nchan, nbin))
+        return dict(iarch=iarch, datafile=datafile, d=d, nsub=nsub,
+                    dev=engine.device(),
+                    nchan=nchan, nbin=nbin, obs=obs, nu_fits_a=nu_fits_a,
+                    nu_refs_a=nu_refs_a, MJDs=MJDs, DM_stored=DM_stored,
+                    DM0=DM0, ok_isubs=ok_isubs, nok=nok, models=models,
+                    model_index=model_index, mask=mask, init=init,
+                    flags_b=flags_b, nu_fit_b=nu_fit_b, nu_out_b=nu_out_b,
+                    guess_tau=guess_tau, first=first, count=count,
+                    world=world, staged=stager.stage(rows),
+                    fit_duration=fit_duration)
+
+    def _fit_archive(self, job, ctx):
+        """Device stage (worker thread): this rank's share of the archive's
+        sub-ints in ONE ppf_fit_batch (guess + fit + post-fit), the result
+        tables all-gathered over ranks; returns numpy tables."""
+        d, nok, first, count = job["d"], job["nok"], job["first"], \
+            job["count"]
+        sl = slice(first, first + count)
+        isubs = job["ok_isubs"][sl]
+        nchan = job["nchan"]
+        t_fit = time.time()
+        dev = job["dev"]
+        nccl = _dist.backend() == "nccl"
+        with torch.cuda.device(dev), torch.cuda.stream(_worker_stream(dev)):
+            data_t = job["staged"].wait()
+            err = None
+            try:
+                table = self._fit_share(job, ctx, data_t, isubs, sl, dev)
+            except Exception as exc:        # every rank raises, below
+                if job["world"] == 1:
+                    raise
+                err = exc
+            if job["world"] > 1:
+                # a failed rank must not leave the others in the all-gather
+                _dist.raise_if_any_failed(err, dev if nccl else None)
+                table = _dist.allgather_rows(table if nccl else table.cpu(),
+                                             nok, job["world"])
+            r = _unpack(table.cpu().numpy(), nchan)
+        job["staged"].release()
+        r["batch_duration"] = time.time() - t_fit
+        return r
+
+    def _fit_share(self, job, ctx, data_t, isubs, sl, dev):
+        """One ppf_fit_batch over this rank's sub-ints -> packed table."""
+        d, count, nchan = job["d"], job["count"], job["nchan"]
+        if not count:
+            return torch.zeros((0, _table_width(nchan)), dtype=torch.float64,
+                               device=dev)
+        res = engine.fit_batch(
+            data_t, job["models"], d.freqs[isubs], d.Ps[isubs],
+            job["init"][sl], job["flags_b"][sl], nu_fits=job["nu_fit_b"][sl],
+            nu_outs=job["nu_out_b"][sl],
+            errs=np.asarray(d.noise_stds)[isubs, 0],
+            chan_mask=job["mask"][sl], model_index=job["model_index"][sl],
+            log10_tau=self.log10_tau, option=0, is_toa=True, guess=True,
+            guess_weights=np.asarray(d.weights)[isubs],
+            guess_DM=np.full(count, job["DM_stored"]), guess_Ns=100,
+            guess_tau=job["guess_tau"][sl] if ctx["fit_scat"] else None,
+            dev=dev)
+        return _pack(res)
+
+    def _book_archive(self, job, r, ctx, start):
+        """Per-sub-integration host bookkeeping (pptoas.py:567-792)."""
+        quiet = ctx["quiet"]
+        print_phase, print_flux = ctx["print_phase"], ctx["print_flux"]
+        print_parangle = ctx["print_parangle"]
+        addtnl_toa_flags = ctx["addtnl_toa_flags"]
+        nu_ref_tuple = ctx["nu_ref_tuple"]
+        d, datafile = job["d"], job["datafile"]
+        nsub, nchan, nbin = job["nsub"], job["nchan"], job["nbin"]
+        obs, nu_fits_a, nu_refs_a = job["obs"], job["nu_fits_a"], \
+            job["nu_refs_a"]
+        MJDs, DM0 = job["MJDs"], job["DM0"]
+        ok_isubs, nok = job["ok_isubs"], job["nok"]
+        models, model_index = job["models"], job["model_index"]
+        mask, flags_b = job["mask"], job["flags_b"]
+        fit_duration = job["fit_duration"]
+        batch_duration = r["batch_duration"]
+        phis = np.zeros(nsub)
+        phi_errs = np.zeros(nsub)
+        TOAs = np.zeros(nsub, dtype="object")
+        TOA_errs = np.zeros(nsub, dtype="object")
+        DMs, DM_errs = np.zeros(nsub), np.zeros(nsub)
+        GMs, GM_errs = np.zeros(nsub), np.zeros(nsub)
+        taus, tau_errs = np.zeros(nsub), np.zeros(nsub)
+        alphas, alpha_errs = np.zeros(nsub), np.zeros(nsub)
+        scales = np.zeros([nsub, nchan])
+        scale_errs = np.zeros([nsub, nchan])
+        snrs = np.zeros(nsub)
+        channel_snrs = np.zeros([nsub, nchan])
+        profile_fluxes = np.zeros([nsub, nchan])
+        profile_flux_errs = np.zeros([nsub, nchan])
+        fluxes, flux_errs = np.zeros(nsub), np.zeros(nsub)
+        flux_freqs = np.zeros(nsub)
+        red_chi2s = np.zeros(nsub)
+        covariances = np.zeros([nsub, self.nfit, self.nfit])
+        nfevals = np.zeros(nsub, dtype="int")
+        rcs = np.zeros(nsub, dtype="int")
+        # ---- per-sub-integration bookkeeping (pptoas.py:567-711) -----
+        for j, isub in enumerate(ok_isubs):
+            fit_flags_j = [int(v) for v in flags_b[j]]
+            ok = mask[j].astype(bool)
+            R = r["results"][j]
+            status = int(R[_lib.RESULT_INDEX["status"]])
+            _nu_zero_messages(fit_flags_j, nu_refs_a[isub])
+            _raise_status(status)
+            if (status & 0xff) not in (0, 1, 2, 4):
+                _status_message(status & 0xff, datafile + "_%d" % isub)
+            results = unpack_result(
+                R, r["scales"][j][ok], r["scale_errs"][j][ok],
+                r["channel_snrs"][j][ok], r["covariance"][j], fit_flags_j,
+                batch_duration / nok)
+            fit_duration += results.duration
+            P = d.Ps[isub]
+            epoch = d.epochs[isub]
+            results.TOA = epoch + _MJD((results.phi * P + d.backend_delay)
+                                       / (3600 * 24.))
+            results.TOA_err = results.phi_err * P * 1e6
+            if self.bary:
+                df = d.doppler_factors[isub]
+                if fit_flags_j[1]:
+                    results.DM *= df
+                if fit_flags_j[2]:
+                    results.GM *= df ** 3
+            else:
+                df = 1.0
+            freqsx = d.freqs[isub, ok]
+            if print_flux:
+                modelx = models[model_index[j]][ok]
+                if results.tau != 0.0:
+                    tau = 10 ** results.tau if self.log10_tau else \
+                        results.tau
+                    scat_model = np.fft.irfft(scattering_portrait_FT(
+                        scattering_times(tau, results.alpha, freqsx,
+                                         results.nu_tau), nbin) *
+                        np.fft.rfft(modelx, axis=1), axis=1)
+                else:
+                    scat_model = np.copy(modelx)
+                smm = scat_model.mean(axis=1)
+                profile_fluxes[isub, ok] = smm * results.scales
+                profile_flux_errs[isub, ok] = abs(smm) * results.scale_errs
+                flux, flux_err = weighted_mean(profile_fluxes[isub, ok],
+                                               profile_flux_errs[isub, ok])
+                flux_freq, _ = weighted_mean(freqsx,
+                                             profile_flux_errs[isub, ok])
+                fluxes[isub], flux_errs[isub] = flux, flux_err
+                flux_freqs[isub] = flux_freq
+            nu_refs_a[isub] = [results.nu_DM, results.nu_GM,
+                               results.nu_tau]
+            phis[isub], phi_errs[isub] = results.phi, results.phi_err
+            TOAs[isub], TOA_errs[isub] = results.TOA, results.TOA_err
+            DMs[isub], DM_errs[isub] = results.DM, results.DM_err
+            GMs[isub], GM_errs[isub] = results.GM, results.GM_err
+            taus[isub], tau_errs[isub] = results.tau, results.tau_err
+            alphas[isub], alpha_errs[isub] = results.alpha, \
+                results.alpha_err
+            nfevals[isub], rcs[isub] = results.nfeval, results.return_code
+            scales[isub, ok] = results.scales
+            scale_errs[isub, ok] = results.scale_errs
+            snrs[isub] = results.snr
+            channel_snrs[isub, ok] = results.channel_snrs
+            try:
+                covariances[isub] = results.covariance_matrix
+            except ValueError:
+                ifit = np.where(fit_flags_j)[0]
+                for ii, a in enumerate(ifit):
+                    for jj, b in enumerate(ifit):
+                        covariances[isub][a, b] = \
+                            results.covariance_matrix[ii, jj]
+            red_chi2s[isub] = results.red_chi2
+            toa_flags = {}
+            if not fit_flags_j[1]:
+                results.DM = None
+                results.DM_err = None
+            if fit_flags_j[2]:
+                toa_flags["gm"] = results.GM
+                toa_flags["gm_err"] = results.GM_err
+            if fit_flags_j[3]:
+                if self.log10_tau:
+                    toa_flags["scat_time"] = 10 ** results.tau * P / df * 1e6
+                    toa_flags["log10_scat_time"] = results.tau + \
+                        np.log10(P / df)
+                    toa_flags["log10_scat_time_err"] = results.tau_err
+                else:
+                    toa_flags["scat_time"] = results.tau * P / df * 1e6
+                    toa_flags["scat_time_err"] = results.tau_err * P / df \
+                        * 1e6
+                toa_flags["scat_ref_freq"] = results.nu_tau * df
+                toa_flags["scat_ind"] = results.alpha
+            if fit_flags_j[4]:
+                toa_flags["scat_ind_err"] = results.alpha_err
+            toa_flags["be"] = d.backend
+            toa_flags["fe"] = d.frontend
+            toa_flags["f"] = d.frontend + "_" + d.backend
+            toa_flags["nbin"] = nbin
+            toa_flags["nch"] = nchan
+            toa_flags["nchx"] = len(freqsx)
+            toa_flags["bw"] = freqsx.max() - freqsx.min()
+            toa_flags["chbw"] = abs(d.bw) / nchan
+            toa_flags["subint"] = isub
+            toa_flags["tobs"] = d.subtimes[isub]
+            toa_flags["fratio"] = freqsx.max() / freqsx.min()
+            toa_flags["tmplt"] = self.modelfile
+            toa_flags["snr"] = results.snr
+            if nu_ref_tuple is not None and np.all(fit_flags_j[:2]):
+                toa_flags["phi_DM_cov"] = results.covariance_matrix[0, 1]
+            toa_flags["gof"] = results.red_chi2
+            if print_phase:
+                toa_flags["phs"] = results.phi
+                toa_flags["phs_err"] = results.phi_err
+            if print_flux:
+                toa_flags["flux"] = fluxes[isub]
+                toa_flags["flux_err"] = flux_errs[isub]
+                toa_flags["flux_ref_freq"] = flux_freqs[isub]
+            if print_parangle:
+                toa_flags["par_angle"] = d.parallactic_angles[isub]
+            for k, v in addtnl_toa_flags.items():
+                toa_flags[k] = v
+            self.TOA_list.append(TOA(datafile, results.nu_DM, results.TOA,
+                                     results.TOA_err, d.telescope,
+                                     d.telescope_code, results.DM,
+                                     results.DM_err, toa_flags))
+        # ---- DeltaDM (pptoas.py:713-729) ------------------------------
+        DeltaDMs = DMs - DM0
+        oks = np.asarray(d.ok_isubs)
+        if np.all(DM_errs[oks]):
+            DM_weights = DM_errs[oks] ** -2
+        else:
+            DM_weights = np.ones(len(DM_errs[oks]))
+        DeltaDM_mean, DeltaDM_var = np.average(DeltaDMs[oks],
+                                               weights=DM_weights,
+                                               returned=True)
+        DeltaDM_var = DeltaDM_var ** -1
+        if len(oks) > 1:
+            DeltaDM_var *= np.sum(((DeltaDMs[oks] - DeltaDM_mean) ** 2) *
+                                  DM_weights) / (len(DeltaDMs[oks]) - 1)
+        DeltaDM_err = DeltaDM_var ** 0.5
+        self.order.append(datafile)
+        self.obs.append(obs)
+        self.doppler_fs.append(d.doppler_factors)
+        self.nu0s.append(d.nu0)
+        self.nu_fits.append(nu_fits_a)
+        self.nu_refs.append(nu_refs_a)
+        self.ok_isubs.append(d.ok_isubs)
+        self.epochs.append(d.epochs)
+        self.MJDs.append(MJDs)
+        self.Ps.append(d.Ps)
+        self.phis.append(phis)
+        self.phi_errs.append(phi_errs)
+        self.TOAs.append(TOAs)
+        self.TOA_errs.append(TOA_errs)
+        self.DM0s.append(DM0)
+        self.DMs.append(DMs)
+        self.DM_errs.append(DM_errs)
+        self.DeltaDM_means.append(DeltaDM_mean)
+        self.DeltaDM_errs.append(DeltaDM_err)
+        self.GMs.append(GMs)
+        self.GM_errs.append(GM_errs)
+        self.taus.append(taus)
+        self.tau_errs.append(tau_errs)
+        self.alphas.append(alphas)
+        self.alpha_errs.append(alpha_errs)
+        self.scales.append(scales)
+        self.scale_errs.append(scale_errs)
+        self.snrs.append(snrs)
+        self.channel_snrs.append(channel_snrs)
+        self.profile_fluxes.append(profile_fluxes)
+        self.profile_flux_errs.append(profile_flux_errs)
+        self.fluxes.append(fluxes)
+        self.flux_errs.append(flux_errs)
+        self.flux_freqs.append(flux_freqs)
+        self.covariances.append(covariances)
+        self.red_chi2s.append(red_chi2s)
+        self.nfevals.append(nfevals)
+        self.rcs.append(rcs)
+        self.fit_durations.append(fit_duration)
+        if not quiet:
+            print("--------------------------")
+            print(datafile)
+            print("~%.4f sec/TOA" % (fit_duration / len(d.ok_isubs)))
+            print("Med. TOA error is %.3f us" % (np.median(
+                phi_errs[oks]) * d.Ps.mean() * 1e6))
+        tot_duration = time.time() - start
+        if not quiet and len(self.ok_isubs):
+            print("--------------------------")
+            print("Total time: %.2f sec, ~%.4f sec/TOA" % (
+                tot_duration,
+                tot_duration / np.array(list(map(len, self.ok_isubs))
+                                        ).sum()))
 
     def get_narrowband_TOAs(self, datafile=None, tscrunch=False,
                             fit_scat=False, log10_tau=True, scat_guess=None,

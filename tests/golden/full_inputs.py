@@ -143,7 +143,13 @@ def align_inputs(c):
         arch.append(dict(subints=subs, weights=weights))
     tn = c.get("tmpl_nchan", nchan)
     tfreqs = S.channel_freqs(tn)
-    prof = S.f32(arch[0]["subints"].mean(axis=(0, 1)))
+    # initial template as in the reference's notebook (make_constant_portrait
+    # with DataPortrait.prof): archive 0's mean profile, dedispersed at DM0
+    # to the band centre, tiled over the template's channels
+    ded = S.rotate(arch[0]["subints"].reshape(-1, nbin),
+                   np.tile(S.DCONST * S.DM0 * (freqs ** -2 - 1500.0 ** -2) /
+                           S.P0, nsub))
+    prof = S.f32(ded.mean(axis=0))
     guess = np.tile(prof, (tn, 1))
     return arch, guess, freqs, tfreqs
 

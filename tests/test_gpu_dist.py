@@ -1,0 +1,100 @@
+"""Multi-rank GetTOAs on the GPU: two ranks (one process each, both on the
+box's one GPU, collectives over gloo) shard every archive's sub-ints
+(pptoas.py:258, 384) and all-gather the full result tables (results,
+scales, scale_errs, channel_snrs, covariance); the sharded run's tables and
+.tim lines are bit-identical to the serial run's."""
+import io
+import os
+import socket
+import contextlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+KEYS = ("phis", "phi_errs", "DMs", "DM_errs", "red_chi2s", "snrs", "scales",
+        "scale_errs", "channel_snrs", "covariances", "nfevals", "rcs",
+        "DeltaDM_means", "DeltaDM_errs", "nu_refs")
+
+
+def run_gettoas(name):
+    """GetTOAs.get_TOAs over the golden archive set `name`; returns the
+    attribute tables and the .tim lines."""
+    import sys
+    sys.path[:0] = [os.path.dirname(HERE), HERE]
+    import test_gpu_fullshape as T
+    from pulseportraiture_amd import pptoas, pplib
+    c, files, gm = T._archives(name)
+    saved = pptoas.load_data, pptoas._MJD
+    pptoas.load_data = lambda fn, **kw: files[fn]
+    pptoas._MJD = T._MJD
+    try:
+        return _gettoas(pptoas, pplib, c, files, gm)
+    finally:
+        pptoas.load_data, pptoas._MJD = saved
+
+
+def _gettoas(pptoas, pplib, c, files, gm):
+    gt = pptoas.GetTOAs.__new__(pptoas.GetTOAs)
+    for a in pptoas._ATTRS:
+        setattr(gt, a, [])
+    gt.datafiles = list(files)
+    gt.is_FITS_model = False
+    gt.modelfile = gm
+    gt.instrumental_response_dict = gt.ird = {"DM": 0.0, "wids": [],
+                                              "irf_types": []}
+    gt.quiet = True
+    gt.get_TOAs(quiet=True, DM0=float(c["DM0"]) if int(c["DM0_given"])
+                else None)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        pplib.write_TOAs(gt.TOA_list)
+    tabs = {k: np.array(getattr(gt, k), dtype=np.float64) for k in KEYS}
+    return tabs, buf.getvalue().splitlines()
+
+
+def _rank(rank, world, port, name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import sys
+    sys.path[:0] = [os.path.dirname(HERE), HERE]
+    import torch.distributed as dist
+    from pulseportraiture_amd import dist as pdist
+    pdist.init("gloo")
+    tabs, lines = run_gettoas(name)
+    if rank == 0:
+        q.put((tabs, lines))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_sharded_gettoas_equals_serial(name):
+    import torch.multiprocessing as mp
+    serial, lines = run_gettoas(name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, name, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    tabs, slines = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for k in KEYS:
+        np.testing.assert_array_equal(tabs[k], serial[k], err_msg=k)
+    assert slines == lines

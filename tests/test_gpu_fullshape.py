@@ -321,7 +321,10 @@ def test_c4_bench_iteration_matches_oracle():
         nu_fit=np.full(nsub, guess_fit_freq(b["freqs"])),
         nchanx=np.full(nsub, nchan))
     data = b["data"].double().cpu().numpy()
-    model0 = np.tile(data[0].mean(axis=0), (nchan, 1))
+    # the bench's initial template: archive 0 dedispersed at DM0, averaged
+    ded = O.rotate_rows(data[0], 0.000241 ** -1 * synth.DM0 * (
+        b["freqs"] ** -2 - 1500.0 ** -2) / b["P"][0])
+    model0 = np.tile(ded.mean(axis=0), (nchan, 1))
     out = torch.zeros((nchan, nbin), dtype=torch.float64, device=dev)
     wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
     ph, w = ppalign._fit_and_weights(R, model0, True, nbin, dev)

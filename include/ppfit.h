@@ -262,6 +262,22 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
                              const double *scattering_index, const double *freqs,
                              const double *nu_ref, double *out, void *stream);
 
+/* Spline (PCA + B-spline) model portraits: pplib.gen_spline_portrait
+ * (pplib.py:966-990) as called by pplib.read_spline_model (pplib.py:3060-3096)
+ * from pptoas.GetTOAs.get_TOAs (pptoas.py:416-419) for make_spline_model
+ * templates.  Per (portrait, channel): the B-spline curve (knots[nknots],
+ * coefs[ncomp][nknots] -- splprep's c arrays, zero-padded --, degree
+ * <= 5) evaluated at freqs[p][n] as FITPACK splev (ext = 0), expanded on
+ * eigvec [nbin_model][ncomp] plus mean_prof [nbin_model]; ncomp = 0 tiles
+ * mean_prof.  nbin != nbin_model: scipy.signal.resample to nbin, then the
+ * reference's half-bin rotate_portrait.  nbin_model and nbin are powers of
+ * two in [32, 8192]; ncomp <= 64.  out: [nport][nchan][nbin] f64 (device). */
+int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin_model,
+                              int32_t nbin, int32_t ncomp, int32_t nknots, int32_t degree,
+                              const double *mean_prof, const double *eigvec,
+                              const double *knots, const double *coefs, const double *freqs,
+                              double *out, void *stream);
+
 /* Synthetic sub-integrations for benchmarks/tests (make_fake_pulsar minus
  * PSRCHIVE, pplib.py:3355-3493): out[s][n] = rotate(model[n], -phi[s],
  * -DM[s], P[s], freqs[n], nu_ref) + N(0, noise) with a counter-based RNG

@@ -98,6 +98,9 @@ SIGNATURES = {
     "ppf_gauss_portrait_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32,
                                                 ctypes.c_char_p, _vp, _vp, _vp,
                                                 _vp, _vp, _vp]),
+    "ppf_spline_portrait_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32,
+                                                 _i32, _i32, _i32, _vp, _vp,
+                                                 _vp, _vp, _vp, _vp, _vp]),
     "ppf_synth_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp,
                                        _vp, _vp, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_uint64,

@@ -597,6 +597,39 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     return PPF_OK;
 }
 
+int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin_model,
+                              int32_t nbin, int32_t ncomp, int32_t nknots, int32_t degree,
+                              const double *mean_prof, const double *eigvec, const double *knots,
+                              const double *coefs, const double *freqs, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (!pow2_in_range(nbin) || !pow2_in_range(nbin_model))
+        return fail(ctx, PPF_EUNSUP, "nbin=%d nbin_model=%d: powers of two in [32, 8192]", nbin,
+                    nbin_model);
+    if (nport < 0 || nchan < 1 || ncomp < 0 || ncomp > ppf::kSplineMaxComp || degree < 0 ||
+        degree > ppf::kSplineMaxDeg || (ncomp > 0 && nknots < 2 * degree + 2))
+        return fail(ctx, PPF_EINVAL, "bad spline model (ncomp=%d nknots=%d degree=%d)", ncomp, nknots,
+                    degree);
+    if (nport == 0) return PPF_OK;
+    if (!mean_prof || !freqs || !out || (ncomp > 0 && (!eigvec || !knots || !coefs)))
+        return fail(ctx, PPF_EINVAL, "null spline argument");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    ppf::SplineArgs a{};
+    a.nport = nport; a.nchan = nchan; a.nbin_model = nbin_model; a.nbin = nbin; a.ncomp = ncomp;
+    a.nknots = nknots; a.degree = degree;
+    a.log2N0 = ilog2(nbin_model / 2); a.log2N1 = ilog2(nbin / 2);
+    a.mean_prof = mean_prof; a.eigvec = eigvec; a.knots = knots; a.coefs = coefs; a.freqs = freqs;
+    a.out = out;
+    int rc;
+    if (nbin != nbin_model) {
+        if ((rc = twiddles(ctx, nbin_model, st, &a.T0, &a.T20))) return rc;
+        if ((rc = twiddles(ctx, nbin, st, &a.T1, &a.T21))) return rc;
+    }
+    if ((e = ppf::launch_spline_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_spline_port");
+    return PPF_OK;
+}
+
 int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, const double *model,
                     const double *freqs, const double *phi, const double *DM, const double *P,
                     double nu_ref, double noise, uint64_t seed, int64_t first_sub,

@@ -197,6 +197,27 @@ struct GaussArgs {
 };
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st);
 
+// pplib.gen_spline_portrait (pplib.py:966-990): per (portrait, channel) row,
+// splev of the B-spline curve tck at the channel frequency (FITPACK splev /
+// fpbspl, ext = 0), the eigenvector expansion plus the mean profile, and
+// (nbin != nbin_model) scipy.signal.resample to nbin followed by the
+// half-bin rotate_portrait of the reference
+struct SplineArgs {
+    int nport, nchan, nbin_model, nbin, ncomp, nknots, degree;
+    int log2N0, log2N1;          // log2 of the half lengths (model, output)
+    const double *mean_prof;     // [nbin_model]
+    const double *eigvec;        // [nbin_model][ncomp]
+    const double *knots;         // [nknots]
+    const double *coefs;         // [ncomp][nknots]  (splprep c, zero-padded)
+    const double *freqs;         // [nport][nchan]
+    const double2 *T0, *T20;     // twiddles of nbin_model
+    const double2 *T1, *T21;     // twiddles of nbin
+    double *out;                 // [nport][nchan][nbin]
+};
+constexpr int kSplineMaxComp = 64;
+constexpr int kSplineMaxDeg = 5;
+hipError_t launch_spline_port(const SplineArgs &a, hipStream_t st);
+
 hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);

@@ -1212,4 +1212,110 @@ hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+
+// ===========================================================================
+// k_spline_port: pplib.gen_spline_portrait (pplib.py:966-990) per row
+// (portrait p, channel n).  Thread 0 evaluates the B-spline curve at
+// x = freqs[p][n] exactly as FITPACK's splev (ext = 0: the end intervals
+// extrapolate) with fpbspl's Cox-de Boor recursion; every thread then forms
+// port[j] = mean_prof[j] + sum_c proj[c] eigvec[j][c] (np.dot(proj,
+// eigvec.T) + mean_prof).  With nbin != nbin_model the row is resampled as
+// scipy.signal.resample(port, nbin) (rfft; keep min(num, Nx)//2 + 1
+// harmonics, the old Nyquist halved when upsampling / doubled when
+// downsampling; irfft; x num/Nx) and then rotated by rotate_portrait(port,
+// 0.5 (1/nbin - 1/nbin_model)): both are folded into one spectrum
+// (the resampled spectrum with the DC and Nyquist imaginary parts dropped,
+// as the irfft -> rfft round trip does, times the phasor), one irfft.
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    __shared__ double proj[kSplineMaxComp];
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x;                   // p * nchan + n
+    const int N0 = a.nbin_model >> 1, N1 = a.nbin >> 1;
+    if (tid == 0) {
+        const double x = a.freqs[row];
+        const int k = a.degree, n = a.nknots;
+        const double *t = a.knots;
+        // knot interval t[l] <= x < t[l+1], l in [k, n - k - 2] (0-based)
+        int l = k;
+        while (l < n - k - 2 && x >= t[l + 1]) ++l;
+        double h[kSplineMaxDeg + 2], hh[kSplineMaxDeg + 2];
+        h[0] = 1.0;
+        for (int j = 1; j <= k; ++j) {
+            for (int i = 0; i < j; ++i) hh[i] = h[i];
+            h[0] = 0.0;
+            for (int i = 1; i <= j; ++i) {
+                const int li = l + i, lj = li - j;
+                if (t[li] != t[lj]) {
+                    const double f = hh[i - 1] / (t[li] - t[lj]);
+                    h[i - 1] += f * (t[li] - x);
+                    h[i] = f * (x - t[lj]);
+                } else {
+                    h[i] = 0.0;
+                }
+            }
+        }
+        for (int c = 0; c < a.ncomp; ++c) {
+            const double *cc = a.coefs + (int64_t)c * n;
+            double sp = 0.0;
+            for (int j = 0; j <= k; ++j) sp += cc[l - k + j] * h[j];
+            proj[c] = sp;
+        }
+    }
+    __syncthreads();
+    auto value = [&](int j) {
+        double v = 0.0;
+        const double *e = a.eigvec + (int64_t)j * a.ncomp;
+        for (int c = 0; c < a.ncomp; ++c) v = fma(proj[c], e[c], v);
+        return v + a.mean_prof[j];
+    };
+    double *o = a.out + row * (int64_t)a.nbin;
+    if (a.nbin == a.nbin_model) {
+        for (int j = tid; j < a.nbin; j += kBlock) o[j] = value(j);
+        return;
+    }
+    // resample + rotate
+    const int NM = N0 > N1 ? N0 : N1;
+    double2 *buf = lds;                    // complex FFT buffer (max N0, N1)
+    double2 *spec = lds + NM;              // output spectrum Y_k, k <= N1
+    for (int j = tid; j < N0; j += kBlock) buf[j] = cmk(value(2 * j), value(2 * j + 1));
+    __syncthreads();
+    lds_fft(buf, a.log2N0, a.T0, false);
+    const int num = a.nbin, Nx = a.nbin_model;
+    const int Nm = num < Nx ? num : Nx, nyq = Nm / 2 + 1;
+    const double scale = (double)num / (double)Nx;
+    const double shift = 0.5 * (1.0 / (double)num - 1.0 / (double)Nx);
+    for (int k = tid; k <= N1; k += kBlock) {
+        double2 Y = cmk(0.0, 0.0);
+        if (k < nyq) {
+            Y = rfft_bin(buf, N0, a.T20, k);
+            if (k == Nm / 2) Y = cscale(Y, num < Nx ? 2.0 : 0.5);   // Nm even (powers of 2)
+        }
+        Y = cscale(Y, scale);
+        if (k == 0 || k == N1) Y.y = 0.0;          // irfft -> rfft round trip
+        spec[k] = cmul(Y, cexp2pi((double)k * shift));
+    }
+    __syncthreads();
+    for (int k = tid; k < N1; k += kBlock) {
+        double2 Xk = spec[k], Xn = spec[N1 - k];
+        if (k == 0) { Xk.y = 0.0; Xn.y = 0.0; }    // irfft: DC and Nyquist real parts
+        buf[k] = irfft_prebin(Xk, Xn, a.T21[k]);
+    }
+    __syncthreads();
+    lds_fft(buf, a.log2N1, a.T1, true);
+    const double sc = 1.0 / (double)N1;
+    double2 *o2 = reinterpret_cast<double2 *>(o);
+    for (int j = tid; j < N1; j += kBlock) o2[j] = cscale(buf[j], sc);
+}
+
+hipError_t launch_spline_port(const SplineArgs &a, hipStream_t st) {
+    const int N0 = a.nbin_model >> 1, N1 = a.nbin >> 1;
+    const int NM = N0 > N1 ? N0 : N1;
+    const size_t lds = a.nbin == a.nbin_model ? 16 : (size_t)(NM + N1 + 1) * sizeof(double2);
+    hipLaunchKernelGGL(k_spline_port, dim3((unsigned)((int64_t)a.nport * a.nchan)), dim3(kBlock), lds,
+                       st, a);
+    return hipGetLastError();
+}
+
 }  // namespace ppf

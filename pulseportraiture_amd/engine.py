@@ -407,6 +407,47 @@ def gauss_portraits(model_code, params, scattering_index, freqs, nu_ref, nbin,
     return out
 
 
+def spline_portraits(mean_prof, eigvec, tck, freqs, nbin=None, dev=None):
+    """PCA + B-spline model portraits (pplib.gen_spline_portrait,
+    pplib.py:966-990) on the device (ppf_spline_portrait_batch): mean_prof
+    [nbin_model], eigvec [nbin_model, ncomp], tck = (knots, [coefs per
+    component], degree) as si.splprep returns it, freqs [nport, nchan] (or
+    [nchan]) -> float64 [nport, nchan, nbin]."""
+    dev = device(dev)
+    mean_prof = np.asarray(mean_prof, dtype=np.float64)
+    eigvec = np.asarray(eigvec, dtype=np.float64)
+    nbin0 = len(mean_prof)
+    nbin = nbin0 if nbin is None else int(nbin)
+    ncomp = eigvec.shape[1] if eigvec.ndim == 2 else 0
+    f = np.atleast_2d(np.asarray(freqs, dtype=np.float64))
+    nport, nchan = f.shape
+    if ncomp:
+        t = np.asarray(tck[0], dtype=np.float64)
+        cs = [np.asarray(c, dtype=np.float64) for c in tck[1]]
+        if len(cs) != ncomp:
+            raise ValueError("tck has %d coefficient arrays, eigvec %d "
+                             "columns" % (len(cs), ncomp))
+        coefs = np.zeros((ncomp, len(t)))
+        for i, c in enumerate(cs):
+            coefs[i, :len(c)] = c
+        degree, nknots = int(tck[2]), len(t)
+    else:
+        t, coefs, degree, nknots = np.zeros(1), np.zeros((1, 1)), 0, 1
+    ev = eigvec if ncomp else np.zeros((nbin0, 1))
+    mp_t = to_dev(mean_prof, dev, torch.float64)
+    ev_t = to_dev(np.ascontiguousarray(ev), dev, torch.float64)
+    t_t = to_dev(t, dev, torch.float64)
+    c_t = to_dev(coefs, dev, torch.float64)
+    f_t = to_dev(f, dev, torch.float64)
+    out = torch.empty((nport, nchan, nbin), dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_spline_portrait_batch(
+        ctx, nport, nchan, nbin0, nbin, ncomp, nknots, degree, _p(mp_t),
+        _p(ev_t), _p(t_t), _p(c_t), _p(f_t), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
 def synth(model, freqs, phi, DM, P, nu_ref, noise, seed, out_dtype=torch.float32,
           dev=None, first=0):
     """Synthetic sub-integrations [nsub, nchan, nbin] on the device."""

@@ -156,10 +156,9 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
     phases/freqs are given."""
     read_only = phases is None and freqs is None
     comps, fit_comps = [], []
-    name = code = None
-    nu_ref = dc = tau = alpha = 0.0
-    fit_dc = fit_tau = fit_alpha = 0
-    with open(modelfile) as fh:
+    name = code = nu_ref = dc = tau = alpha = None
+    fit_dc = fit_tau = fit_alpha = None
+    with open(modelfile) as fh:      # a pickled spline model: UnicodeDecodeError
         lines = fh.readlines()
     for line in lines:
         info = line.split()
@@ -184,6 +183,12 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
                 fit_comps.append([int(v) for v in info[2::2]])
         except IndexError:
             pass
+    # a missing line leaves the reference's local unbound (pplib.py:3022-3026)
+    for var, val in (("dc", dc), ("tau", tau), ("fit_dc", fit_dc),
+                     ("fit_tau", fit_tau)):
+        if val is None:
+            raise UnboundLocalError("local variable '%s' referenced before "
+                                    "assignment" % var)
     ngauss = len(comps)
     params = np.zeros(ngauss * 6 + 2)
     fit_flags = np.zeros(len(params))
@@ -192,6 +197,12 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
     for ig in range(ngauss):
         params[2 + ig * 6:8 + ig * 6] = comps[ig]
         fit_flags[2 + ig * 6:8 + ig * 6] = fit_comps[ig]
+    for var, val in (("modelname", name), ("model_code", code),
+                     ("nu_ref", nu_ref), ("alpha", alpha)) + \
+            ((("fit_alpha", fit_alpha),) if read_only else ()):
+        if val is None:
+            raise UnboundLocalError("local variable '%s' referenced before "
+                                    "assignment" % var)
     if read_only:
         return (name, code, nu_ref, ngauss, params, fit_flags, alpha,
                 fit_alpha)
@@ -205,6 +216,40 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
     if not quiet:
         print("Model Name: %s" % name)
     return name, ngauss, model
+
+
+def gen_spline_portrait(mean_prof, freqs, eigvec, tck, nbin=None):
+    """pplib.py:966-990 on the device (ppf_spline_portrait_batch: splev of
+    the B-spline curve per channel, eigenvector expansion, mean profile and,
+    for nbin != len(mean_prof), scipy.signal.resample + the half-bin
+    rotate_portrait)."""
+    from . import engine
+    out = engine.spline_portraits(mean_prof, eigvec, tck,
+                                  np.asarray(freqs, dtype=float)[None, :],
+                                  nbin)
+    return out[0].cpu().numpy()
+
+
+def read_spline_model(modelfile, freqs=None, nbin=None, quiet=False):
+    """pplib.py:3060-3096: a make_spline_model(...) file -- the pickled
+    (model name, source, datafile, mean profile, eigenvectors, tck) -- read
+    as the reference reads it; with freqs, the portrait built on the device
+    by gen_spline_portrait."""
+    import pickle
+    if not quiet:
+        print("Reading model from %s..." % modelfile)
+    try:
+        with open(modelfile, "rb") as fh:
+            modelname, source, datafile, mean_prof, eigvec, tck = \
+                pickle.load(fh)
+    except UnicodeDecodeError:       # python2 to python3 pickling issues
+        with open(modelfile, "rb") as fh:
+            modelname, source, datafile, mean_prof, eigvec, tck = \
+                pickle.load(fh, encoding="bytes")
+    if freqs is None:
+        return (modelname, source, datafile, mean_prof, eigvec, tck)
+    return (modelname, gen_spline_portrait(mean_prof, freqs, eigvec, tck,
+                                           nbin))
 
 
 # --------------------------------------------------------- device routines --

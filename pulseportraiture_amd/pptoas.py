@@ -211,8 +211,13 @@ class GetTOAs(object):
         in ONE ppf_gauss_portrait_batch launch (k_gauss_port)."""
         if self.is_FITS_model:
             raise NotImplementedError("FITS (archive) templates need PSRCHIVE")
-        (self.model_name, code, nu_ref, self.ngauss, gparams, _mff, alpha,
-         _mfa) = read_model(self.modelfile, quiet=True)
+        try:
+            (self.model_name, code, nu_ref, self.ngauss, gparams, _mff, alpha,
+             _mfa) = read_model(self.modelfile, quiet=True)
+        except (UnboundLocalError, UnicodeDecodeError):
+            # a make_spline_model template (pptoas.py:416-419): one device
+            # portrait per distinct frequency set, unscattered
+            return self._spline_models(d, ok_isubs)
         if fit_scat:
             (self.model_code, self.model_nu_ref, self.gparams,
              self.alpha) = code, nu_ref, gparams, alpha
@@ -236,6 +241,28 @@ class GetTOAs(object):
         models = engine.gauss_portraits(
             code, np.stack(prms), 0.0 if fit_scat else alpha,
             np.stack(freqs), nu_ref, nbin).cpu().numpy()
+        return models, np.array(index, dtype=np.int32)
+
+    def _spline_models(self, d, ok_isubs):
+        """read_spline_model(modelfile, freqs, nbin) per sub-integration
+        (pptoas.py:416-419), the distinct frequency sets of the archive in
+        ONE ppf_spline_portrait_batch launch."""
+        from .pplib import read_spline_model
+        (self.model_name, _src, _df, mean_prof, eigvec,
+         tck) = read_spline_model(self.modelfile, quiet=True)
+        nbin = len(d.phases)
+        cache, freqs, index = {}, [], []
+        for isub in ok_isubs:
+            key = d.freqs[isub].tobytes()
+            if key not in cache:
+                cache[key] = len(freqs)
+                freqs.append(np.asarray(d.freqs[isub], dtype=float))
+            index.append(cache[key])
+        if not freqs:
+            return np.zeros((0, len(d.freqs[0]), nbin)), \
+                np.zeros(0, dtype=np.int32)
+        models = engine.spline_portraits(mean_prof, eigvec, tck,
+                                         np.stack(freqs), nbin).cpu().numpy()
         return models, np.array(index, dtype=np.int32)
 
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None,

@@ -28,6 +28,22 @@ GMODEL_PARAMS = np.array([
 ])
 
 
+def write_gmodel(path, name="PSR_1234-5678"):
+    """The example template as a .gmodel file (the ppgauss format
+    read_model parses, pplib.py:2990-3026)."""
+    p = GMODEL_PARAMS
+    lines = ["MODEL   %s" % name, "CODE    %s" % GMODEL_CODE,
+             "FREQ    %.5f" % GMODEL_NU_REF, "DC      %.8f 1" % p[0],
+             "TAU     %.8f 1" % p[1], "ALPHA   %.3f      0" % GMODEL_ALPHA]
+    for i in range((len(p) - 2) // 6):
+        c = p[2 + 6 * i:8 + 6 * i]
+        lines.append("COMP%02d  " % (i + 1) +
+                     "  ".join("%.8f 1" % v for v in c))
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    return path
+
+
 def channel_freqs(nchan, lo=1100.0, bw=800.0):
     cw = bw / nchan
     return np.linspace(lo + cw / 2, lo + bw - cw / 2, nchan)

@@ -62,8 +62,8 @@ def toa_case(name):
         out.append(dict(subints=sub, weights=fi["weights"], dfs=fi["dfs"],
                         epochs=fi["epochs"], noise=c["f%d_noise" % f],
                         snrs=c["f%d_snrs" % f]))
-    gm = FI.NARROW_GMODEL if conf.get("narrow") else \
-        os.path.join(G.GOLDEN, "example.gmodel")
+    gm = FI.NARROW_GMODEL if conf.get("narrow") else FI.SPLINE_MODEL if \
+        conf.get("spline") else os.path.join(G.GOLDEN, "example.gmodel")
     return c, out, freqs, gm
 
 

@@ -20,6 +20,39 @@ NARROW_PARAMS = np.concatenate([S.read_gmodel()[2],
                                 [0.62, 0.0, 0.002, 0.0, 3.0, -1.0]])
 
 
+SPLINE_MODEL = os.path.join(HERE, "spline.spl")
+SPLINE_NBIN, SPLINE_NCOMP = 512, 3
+
+
+def spline_parts():
+    """A make_spline_model-type model (ppspline.py's PCA + B-spline, built
+    here with numpy/scipy from the example.gmodel portrait at 64 channels,
+    512 bins): (modelname, source, datafile, mean_prof, eigvec [512, 3],
+    tck = splprep(projections, u=freqs, k=3))."""
+    import scipy.interpolate as si
+    model, freqs = S.template(64, SPLINE_NBIN)
+    mean_prof = model.mean(axis=0)
+    delta = model - mean_prof
+    _, _, vt = np.linalg.svd(delta, full_matrices=False)
+    eigvec = np.ascontiguousarray(vt[:SPLINE_NCOMP].T)
+    proj = delta @ eigvec
+    tck, _ = si.splprep(list(proj.T), u=freqs, k=3,
+                        s=1e-4 * float((proj ** 2).sum()))
+    tck = [np.asarray(tck[0]), [np.asarray(c) for c in tck[1]], int(tck[2])]
+    return ("synthetic_spline", "J1234-5678", "synthetic.fits", mean_prof,
+            eigvec, tck)
+
+
+def write_spline(path=SPLINE_MODEL):
+    """tests/golden/spline.spl (committed; rewritten only if missing): the
+    pickle read_spline_model reads (pplib.py:3083-3088)."""
+    import pickle
+    if os.path.exists(path):
+        return
+    with open(path, "wb") as fh:
+        pickle.dump(spline_parts(), fh, protocol=4)
+
+
 def write_narrow(path=NARROW_GMODEL):
     """tests/golden/narrow.gmodel (committed; rewritten only if missing)."""
     if os.path.exists(path):
@@ -85,7 +118,17 @@ TOAS = [
     dict(name="c2", nfile=1, nsub=8, nchan=512, nbin=2048, seed=202),
     dict(name="narrow", nfile=1, nsub=4, nchan=512, nbin=2048, seed=203,
          narrow=True),
+    # get_TOAs with a spline template (pptoas.py:416-419), 512 -> 1024 bins
+    dict(name="spline", nfile=2, nsub=4, nchan=64, nbin=1024, seed=204,
+         spline=True),
 ]
+
+# gen_spline_portrait cases: (name, nchan, lo, bw, nbin [None = model's])
+SPLINES = [("same", 64, 1100.0, 800.0, None), ("n512", 48, 1150.0, 700.0, 512),
+           ("up1024", 64, 1100.0, 800.0, 1024), ("up4096", 32, 1200.0, 600.0,
+                                                   4096),
+           ("down256", 64, 1100.0, 800.0, 256), ("down64", 100, 1120.0, 760.0,
+                                                 64)]
 
 
 def toa_inputs(c):

@@ -44,7 +44,8 @@ import make_golden_align as mga  # noqa: E402
 import numpy as np  # noqa: E402
 import synth_np as S  # noqa: E402
 from full_inputs import (FITS, TOAS, ALIGNS, NARROW_GMODEL, fit_inputs,  # noqa: E402
-                         toa_inputs, align_inputs, write_narrow)
+                         toa_inputs, align_inputs, write_narrow, SPLINES,
+                         SPLINE_MODEL, write_spline)
 
 OUT = os.path.join(HERE, "full.npz")
 
@@ -113,7 +114,8 @@ def run_toas(c):
     gt = mg.pptoas.GetTOAs.__new__(mg.pptoas.GetTOAs)
     gt.datafiles = list(files.keys())
     gt.is_FITS_model = False
-    gt.modelfile = NARROW_GMODEL if c.get("narrow") else mg.GMODEL
+    gt.modelfile = (NARROW_GMODEL if c.get("narrow") else SPLINE_MODEL if
+                    c.get("spline") else mg.GMODEL)
     for attr in ["obs", "doppler_fs", "nu0s", "nu_fits", "nu_refs",
                  "ok_idatafiles", "ok_isubs", "epochs", "MJDs", "Ps", "phis",
                  "phi_errs", "TOAs", "TOA_errs", "DM0s", "DMs", "DM_errs",
@@ -247,11 +249,35 @@ def run_scales():
     return out
 
 
+def run_splines():
+    """pplib.gen_spline_portrait (pplib.py:966-990) through
+    read_spline_model (pplib.py:3060-3096) on tests/golden/spline.spl: same,
+    up- and down-sampled nbin, other frequency grids; plus the ncomp = 0
+    (mean profile only) branch."""
+    out = {}
+    for name, nchan, lo, bw, nbin in SPLINES:
+        freqs = S.channel_freqs(nchan, lo, bw)
+        with contextlib.redirect_stdout(io.StringIO()):
+            _, port = mg.pplib.read_spline_model(SPLINE_MODEL, freqs, nbin,
+                                                 quiet=True)
+        out[name + "_freqs"] = freqs
+        out[name + "_nbin"] = np.int64(-1 if nbin is None else nbin)
+        out[name + "_out"] = port
+    _, _, _, mean_prof, eigvec, tck = mg.pplib.read_spline_model(
+        SPLINE_MODEL, quiet=True)
+    freqs = S.channel_freqs(16, 1100.0, 800.0)
+    out["mean_freqs"] = freqs
+    out["mean_out"] = mg.pplib.gen_spline_portrait(
+        mean_prof, freqs, np.zeros((len(mean_prof), 0)), tck, 1024)
+    return out
+
+
 def main():
     only = None
     if "--only" in sys.argv:
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     write_narrow()
+    write_spline()
     old = {}
     if os.path.exists(OUT):
         z = np.load(OUT)
@@ -261,7 +287,8 @@ def main():
     jobs = ([("fit", c, run_fit) for c in FITS] +
             [("toas", c, run_toas) for c in TOAS] +
             [("align", c, run_align) for c in ALIGNS] +
-            [("scales", dict(name="scales"), lambda c: run_scales())])
+            [("scales", dict(name="scales"), lambda c: run_scales())] +
+            [("spline", dict(name="gen"), lambda c: run_splines())])
     for kind, c, fn in jobs:
         key = "%s_%s" % (kind, c["name"])
         if only is not None and key not in only and c["name"] not in only:

@@ -3,6 +3,8 @@ oracle_c5.npz): the inputs rebuild bit for bit from their stored parameters
 (SHA-256), the oracle reproduces the reference's full-shape outputs
 (parity pinning of the checker at the BASELINE shapes), and the host
 get_scales_full matches the reference's."""
+import os
+
 import numpy as np
 import pytest
 
@@ -20,7 +22,7 @@ def test_fit_inputs_rebuild(name):
     F.fit_case(name)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "narrow"])
+@pytest.mark.parametrize("name", ["c1", "c2", "narrow", "spline"])
 def test_toa_inputs_rebuild(name):
     F.toa_case(name)
 
@@ -120,3 +122,35 @@ def test_get_scales_full_matches_reference():
                                         bool(g["s%d_log10_tau" % i]))
         np.testing.assert_allclose(got, g["s%d_out" % i], rtol=1e-12,
                                    atol=1e-14 * np.abs(g["s%d_out" % i]).max())
+
+
+def test_spline_model_file():
+    """tests/golden/spline.spl (the make_spline_model-type template the
+    spline goldens were made with) reads back through read_spline_model
+    (pplib.py:3060-3096) as the parts full_inputs.spline_parts() builds, and
+    read_model rejects it with the UnicodeDecodeError GetTOAs catches to
+    fall back to the spline reader (pptoas.py:416)."""
+    import full_inputs as FI
+    from pulseportraiture_amd import pplib
+    name, src, df, mean_prof, eigvec, tck = pplib.read_spline_model(
+        FI.SPLINE_MODEL, quiet=True)
+    parts = FI.spline_parts()
+    assert (name, src, df) == parts[:3]
+    np.testing.assert_allclose(mean_prof, parts[3], rtol=1e-12)
+    np.testing.assert_allclose(np.abs(eigvec), np.abs(parts[4]), atol=1e-10)
+    assert eigvec.shape == (FI.SPLINE_NBIN, FI.SPLINE_NCOMP)
+    assert int(tck[2]) == 3 and len(tck[1]) == FI.SPLINE_NCOMP
+    with pytest.raises(UnicodeDecodeError):
+        pplib.read_model(FI.SPLINE_MODEL, quiet=True)
+
+
+def test_read_model_missing_line_unbound(tmp_path):
+    """A .gmodel without its DC line leaves the reference's local unbound
+    (pplib.py:3022): UnboundLocalError, as GetTOAs expects."""
+    from pulseportraiture_amd import pplib
+    src = open(os.path.join(G.GOLDEN, "example.gmodel")).read().splitlines()
+    bad = tmp_path / "nodc.gmodel"
+    bad.write_text("\n".join(l for l in src if not l.startswith("DC")) +
+                   "\n")
+    with pytest.raises(UnboundLocalError):
+        pplib.read_model(str(bad), quiet=True)

@@ -141,13 +141,14 @@ def _same_printed_number(a, b):
     return abs(fa - fb) <= 1.01 * 10 ** (-dec)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "narrow"])
+@pytest.mark.parametrize("name", ["c1", "c2", "narrow", "spline"])
 def test_fullshape_gettoas_matches_reference(name, monkeypatch, tmp_path,
                                              capsys):
     """GetTOAs.get_TOAs against the reference's run: configs[0] (the
     examples/example.py archive set: 5 x 10 x 64 x 512 with scintillation,
-    get_TOAs(DM0=DM0)), one configs[1]-shape archive (8 x 512 x 2048) and the
-    narrow-template archive; per sub-int phases/DMs within 0.01 sigma,
+    get_TOAs(DM0=DM0)), one configs[1]-shape archive (8 x 512 x 2048), the
+    narrow-template archive and a spline (make_spline_model) template
+    resampled 512 -> 1024 bins; per sub-int phases/DMs within 0.01 sigma,
     chi2_red 1e-8, DeltaDM, and every .tim token to its printed precision."""
     from pulseportraiture_amd import pptoas, pplib
     c, files, gm = _archives(name)
@@ -181,7 +182,7 @@ def test_fullshape_gettoas_matches_reference(name, monkeypatch, tmp_path,
         ta, tb = a.split(), b.split()
         assert len(ta) == len(tb)
         for i, (x, y) in enumerate(zip(ta, tb)):
-            if x.endswith(".gmodel"):       # -tmplt path differs
+            if x.endswith((".gmodel", ".spl")):   # -tmplt path differs
                 continue
             if i == 1:
                 # the TOA frequency is the zero-covariance frequency nu_0,
@@ -343,3 +344,32 @@ def test_c4_bench_iteration_matches_oracle():
     port, _ = O.align_archives(archives, model_data, fit_dm=True, niter=1)
     np.testing.assert_allclose(got, port[0], rtol=0,
                                atol=1e-6 * np.abs(port[0]).max())
+
+
+# ----------------------------------------------------- spline templates ---
+@pytest.mark.parametrize("name", [n for n, *_ in F.FI.SPLINES] + ["mean"])
+def test_spline_portrait_matches_reference(name):
+    """pplib.read_spline_model(modelfile, freqs, nbin) -> gen_spline_portrait
+    (pplib.py:966-990, 3060-3096) on the device (k_spline_port) against the
+    reference's portraits: splev per channel, eigenvector expansion and
+    scipy.signal.resample + half-bin rotation for nbin != 512 (up to 4096,
+    down to 64); "mean" is the ncomp = 0 branch resampled to 1024 bins.
+    Tolerance 1e-11 of the portrait's peak (fp64 FFT rounding)."""
+    from pulseportraiture_amd import pplib
+    g = F.case("spline", "gen")
+    freqs = g[name + "_freqs"]
+    ref = g[name + "_out"]
+    if name == "mean":
+        _, _, _, mean_prof, eigvec, tck = pplib.read_spline_model(
+            F.FI.SPLINE_MODEL, quiet=True)
+        got = pplib.gen_spline_portrait(mean_prof, freqs,
+                                        np.zeros((len(mean_prof), 0)), tck,
+                                        1024)
+    else:
+        nbin = int(g[name + "_nbin"])
+        _, got = pplib.read_spline_model(F.FI.SPLINE_MODEL, freqs,
+                                         None if nbin < 0 else nbin,
+                                         quiet=True)
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0,
+                               atol=1e-11 * np.abs(ref).max())

@@ -45,6 +45,25 @@ def main():
                            out["f0_snrs"], np.full(nsub, MGF.S.P0), MGF.S.DM0,
                            fi["dfs"], noise_stds=out["f0_noise"])
         orc_s = time.perf_counter() - t0
+        # the scattering fits (bench --fit full / scat): the reference's
+        # fit_portrait_full against the oracle's on the C3 golden inputs
+        from full_inputs import FITS
+        scat = {}
+        for mode, name in (("full", "c3_all_512x2048_a"),
+                           ("scat", "c3_pdta_512x2048")):
+            fc = [f for f in FITS if f["name"] == name][0]
+            r = MGF.run_fit(fc)
+            data, model, freqs, P, _, init, nu_fit = MGF.fit_inputs(fc)
+            t0 = time.perf_counter()
+            O.fit_portrait_full(data.astype(np.float64), model, list(init), P,
+                                freqs, [nu_fit] * 3, [None] * 3, r["errs"],
+                                list(fc["flags"]), log10_tau=True)
+            o_s = time.perf_counter() - t0
+            scat[mode] = dict(case=name, flags=list(fc["flags"]),
+                              reference_s_per_fit=float(r["ref_seconds"]),
+                              oracle_s_per_fit=o_s,
+                              reference_over_oracle_time=float(
+                                  r["ref_seconds"]) / o_s)
     res = dict(shape="512x2048 phase+DM GetTOAs loop", nsub=nsub,
                reference_s_per_fit=ref_s / nsub,
                oracle_s_per_fit=orc_s / nsub,
@@ -53,7 +72,8 @@ def main():
                threads=1, numpy=np.__version__,
                note="measured in the build container (the reference never "
                     "travels to the GPU box); bench.py divides the oracle's "
-                    "rate on the GPU box host by this ratio")
+                    "rate on the GPU box host by this ratio",
+               scattering_fits=scat)
     path = os.path.join(ROOT, "profiles", "cpu_ratio.json")
     json.dump(res, open(path, "w"), indent=1)
     print(json.dumps(res, indent=1))

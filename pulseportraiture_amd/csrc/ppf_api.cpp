@@ -371,10 +371,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.state = (ppf::TRState *)(ws + L.state);
     sa.partials = (double *)(ws + L.partials);
     sa.active = (unsigned *)(ws + L.active);
+    sa.kinds = (unsigned *)(ws + L.active + 16);
     if (!ctx->host_active) {
-        e = hipHostMalloc((void **)&ctx->host_active, sizeof(unsigned));
+        e = hipHostMalloc((void **)&ctx->host_active, 4 * sizeof(unsigned));
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
     }
+    if ((e = hipMemsetAsync(sa.kinds, 0, 2 * sizeof(unsigned), st)) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemsetAsync");
     sa.moments = use_moments;
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
@@ -382,6 +385,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.xslot = xslot;
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
+    // how many fits iterate on the moments and how many on streaming passes:
+    // the iteration loop launches only the kernels some fit needs
+    if ((e = hipMemcpyAsync(ctx->host_active + 1, sa.kinds, 2 * sizeof(unsigned), hipMemcpyDeviceToHost,
+                            st)) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemcpyAsync");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+    const bool any_mom = ctx->host_active[1] != 0, any_pass = ctx->host_active[2] != 0;
     ppf::XmomArgs ma{};
     ma.nsub = d->nsub; ma.nchan = d->nchan; ma.nbin = d->nbin; ma.log2N = xa.log2N;
     ma.nblk = L.nblk; ma.cb = L.cb; ma.dtype = d->data_dtype; ma.xcd_swizzle = xa.xcd_swizzle;
@@ -401,10 +411,10 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // sub-ints still needing work is read back between groups.
     const int maxiter = d->max_iter > 0 ? d->max_iter : 200 * 5;
     int iter = 0;
-    for (int group = sa.moments ? 3 : 6;; group = sa.moments ? 2 : 4) {
+    for (int group = sa.moments ? 3 : 6; any_mom || any_pass; group = sa.moments ? 2 : 4) {
         for (int g = 0; g < group; ++g) {
-            if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
-            if (sa.moments) {
+            if (any_pass && (e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
+            if (sa.moments && any_mom) {
                 const bool full = iter == 0 && g == 0;
                 if (full && fused) mark(5);
                 e = fused ? ppf::launch_xmom(ma, full, st) : ppf::launch_moments(sa, st);
@@ -416,8 +426,9 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             }
             if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");
-            if ((e = ppf::launch_tr_step(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_step");
-            if (sa.moments && (e = ppf::launch_tr_mom(sa, st)) != hipSuccess)
+            if (any_pass && (e = ppf::launch_tr_step(sa, st)) != hipSuccess)
+                return hip_fail(ctx, e, "k_tr_step");
+            if (sa.moments && any_mom && (e = ppf::launch_tr_mom(sa, st)) != hipSuccess)
                 return hip_fail(ctx, e, "k_tr_mom");
         }
         iter += group;

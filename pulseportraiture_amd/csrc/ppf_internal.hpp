@@ -106,6 +106,7 @@ struct SolveArgs {
     TRState *state;              // [nsub]
     double *partials;            // [nsub][pass_blocks(nchan)][21]
     unsigned *active;            // sub-ints still iterating (k_tr_step)
+    unsigned *kinds;             // k_tr_init: [0] moment-mode fits, [1] streaming-pass fits
     // moment-expansion solver for fits without scattering (ppf_moments)
     int moments;                 // 1: enabled
     double2 *mom;                // [nsub][2][nchan][kMoments]

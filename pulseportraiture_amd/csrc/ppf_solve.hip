@@ -265,6 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         S.mvalid[0] = mmode;
         S.mvalid[1] = 0;
         for (int i = 0; i < 3; ++i) { S.mc[0][i] = x[i]; S.mc[1][i] = x[i]; }
+        // which iteration kernels the call needs at all (the host skips the
+        // others)
+        if (a.kinds && S.phase == PH_INIT) atomicAdd(a.kinds + (mmode ? 0 : 1), 1u);
     }
     if (mmode) {
         const double P = a.P[s];
@@ -366,33 +369,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 #define PPF_PASS_KB 4
 #endif
         constexpr int KB = PPF_PASS_KB;
-        // three rotating groups: loads run two groups ahead of the sums
-        double2 xv[KB], xn[KB], xn2[KB];
-        double pv[KB], pn[KB], pn2[KB];
+        // two buffers, loads one group ahead of the sums.  The loop is
+        // unrolled by two so each buffer keeps its registers (rotating them
+        // with moves would make each iteration wait for all its loads).
+        // Loads are unconditional (the index clamped into the row) and terms
+        // past the last harmonic are zeroed where they are SUMMED: a select
+        // on a freshly loaded value would also force that wait.
+        double2 xa[KB], xb[KB];
+        double pa[KB], pb[KB];
         auto ldg = [&](int kb, double2 (&xo)[KB], double (&po)[KB]) {
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
                 const int k = min(kb + u, kend - 1);
-                // past the last harmonic: zero terms (no branch in the group)
-                const bool in = kb + u < kend;
-                const double2 xl = Xc[k * xs];
-                xo[u] = in ? xl : cmk(0.0, 0.0);
-                if (SCAT) {
-                    const double pl = Pc[k * xs];
-                    po[u] = in ? pl : 0.0;
-                }
+                xo[u] = Xc[k * xs];
+                if (SCAT) po[u] = Pc[k * xs];
             }
         };
-        ldg(0, xv, pv);
-        if (KB < kend) ldg(KB, xn, pn);
         double2 E = cmk(1.0, 0.0);
-        for (int kb = 0; kb < kend; kb += KB) {
-            if (kb + 2 * KB < kend) ldg(kb + 2 * KB, xn2, pn2);
+        auto sum_group = [&](int kb, const double2 (&xv)[KB], const double (&pv)[KB]) {
             if ((kb & 63) == 0) E = cexp2pi((double)kb * phin);   // exact seed every 64
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
                 const double kk = (double)(kb + u);
-                const double2 y = cmul(xv[u], E);
+                const bool in = kb + u < kend;
+                const double2 y = in ? cmul(xv[u], E) : cmk(0.0, 0.0);
                 if (!SCAT) {
                     a0 += y.x;
                     a1 = fma(kk, y.y, a1);
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
                     q1 = fma(-uu, z2.y, q1);
                     q1p = fma(kk * uu, z2.x, q1p);
                     q2 = fma(-u2, z3, q2);
-                    const double Pk = pv[u] * inv_e2;
+                    const double Pk = (in ? pv[u] : 0.0) * inv_e2;
                     s0 = fma(d, Pk, s0);
                     const double tp = u2 * d * d * Pk;
                     t1 += tp;
@@ -423,13 +423,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
                 }
                 E = cmul(E, W);
             }
-#pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                xv[u] = xn[u];
-                pv[u] = pn[u];
-                xn[u] = xn2[u];
-                pn[u] = pn2[u];
-            }
+        };
+        ldg(0, xa, pa);
+        // (no early exit: a trailing group may sum zeros, which keeps one
+        // straight-line body and its load/wait schedule)
+        for (int kb = 0; kb < kend; kb += 2 * KB) {
+            ldg(kb + KB, xb, pb);
+            sum_group(kb, xa, pa);
+            ldg(kb + 2 * KB, xa, pa);
+            sum_group(kb + KB, xb, pb);
         }
         double my[10];
         my[0] = a0; my[1] = -kTwoPi * a1; my[2] = -kTwoPi * kTwoPi * a2;

@@ -864,29 +864,44 @@ hipError_t launch_model_pow_t(const double2 *Mft, int nchan, int nharm, int nmod
 // 1025 harmonics; at 16384 x 1024 over 400-800 MHz the narrow component
 // reaches Nyquist and nothing is cut).
 // rel < 0 (ppf_fit_desc.options PPF_OPT_NO_HCUT): KC = nharm.
-__global__ __launch_bounds__(256) void k_model_cut(const double *MP, int nchan, int nharm, int nmodel,
-                                                   double rel, int32_t *KC) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)nmodel * nchan) return;
-    const int m = (int)(i / nchan), n = (int)(i % nchan);
-    const double *p = MP + (int64_t)m * nharm * nchan + n;
-    int kc = nharm;
-    if (rel >= 0.0) {
-        double mx = 0.0;
-        for (int k = 0; k < nharm; ++k) mx = fmax(mx, p[(int64_t)k * nchan]);
-        const double thr = rel * mx;
-        kc = 1;
-        for (int k = nharm - 1; k >= 1; --k)
-            if (p[(int64_t)k * nchan] > thr) { kc = k + 1; break; }
+// workgroup = 64 channels (lanes) x 16 waves, each wave a 1/16 share of the
+// harmonics (loads coalesced across the channels), reduced through LDS
+constexpr int kCutWaves = 16;
+__global__ __launch_bounds__(64 * kCutWaves) void k_model_cut(const double *MP, int nchan, int nharm,
+                                                             int nmodel, double rel, int32_t *KC) {
+    __shared__ double smx[kCutWaves][64];
+    __shared__ int skc[kCutWaves][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cblk = (nchan + 63) / 64;
+    const int m = blockIdx.x / cblk, n = (blockIdx.x % cblk) * 64 + lane;
+    const bool on = n < nchan;
+    const double *p = MP + (int64_t)m * nharm * nchan + (on ? n : 0);
+    double mx = 0.0;
+    if (rel >= 0.0 && on)
+        for (int k = w; k < nharm; k += kCutWaves) mx = fmax(mx, p[(int64_t)k * nchan]);
+    smx[w][lane] = mx;
+    __syncthreads();
+    mx = 0.0;
+    for (int q = 0; q < kCutWaves; ++q) mx = fmax(mx, smx[q][lane]);
+    const double thr = rel * mx;
+    // last harmonic k >= 1 above the threshold (KC = k + 1; 1 when none)
+    int kc = 1;
+    if (rel >= 0.0 && on)
+        for (int k = w; k < nharm; k += kCutWaves)
+            if (k >= 1 && p[(int64_t)k * nchan] > thr) kc = k + 1;
+    skc[w][lane] = kc;
+    __syncthreads();
+    if (w == 0 && on) {
+        for (int q = 1; q < kCutWaves; ++q) kc = max(kc, skc[q][lane]);
+        KC[(int64_t)m * nchan + n] = rel >= 0.0 ? kc : nharm;
     }
-    KC[i] = kc;
 }
 
 hipError_t launch_model_cut(const double *MP, int nchan, int nharm, int nmodel, bool off,
                             int32_t *KC, hipStream_t st) {
-    const int64_t n = (int64_t)nmodel * nchan;
-    hipLaunchKernelGGL(k_model_cut, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, MP, nchan,
-                       nharm, nmodel, off ? -1.0 : kCutRel, KC);
+    const int cblk = (nchan + 63) / 64;
+    hipLaunchKernelGGL(k_model_cut, dim3((unsigned)(nmodel * cblk)), dim3(64 * kCutWaves), 0, st, MP,
+                       nchan, nharm, nmodel, off ? -1.0 : kCutRel, KC);
     return hipGetLastError();
 }
 

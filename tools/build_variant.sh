@@ -7,7 +7,7 @@ flags="$*"
 root=$(cd $(dirname $0)/.. && pwd)
 od=$root/build/variants/$name
 mkdir -p $od
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -ffp-contract=fast -munsafe-fp-atomics $flags"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed -ffp-contract=fast -munsafe-fp-atomics $flags"
 C=$root/pulseportraiture_amd/csrc
 $H -c $C/ppf_kernels.hip -o $od/k.o &
 $H -c $C/ppf_xspec.hip -o $od/x.o &

@@ -338,14 +338,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 
     int g, cb;
     block_map(a.xcd_swizzle, a.nblk, g, cb);
-    const int s = g * XW + wave;
+    // wave-uniform in SGPRs (readfirstlane): the row pointers then take the
+    // SADDR + 32-bit lane offset load form instead of 64-bit VGPR pointers
+    // (at 256 VGPRs those spilled, and every scratch reload waited for all
+    // outstanding row prefetches)
+    const int s = __builtin_amdgcn_readfirstlane(g * XW + wave);
     const TRState *st = reinterpret_cast<const TRState *>(a.state);
     const bool act = s < a.nsub && st[s].mmode && st[s].need_mom;
     if (!__syncthreads_or(act)) return;                  // uniform per workgroup
     const int q = act ? st[s].mtarget : 0;
     const double c0 = act ? st[s].mc[q][0] : 0.0, c1 = act ? st[s].mc[q][1] : 0.0,
                  c2 = act ? st[s].mc[q][2] : 0.0;
-    const int sv = act ? s : 0;
+    const int sv = __builtin_amdgcn_readfirstlane(act ? s : 0);
 
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
     const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)sv * a.nchan * (2 * N);
@@ -412,9 +416,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         const double sb = bin_centre(phc, 2 * N);
         nx_sh = (int)(sb - (double)(2 * N) * floor(sb / (double)(2 * N)));
         nx_r = phc - sb / (double)(2 * N);          // residual centre offset
-        const VecT *x = reinterpret_cast<const VecT *>(rows + (int64_t)n * (2 * N));
+        const char *x = reinterpret_cast<const char *>(rows + (int64_t)n * (2 * N));
+        // the lane's byte offset is re-derived every round (opaque): hoisted,
+        // base + offset became a live 64-bit VGPR pointer that spilled
+        unsigned off = (unsigned)lane * 16u;
+        asm volatile("" : "+v"(off));
 #pragma unroll
-        for (int c = 0; c < NLD; ++c) zr[c] = x[lane + 64 * c];
+        for (int c = 0; c < NLD; ++c)
+            zr[c] = *reinterpret_cast<const VecT *>(x + off + 1024u * (unsigned)c);
     };
     auto usable = [&](int n) {
         return act && n < cend && __builtin_amdgcn_readlane(ch_use, n - cbase) != 0;
@@ -518,7 +527,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
                 mres[n] = res_in;
             }
         } else if (act && n < cend && lane < 4) {
-            a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;    // masked channel
+            unsigned lo = (unsigned)lane;       // opaque: see fetch()
+            asm volatile("" : "+v"(lo));
+            a.chan[((int64_t)s * a.nchan + n) * 4 + lo] = 0.0;      // masked channel
         }
         XP(2);
         __syncthreads();
@@ -575,7 +586,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             const int idx = (om & 1) * 256 + (row >> 2) * 64 + ((row & 3) << 4) + (om >> 1);
 #pragma unroll
             for (int w2 = 0; w2 < XW; ++w2) val += reinterpret_cast<const double *>(lds + w2 * SLW)[idx];
-            if (live) mom[((int64_t)n * kMoments + om) * 2 + ori] = val * ie;
+            unsigned mo = (unsigned)(om * 2 + ori);     // opaque: see fetch()
+            asm volatile("" : "+v"(mo));
+            if (live) mom[(int64_t)n * kMoments * 2 + mo] = val * ie;
         }
         __syncthreads();
         XP(5);

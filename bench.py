@@ -523,6 +523,9 @@ def main():
     khist = np.zeros((ncalls, 2))
     kgot = lib.ppf_kernel_ms_history(ctx, ncalls, khist.ctypes.data)
     kern_ms = khist[:kgot].sum(axis=0)
+    phist = np.zeros((ncalls, 2))
+    pgot = lib.ppf_pass_ms_history(ctx, ncalls, phist.ctypes.data)
+    pass_ms, pass_launches = phist[:pgot].sum(axis=0)
     res_np = last.cpu().numpy()
     I = _lib.RESULT_INDEX
     nfev = res_np[:, I["nfeval"]]
@@ -566,6 +569,17 @@ def main():
                              unit=xspec_unit,
                              bytes=steps_subints * xspec_unit +
                              ncalls * nchan * nharm * 16)
+        #  k_pass<true> (one trust-region evaluation per launch of every fit
+        #   still iterating): read the fit's cut X (the same xh harmonics
+        #   k_xspec_w wrote), write its per-channel stats (10 f64) and the
+        #   block partials (21 f64 per 256 channels); |M|^2 of the cut
+        #   harmonics once per launch (shared by the batch: L2/MALL)
+        nblkp = (nchan + 255) // 256
+        pass_unit = xh * 16 + nchan * 80 + nblkp * 21 * 8
+        evals = steps_subints * mean_passes
+        kern["pass"] = dict(name="k_pass<true>", ms=pass_ms, unit=pass_unit,
+                            launches=int(pass_launches),
+                            bytes=evals * pass_unit + pass_launches * xh * 8)
     else:
         kern["xmom"] = dict(name="k_xmom_g<%d, 0, true, true>" % L2N,
                             ms=kern_ms[0], unit=xmom_unit,
@@ -576,23 +590,28 @@ def main():
     achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
     # HBM traffic per launch from the PMC passes (profiles/pmc_reduce.py):
     # measured bytes per unit x the units one launch processes
+    nlaunch = dk.get("launches", ncalls)
+    units_launch = (steps_subints if "launches" not in dk else
+                    steps_subints * mean_passes) / nlaunch
     traffic = None
     if os.path.exists(args.pmc):
-        try:
-            pm = json.load(open(args.pmc))["kernels"][dom]
-            traffic = round(pm["hbm_bytes"] * (steps_subints / ncalls))
-        except Exception:
-            traffic = None
+        pm = json.load(open(args.pmc)).get("modes", {}).get(args.fit, {})
+        pk = pm.get("kernels", {}).get(dom)
+        if pk:
+            traffic = round(pk["hbm_bytes"] * units_launch)
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                 unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
                 traffic=traffic, kernel=dk["name"],
-                algorithmic_bytes_per_launch=dk["bytes"] / ncalls,
-                avg_launch_ms=round(dk["ms"] / ncalls, 4),
-                units_per_launch=steps_subints / ncalls)
+                algorithmic_bytes_per_launch=dk["bytes"] / nlaunch,
+                algorithmic_bytes_per_unit=dk["unit"],
+                avg_launch_ms=round(dk["ms"] / nlaunch, 4),
+                launches=int(nlaunch), units_per_launch=units_launch)
     names = ["model_rfft", "xspec", "guess", "solve"]
     stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
     kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),
-                       avg_launch_ms=round(float(v["ms"]) / ncalls, 4),
+                       launches=int(v.get("launches", ncalls)),
+                       avg_launch_ms=round(float(v["ms"]) /
+                                           max(1, v.get("launches", ncalls)), 4),
                        gbs=(None if not v["ms"] else
                             round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
                for k, v in kern.items()}

@@ -176,6 +176,11 @@ int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms);
  * moment-mode sub-int; 0 if the call had none), [1] the guess-profile pass
  * (k_dsum_w; 0 without a guess).  Same event ring as ppf_stage_ms_history. */
 int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms);
+/* The streaming passes (k_pass: one trust-region evaluation of every
+ * scattering fit still iterating) of the last n profiled ppf_fit_batch calls
+ * into ms[n][2]: [0] their summed duration in ms (HIP events around each
+ * launch), [1] the number of launches. */
+int ppf_pass_ms_history(ppf_ctx *ctx, int n, double *ms);
 
 /* Workspace needed by ppf_fit_batch for `desc` (only sizes/flags are read). */
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc);

@@ -1,16 +1,21 @@
 #!/usr/bin/env python
-"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py to
-per-unit HBM traffic (profiles/pmc_summary.json, read by bench.py).
+"""Reduce the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of a
+tools/prof.sh run of bench.py to HBM traffic per unit of work
+(profiles/pmc_summary.json, read by bench.py for `roofline.traffic`).
 
-    python profiles/pmc_reduce.py <fetch_dir> <write_dir> <bench_json_log> \
-        [--nchan 512] [--out profiles/pmc_summary.json]
+    python profiles/pmc_reduce.py gpurun_out/prof_TAG [--out ...]
 
 Counter handling follows MI355X_MICROARCH.md (HBM section): counters are in
 KiB; FETCH_SIZE counts half of the bytes of wide coalesced streaming reads on
-gfx950, so it is doubled; WRITE_SIZE is taken as is.  Unit: one
-sub-integration; a launch processes `chunk` sub-integrations (bench config).
-  xmom -- the first (full) fused moment pass k_xmom_g<*, *, *, true>
-  dsum -- the guess-profile pass k_dsum_w
+gfx950, so it is doubled; WRITE_SIZE is taken as is.  Entries are keyed by
+the bench fit mode (phase+DM, full, scat) and kernel:
+  xmom  -- the first (full) fused moment pass k_xmom_g<*, *, *, true>;
+           unit = one sub-integration
+  dsum  -- the guess-profile pass k_dsum_w; unit = one sub-integration
+  xspec -- the cross-spectrum pass k_xspec_w; unit = one sub-integration
+  pass  -- the streaming trust-region evaluation k_pass<true>; unit = one
+           evaluation of one sub-integration (the run's launches process
+           nsub x mean_passes_per_fit evaluations per call)
 """
 import argparse
 import collections
@@ -18,6 +23,9 @@ import csv
 import glob
 import json
 import os
+
+KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
+           "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", "")}
 
 
 def load(d):
@@ -29,46 +37,51 @@ def load(d):
     return rows
 
 
-def pick(rows, key):
-    return [r for k, v in rows.items() if key in k for r in v]
-
-
-KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", "")}
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("fetch_dir")
-    ap.add_argument("write_dir")
-    ap.add_argument("bench_log")
+    ap.add_argument("prof_dir")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(
         os.path.abspath(__file__)), "pmc_summary.json"))
     a = ap.parse_args()
-    line = [l for l in open(a.bench_log) if l.startswith("{")][-1]
+    line = [ln for ln in open(os.path.join(a.prof_dir, "ks.log"))
+            if ln.startswith("{")][-1]
     bench = json.loads(line)
-    per_launch = min(bench["config"]["chunk"], bench["config"]["nsub_per_gpu"])
-    fr, wr = load(a.fetch_dir), load(a.write_dir)
+    cfg = bench["config"]
+    mode = cfg["fit"]
+    calls = bench["steps"] + bench["warmup"]
+    per_launch = min(cfg["chunk"], cfg["nsub_per_gpu"])
+    fr = load(os.path.join(a.prof_dir, "fetch"))
+    wr = load(os.path.join(a.prof_dir, "write"))
     KiB = 1024.0
-    out = dict(source=dict(fetch=a.fetch_dir, write=a.write_dir,
-                           bench=bench["config"]["workload"],
+    old = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    out = old if "modes" in old else {"modes": {}}
+    ent = dict(source=dict(prof=a.prof_dir, bench=cfg["workload"],
                            correction="FETCH_SIZE x2 (gfx950 wide reads), "
                                       "WRITE_SIZE x1, KiB -> bytes"),
                kernels={})
     for key, (pre, post) in KERNELS.items():
-        sel = lambda rows: [r for k, v in rows.items()
-                            if pre in k and post in k for r in v]
+        def sel(rows):
+            return [r for k, v in rows.items() if pre in k and post in k
+                    for r in v]
         f, w = sel(fr), sel(wr)
         if not f or not w:
             continue
-        fb = sum(float(r["Counter_Value"]) for r in f) * KiB * 2 / len(f)
-        wb = sum(float(r["Counter_Value"]) for r in w) * KiB / len(w)
-        out["kernels"][key] = dict(
-            unit="sub-integration", subints_per_launch=per_launch,
-            fetch_bytes=fb / per_launch, write_bytes=wb / per_launch,
-            hbm_bytes=(fb + wb) / per_launch, launches=len(f),
+        fb = sum(float(r["Counter_Value"]) for r in f) * KiB * 2
+        wb = sum(float(r["Counter_Value"]) for r in w) * KiB
+        if key == "pass":
+            units = calls * cfg["nsub_per_gpu"] * bench["mean_passes_per_fit"]
+            unit = "sub-integration evaluation"
+        else:
+            units = len(f) * per_launch
+            unit = "sub-integration"
+        ent["kernels"][key] = dict(
+            unit=unit, units=units, launches=len(f),
+            fetch_bytes=fb / units, write_bytes=wb / units,
+            hbm_bytes=(fb + wb) / units,
             kernel=sorted({r["Kernel_Name"] for r in f}))
+    out["modes"][mode] = ent
     json.dump(out, open(a.out, "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    print(json.dumps(ent, indent=1))
 
 
 if __name__ == "__main__":

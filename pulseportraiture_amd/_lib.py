@@ -78,6 +78,7 @@ SIGNATURES = {
     "ppf_last_stage_ms": (ctypes.c_int, [_vp, _vp]),
     "ppf_stage_ms_history": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_kernel_ms_history": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+    "ppf_pass_ms_history": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_fit_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(FitDesc)]),
     "ppf_fit_batch": (ctypes.c_int, [_vp, ctypes.POINTER(FitDesc), _vp]),
     "ppf_fit2_batch": (ctypes.c_int, [_vp, ctypes.POINTER(FitDesc), _vp]),

@@ -10,6 +10,8 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/ppfit.h"
 #include "ppf_internal.hpp"
@@ -27,6 +29,10 @@ struct ppf_ctx {
     static constexpr int kEv = 9;
     hipEvent_t ring[kRing][kEv] = {};
     bool ran[kRing][6] = {};
+    // every streaming pass (k_pass) of a call: its (start, end) event pairs,
+    // the pool grown on demand and reused by the ring slot
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pass_ev[kRing];
+    int npass[kRing] = {};
     long ncalls = 0;
     unsigned *host_active = nullptr;   // pinned, for the iteration loop
 };
@@ -183,6 +189,11 @@ void ppf_destroy(ppf_ctx *ctx) {
     for (auto &set : ctx->ring)
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
+    for (auto &v : ctx->pass_ev)
+        for (auto &pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
     if (ctx->host_active) (void)hipHostFree(ctx->host_active);
     delete ctx;
 }
@@ -242,6 +253,29 @@ int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms) {
     return n;
 }
 
+int ppf_pass_ms_history(ppf_ctx *ctx, int n, double *ms) {
+    if (!ctx || !ms || n < 0) return PPF_EINVAL;
+    if (!ctx->prof) return fail(ctx, PPF_EINVAL, "profiling is off");
+    long avail = ctx->ncalls < ppf_ctx::kRing ? ctx->ncalls : ppf_ctx::kRing;
+    if (n > avail) n = (int)avail;
+    for (int c = 0; c < n; ++c) {
+        int slot = (int)((ctx->ncalls - n + c) % ppf_ctx::kRing);
+        double tot = 0.0;
+        for (int i = 0; i < ctx->npass[slot]; ++i) {
+            const auto &pr = ctx->pass_ev[slot][i];
+            hipError_t e = hipEventSynchronize(pr.second);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+            float t = 0.f;
+            e = hipEventElapsedTime(&t, pr.first, pr.second);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+            tot += (double)t;
+        }
+        ms[c * 2 + 0] = tot;
+        ms[c * 2 + 1] = (double)ctx->npass[slot];
+    }
+    return n;
+}
+
 int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4) {
     int n = ppf_stage_ms_history(ctx, 1, ms4);
     if (n < 0) return n;
@@ -275,6 +309,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         if (ctx->prof) (void)hipEventRecord(ctx->ring[slot][i], st);
     };
     for (int i = 0; i < 4; ++i) ctx->ran[slot][i] = true;
+    ctx->npass[slot] = 0;
     ctx->ran[slot][2] = d->guess != 0;
     ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
@@ -413,7 +448,23 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     int iter = 0;
     for (int group = sa.moments ? 3 : 6; any_mom || any_pass; group = sa.moments ? 2 : 4) {
         for (int g = 0; g < group; ++g) {
-            if (any_pass && (e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
+            if (any_pass) {
+                std::pair<hipEvent_t, hipEvent_t> *pe = nullptr;
+                if (ctx->prof) {
+                    auto &v = ctx->pass_ev[slot];
+                    if ((int)v.size() <= ctx->npass[slot]) {
+                        std::pair<hipEvent_t, hipEvent_t> pr{};
+                        if ((e = hipEventCreate(&pr.first)) != hipSuccess ||
+                            (e = hipEventCreate(&pr.second)) != hipSuccess)
+                            return hip_fail(ctx, e, "hipEventCreate");
+                        v.push_back(pr);
+                    }
+                    pe = &v[ctx->npass[slot]++];
+                    (void)hipEventRecord(pe->first, st);
+                }
+                if ((e = ppf::launch_pass(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_pass");
+                if (pe) (void)hipEventRecord(pe->second, st);
+            }
             if (sa.moments && any_mom) {
                 const bool full = iter == 0 && g == 0;
                 if (full && fused) mark(5);

@@ -62,20 +62,21 @@ def _worker_stream(dev):
 
 
 class _Staged(object):
-    def __init__(self, t, ev):
-        self.t, self.ev = t, ev
+    def __init__(self, fut):
+        self.fut = fut
 
     def wait(self):
         """The uploaded rows, ordered after the upload on the caller's
         current stream."""
-        if self.ev is not None:
-            cur = torch.cuda.current_stream(self.t.device)
-            cur.wait_event(self.ev)
-            self.t.record_stream(cur)
-        return self.t
+        t, ev = self.fut.result()
+        if ev is not None:
+            cur = torch.cuda.current_stream(t.device)
+            cur.wait_event(ev)
+            t.record_stream(cur)
+        return t
 
     def release(self):
-        self.t = self.ev = None
+        self.fut = None
 
 
 class _Stager(object):
@@ -83,45 +84,55 @@ class _Stager(object):
     two pinned host buffers (float32 when every amplitude survives the round
     trip, as PSRCHIVE stores them) and uploaded asynchronously on a copy
     stream, so the upload of archive i+1 overlaps the fit of archive i; a
-    buffer is reused only after its previous upload has completed."""
+    buffer is reused only after its previous upload has completed.  The
+    copy into pinned memory and the upload run on a thread of their own, so
+    the caller goes on to the next archive's host work at once."""
 
     def __init__(self):
         self.bufs, self.events, self.k = [None, None], [None, None], 0
         self.stream = None
+        self.pool = ThreadPoolExecutor(max_workers=1)
 
     def stage(self, rows):
+        """rows: an array [n, nchan, nbin] or a view of one (no copy is
+        made before the one into pinned memory, which runs on torch's CPU
+        thread pool: a single-threaded numpy copy of a 268 MB archive costs
+        ~25 ms, more than its fit)."""
         dev = engine.device()
-        rows = np.asarray(rows)
-        if rows.dtype != np.float32:
-            r32 = rows.astype(np.float32)
-            if np.array_equal(r32, rows):
-                rows = r32
-            else:
-                rows = np.asarray(rows, dtype=np.float64)
-        if rows.size == 0:
-            return _Staged(torch.zeros(rows.shape, dtype=torch.float32,
-                                       device=dev), None)
+        return _Staged(self.pool.submit(self._stage, np.asarray(rows), dev))
+
+    def _stage(self, rows, dev):
+        src = torch.from_numpy(rows)
+        if src.dtype != torch.float32:
+            src = src.to(torch.float64)
+            s32 = src.to(torch.float32)
+            if bool(torch.equal(s32.to(torch.float64), src)):
+                src = s32
+        if src.numel() == 0:
+            return torch.zeros(tuple(src.shape), dtype=torch.float32,
+                               device=dev), None
         k = self.k
         self.k ^= 1
         if self.events[k] is not None:
             self.events[k].synchronize()
-        need = rows.nbytes
+        need = src.numel() * src.element_size()
         if self.bufs[k] is None or self.bufs[k].numel() < need:
             self.bufs[k] = torch.empty(need, dtype=torch.uint8,
                                        pin_memory=True)
-        tdt = torch.float32 if rows.dtype == np.float32 else torch.float64
-        host = self.bufs[k][:need].view(tdt).view(rows.shape)
-        np.copyto(host.numpy(), rows)
-        if self.stream is None:
-            self.stream = torch.cuda.Stream(dev)
-        with torch.cuda.stream(self.stream):
-            t = host.to(dev, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
+        host = self.bufs[k][:need].view(src.dtype).view(src.shape)
+        host.copy_(src)
+        with torch.cuda.device(dev):
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(self.stream):
+                t = host.to(dev, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
         self.events[k] = ev
-        return _Staged(t, ev)
+        return t, ev
 
     def close(self):
+        self.pool.shutdown(wait=True)
         for ev in self.events:
             if ev is not None:
                 ev.synchronize()
@@ -204,7 +215,7 @@ class GetTOAs(object):
         self.quiet = quiet
 
     # ------------------------------------------------------------------
-    def _models(self, d, ok_isubs, fit_scat, quiet):
+    def _models(self, d, ok_isubs, fit_scat, quiet, host=True):
         """Model portrait per sub-integration (pptoas.py:385-419): the
         .gmodel is parsed once (read_model, pplib.py:2971-3057) and every
         distinct (frequency set, TAU [bin]) portrait of the archive is built
@@ -217,7 +228,7 @@ class GetTOAs(object):
         except (UnboundLocalError, UnicodeDecodeError):
             # a make_spline_model template (pptoas.py:416-419): one device
             # portrait per distinct frequency set, unscattered
-            return self._spline_models(d, ok_isubs)
+            return self._spline_models(d, ok_isubs, host)
         if fit_scat:
             (self.model_code, self.model_nu_ref, self.gparams,
              self.alpha) = code, nu_ref, gparams, alpha
@@ -240,10 +251,11 @@ class GetTOAs(object):
                 np.zeros(0, dtype=np.int32)
         models = engine.gauss_portraits(
             code, np.stack(prms), 0.0 if fit_scat else alpha,
-            np.stack(freqs), nu_ref, nbin).cpu().numpy()
-        return models, np.array(index, dtype=np.int32)
+            np.stack(freqs), nu_ref, nbin)
+        return (models.cpu().numpy() if host else models,
+                np.array(index, dtype=np.int32))
 
-    def _spline_models(self, d, ok_isubs):
+    def _spline_models(self, d, ok_isubs, host=True):
         """read_spline_model(modelfile, freqs, nbin) per sub-integration
         (pptoas.py:416-419), the distinct frequency sets of the archive in
         ONE ppf_spline_portrait_batch launch."""
@@ -262,8 +274,9 @@ class GetTOAs(object):
             return np.zeros((0, len(d.freqs[0]), nbin)), \
                 np.zeros(0, dtype=np.int32)
         models = engine.spline_portraits(mean_prof, eigvec, tck,
-                                         np.stack(freqs), nbin).cpu().numpy()
-        return models, np.array(index, dtype=np.int32)
+                                         np.stack(freqs), nbin)
+        return (models.cpu().numpy() if host else models,
+                np.array(index, dtype=np.int32))
 
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None,
                  bary=True, fit_DM=True, fit_GM=False, fit_scat=False,
@@ -414,7 +427,14 @@ class GetTOAs(object):
                 len(d.ok_isubs), d.integration_length / nsub))
         ok_isubs = list(d.ok_isubs)
         nok = len(ok_isubs)
-        models, model_index = self._models(d, ok_isubs, fit_scat, quiet)
+        # the portraits stay in HBM: the fit worker orders itself after
+        # their generation on this thread's stream (models_ev)
+        models, model_index = self._models(d, ok_isubs, fit_scat, quiet,
+                                           host=False)
+        models_ev = None
+        if isinstance(models, torch.Tensor) and models.is_cuda:
+            models_ev = torch.cuda.Event()
+            models_ev.record(torch.cuda.current_stream(models.device))
         # ---- gather the batch (pptoas.py:384-529) --------------------
         mask = np.zeros((nok, nchan), dtype=np.uint8)
         init = np.zeros((nok, 5))
@@ -481,13 +501,20 @@ class GetTOAs(object):
             flags_b[j] = fit_flags
         rank, world = _rank_world()
         first, count = _dist.shard(nok, rank, world)
-        rows = np.asarray(d.subints)[ok_isubs[first:first + count], 0] \
-            if count else np.zeros((0, nchan, nbin))
+        sel = ok_isubs[first:first + count]
+        if count and sel == list(range(sel[0], sel[0] + count)):
+            # contiguous sub-ints (the usual case): a view, no gather copy
+            rows = np.asarray(d.subints)[sel[0]:sel[0] + count, 0]
+        elif count:
+            rows = np.asarray(d.subints)[sel, 0]
+        else:
+            rows = np.zeros((0, nchan, nbin))
         return dict(iarch=iarch, datafile=datafile, d=d, nsub=nsub,
                     dev=engine.device(),
                     nchan=nchan, nbin=nbin, obs=obs, nu_fits_a=nu_fits_a,
                     nu_refs_a=nu_refs_a, MJDs=MJDs, DM_stored=DM_stored,
                     DM0=DM0, ok_isubs=ok_isubs, nok=nok, models=models,
+                    models_ev=models_ev,
                     model_index=model_index, mask=mask, init=init,
                     flags_b=flags_b, nu_fit_b=nu_fit_b, nu_out_b=nu_out_b,
                     guess_tau=guess_tau, first=first, count=count,
@@ -508,6 +535,10 @@ class GetTOAs(object):
         nccl = _dist.backend() == "nccl"
         with torch.cuda.device(dev), torch.cuda.stream(_worker_stream(dev)):
             data_t = job["staged"].wait()
+            if job.get("models_ev") is not None:
+                cur = torch.cuda.current_stream(dev)
+                cur.wait_event(job["models_ev"])
+                job["models"].record_stream(cur)
             err = None
             try:
                 table = self._fit_share(job, ctx, data_t, isubs, sl, dev)
@@ -558,6 +589,8 @@ class GetTOAs(object):
         MJDs, DM0 = job["MJDs"], job["DM0"]
         ok_isubs, nok = job["ok_isubs"], job["nok"]
         models, model_index = job["models"], job["model_index"]
+        if ctx["print_flux"] and isinstance(models, torch.Tensor):
+            models = models.cpu().numpy()
         mask, flags_b = job["mask"], job["flags_b"]
         fit_duration = job["fit_duration"]
         batch_duration = r["batch_duration"]

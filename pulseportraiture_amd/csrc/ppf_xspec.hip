@@ -134,7 +134,13 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
         kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
     }
 
-    auto usable = [&](int n) { return n < cend && (!mask || mask[n]); };
+    // the block's channel mask in lane registers (a.cb <= 64): testing the
+    // next channel needs no global load (whose vmcnt wait would also wait
+    // for every load issued before it)
+    const int mlane = (cbase + lane < cend && (!mask || mask[cbase + lane])) ? 1 : 0;
+    auto usable = [&](int n) {
+        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
+    };
     RowT zr[R];
     auto fetch = [&](int n) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
@@ -154,7 +160,9 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
             double2 x[R];
 #pragma unroll
             for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-            if (usable(n + kXW)) fetch(n + kXW);       // next row in flight during this FFT
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            const bool nxt = usable(n + kXW);
+            if (nxt) fetch(n + kXW);                   // next row in flight during this FFT
             wfft::fft_row<LOG2N>(x, buf, a.T, lane);
 
             // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
@@ -190,7 +198,6 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
 
-            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
             {
                 // in place: X_k -> pad(k), X_{N-k} -> pad(N-k); the pair
                 // (0, N) keeps X_N in pad(N/2) (read above as Dm)
@@ -201,6 +208,9 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
                     double2 Dlo, Dhi;
                     rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
                     w = cmul(w, w_step);
+                    // (loading these before the next row's prefetch, so their
+                    // in-order wait skips it, was measured: the extra
+                    // registers cost occupancy, C5 29.7 -> 33.2 ms)
                     const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
                     buf[wfft::pad<LOG2N>(klo)] =
                         (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Build an experimental libppfit variant: tools/build_variant.sh NAME "-DMACRO=1 ..."
-# -> build/variants/libppfit_NAME.so (select with PPFIT_LIB=...)
+# -> varlib/libppfit_NAME.so (select with PPFIT_LIB=...)
 set -e
 name=$1; shift
 flags="$*"
 root=$(cd $(dirname $0)/.. && pwd)
-od=$root/build/variants/$name
+od=$root/varlib/tmp_$name
 mkdir -p $od
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed -ffp-contract=fast -munsafe-fp-atomics $flags"
 C=$root/pulseportraiture_amd/csrc
@@ -14,6 +14,6 @@ $H -c $C/ppf_xspec.hip -o $od/x.o &
 $H -c $C/ppf_solve.hip -o $od/s.o &
 $H -x hip -c $C/ppf_api.cpp -o $od/a.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/build/variants/libppfit_$name.so $od/k.o $od/x.o $od/s.o $od/a.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/varlib/libppfit_$name.so $od/k.o $od/x.o $od/s.o $od/a.o
 rm -rf $od
-echo built build/variants/libppfit_$name.so
+echo built varlib/libppfit_$name.so

@@ -26,8 +26,8 @@ def main():
     get(out.ctypes.data, 1)
     bench.main()
     get(out.ctypes.data, 1)
-    names = ["load issue", "fft", "pair+noise", "barrier1", "mfma issue", "epilogue", "wait+convert"]
-    tot = float(out[:7].sum())
+    names = os.environ.get("XP_NAMES", "load issue,fft,pair+noise,barrier1,mfma issue,epilogue,wait+convert,-").split(",")
+    tot = float(out[:8].sum())
     for i, nm in enumerate(names):
         print("%-14s %14d  %5.1f%%" % (nm, out[i], 100.0 * out[i] / tot))
 

@@ -4,5 +4,5 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-PPFIT_LIB=build/variants/libppfit_xprof.so timeout -k 10 200 python tools/xprof.py > gpurun_out/xprof_$1.log 2>&1
-bash tools/var_bench.sh $1 "--nsub 2500 --steps 2 --warmup 1 --passes 2" build/variants/libppfit_*.so > gpurun_out/sens_$1.log 2>&1
+PPFIT_LIB=varlib/libppfit_xprof.so timeout -k 10 200 python tools/xprof.py > gpurun_out/xprof_$1.log 2>&1
+bash tools/var_bench.sh $1 "--nsub 2500 --steps 2 --warmup 1 --passes 2" varlib/libppfit_*.so > gpurun_out/sens_$1.log 2>&1

@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 METRIC = ("subint portrait fits/sec (phase+DM, 512ch×2048bin) at "
           "1/2/4/8 MI355X")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TF = 78.6            # MI355X spec: FP64 vector = FP64 matrix = 78.6 TFLOPS (half the 157.3 FP32 rate, MI355X_MICROARCH.md)
 
 
 def parse():
@@ -606,6 +607,25 @@ def main():
                 algorithmic_bytes_per_unit=dk["unit"],
                 avg_launch_ms=round(dk["ms"] / nlaunch, 4),
                 launches=int(nlaunch), units_per_launch=units_launch)
+    # fp64 issue roofline of the same kernel: flops per unit from the SQ
+    # counter passes (profiles/fp64_reduce.py: f64 VALU add/mul/fma/trans x 64
+    # lanes, fma x 2, + 512 per f64 MFMA MOP) x the units of one launch / the
+    # launch's event-timed duration, against the fp64 peak
+    fp64 = None
+    fpath = os.path.join(ROOT, "profiles", "fp64_summary.json")
+    if os.path.exists(fpath):
+        fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
+        fk = fm.get("kernels", {}).get(dom)
+        if fk:
+            tf = fk["flops_per_unit"] * units_launch / (dk["ms"] / nlaunch / 1e3) / 1e12
+            fp64 = dict(bound="fp64", achieved=round(tf, 2), peak=FP64_PEAK_TF,
+                        unit="TFLOP/s", frac=round(tf / FP64_PEAK_TF, 4),
+                        flops_per_unit=round(fk["flops_per_unit"]),
+                        valu_f64_per_unit=round(fk["valu_f64_per_unit"]),
+                        mfma_f64_per_unit=round(fk["mfma_f64_per_unit"], 1),
+                        valu_active_per_wave=fk.get("valu_active_per_wave"),
+                        clock_ghz=fk.get("clock_ghz"),
+                        source=os.path.relpath(fpath, ROOT))
     names = ["model_rfft", "xspec", "guess", "solve"]
     stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
     kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),
@@ -639,7 +659,7 @@ def main():
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),
-               roofline=roof, stage_ms=stages, kernels=kernels,
+               roofline=roof, fp64_roofline=fp64, stage_ms=stages, kernels=kernels,
                mean_passes_per_fit=round(mean_passes, 3),
                mean_evals_per_fit=round(mean_nfev, 3),
                fits_converged_frac=round(float(np.mean(

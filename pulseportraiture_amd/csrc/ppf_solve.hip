@@ -305,7 +305,20 @@ template <bool SCAT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS_WPE))) void k_pass(SolveArgs a) {
     __shared__ double red[kWaves * 21];
     const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
-    const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+    // channel-block-major order: the workgroups resident together share one
+    // block of |M|^2 (nharm x 256 channels, read by every sub-int's pass)
+    // instead of each streaming its own.  With nblk a multiple of 8 the
+    // blocks of one XCD (workgroups b = x mod 8) take nblk / 8 channel blocks
+    // for all sub-ints, so that XCD's L2 holds its |M|^2 share.
+    int s, blk;
+    if (nblk % 8 == 0) {
+        const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
+        blk = x * (nblk >> 3) + r / a.nsub;
+        s = r % a.nsub;
+    } else {
+        blk = blockIdx.x / a.nsub;
+        s = blockIdx.x % a.nsub;
+    }
     const TRState &S = a.state[s];
     if (S.phase == PH_DONE || S.scat != (SCAT ? 1 : 0) || S.mmode) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -595,7 +595,8 @@ def main():
     units_launch = (steps_subints if "launches" not in dk else
                     steps_subints * mean_passes) / nlaunch
     traffic = None
-    if os.path.exists(args.pmc):
+    # (the PMC / SQ summaries are of the default, cut configuration)
+    if os.path.exists(args.pmc) and not args.no_hcut:
         pm = json.load(open(args.pmc)).get("modes", {}).get(args.fit, {})
         pk = pm.get("kernels", {}).get(dom)
         if pk:
@@ -613,7 +614,7 @@ def main():
     # launch's event-timed duration, against the fp64 peak
     fp64 = None
     fpath = os.path.join(ROOT, "profiles", "fp64_summary.json")
-    if os.path.exists(fpath):
+    if os.path.exists(fpath) and not args.no_hcut:
         fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
         fk = fm.get("kernels", {}).get(dom)
         if fk:

@@ -275,6 +275,14 @@ def bench_align(args):
     dist.barrier()
     dt = dist.max_over_ranks(time.perf_counter() - t0, dev)
     value = total * args.steps / dt
+    fitstats = {}
+    lr = R.__dict__.get("_dev_inputs", {}).get("last_results")
+    if lr is not None:
+        from pulseportraiture_amd import _lib
+        I = _lib.RESULT_INDEX
+        lr = lr.cpu().numpy()
+        fitstats = dict(mean_passes_per_fit=round(float(lr[:, I["npass"]].mean()), 3),
+                        mean_evals_per_fit=round(float(lr[:, I["nfeval"]].mean()), 3))
     out = dict(metric="archive fits+aligns/sec (ppalign iteration, %dch×"
                       "%dbin) at 1/2/4/8 MI355X" % (nchan, nbin),
                value=round(value, 2), unit="archive-iterations/s",
@@ -290,7 +298,7 @@ def bench_align(args):
                            nsub_per_gpu=args.nsub, nchan=nchan, nbin=nbin,
                            fit="align", parallelism="dp%d" % world),
                roofline=None, cpu_baseline=None,
-               template_peak=float(torch.as_tensor(m).abs().max()))
+               template_peak=float(torch.as_tensor(m).abs().max()), **fitstats)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()

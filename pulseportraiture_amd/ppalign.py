@@ -260,6 +260,7 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
         guess_Ns=nbin, dev=dev, guess_ref=1)   # ppalign.py:214-219: at nu_fit
     I = _lib.RESULT_INDEX
     r = res["results"]
+    dc["last_results"] = r               # (diagnostics: bench.py --fit align)
     st = r[:, I["status"]].to(torch.int64).cpu().numpy()
     bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
     if len(bad):

@@ -59,9 +59,16 @@ enum ppf_status {
 
 /* ppf_fit_desc.options bits */
 enum ppf_option {
-    PPF_OPT_NO_HCUT = 1      /* sum every harmonic: no per-channel cutoff of
+    PPF_OPT_NO_HCUT = 1,     /* sum every harmonic: no per-channel cutoff of
                                 the harmonics whose template power is below
                                 1e-28 of the channel's peak */
+    PPF_OPT_NO_X = 2         /* the caller has checked that no sub-int
+                                streams the cross spectrum (no scattering
+                                flag, zero initial tau): on the fused
+                                phase+DM path no X slot is reserved and the
+                                cross-spectrum pass is not launched (a
+                                sub-int that would need X ends with
+                                PPF_ST_NOSPACE) */
 };
 
 enum ppf_mode {

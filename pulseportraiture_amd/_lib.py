@@ -21,6 +21,7 @@ ST_SUCCESS, ST_MAXITER, ST_CONVERGED, ST_LINALG = 0, 1, 2, 3
 ST_NO_ROOT, ST_SINGULAR, ST_NONFINITE, ST_NOFIT = 0x100, 0x200, 0x400, 0x800
 ST_NOSPACE = 0x1000
 OPT_NO_HCUT = 1           # ppf_fit_desc.options
+OPT_NO_X = 2
 ABI_VERSION = 2
 
 # ppf_result: 32 doubles (include/ppfit.h)

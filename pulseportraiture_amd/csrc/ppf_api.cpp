@@ -107,6 +107,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
     L.fused = ppf::xspec_wave_supported(ilog2(d->nbin / 2), L.cb) ? 1 : 0;
     L.xcap = (L.fused && d->x_subints > 0 && d->x_subints < d->nsub) ? d->x_subints : d->nsub;
+    if (L.fused && (d->options & PPF_OPT_NO_X)) L.xcap = 0;
     L.cbd = d->nchan < 128 ? d->nchan : 128;          // k_dsum channel block
     L.nblkd = (d->nchan + L.cbd - 1) / L.cbd;
     size_t o = 0;
@@ -354,7 +355,11 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // fused: only k_pass reads X, and only below its channels' cutoffs
     xa.KC = fused ? (const int32_t *)(ws + L.KC) : nullptr;
     if (wave) {
-        if ((e = ppf::launch_xspec_wave(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec_w");
+        // (nothing to do when the caller has ruled out X: every sub-int is
+        // fitted from k_xmom_g's moments)
+        if (!(fused && L.xcap == 0) &&
+            (e = ppf::launch_xspec_wave(xa, st)) != hipSuccess)
+            return hip_fail(ctx, e, "k_xspec_w");
     } else {
         if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
     }

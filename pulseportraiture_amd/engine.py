@@ -211,7 +211,8 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.guess_weights, d.guess_DM = pp(per_sub["gw"]), pp(per_sub["gdm"])
     d.guess_tau = pp(per_sub["gtau"])
     d.x_subints = int(max(n_x, 1)) if n_x < (c1 - c0) else 0
-    d.options = _lib.OPT_NO_HCUT if cfg["no_hcut"] else 0
+    d.options = (_lib.OPT_NO_HCUT if cfg["no_hcut"] else 0) | \
+        (_lib.OPT_NO_X if n_x == 0 else 0)
     d.guess_ref = int(cfg["guess_ref"])
     return d
 

@@ -48,12 +48,21 @@ def test_workspace_query_and_validation_without_gpu():
     d.x_subints = 2
     nb2 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     assert nb - nb2 == 8 * 512 * 1025 * 16
+    # PPF_OPT_NO_X (the caller ruled X out, engine.fit_batch when
+    # x_subints() == 0): no slot at all on the fused path
+    d.options = _lib.OPT_NO_X
+    nb0 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    assert nb2 - nb0 == 2 * 512 * 1025 * 16
+    d.options = 0
     # off the fused path (nbin 4096: block FFT, moments taken from X) every
     # sub-int streams X whatever x_subints says
     d.nbin = 4096
     nb3 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     d.x_subints = 0
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == nb3
+    d.options = _lib.OPT_NO_X          # ignored off the fused path
+    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == nb3
+    d.options = 0
     d.nbin = 1000   # not a power of two
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0
     # a NULL context is rejected before touching the device

@@ -1,5 +1,5 @@
 """Section cycle profile of k_xmom_g from a PPF_XM_PROF build:
-PPFIT_LIB=build/variants/libppfit_xprof.so python tools/xprof.py
+PPFIT_LIB=varlib/libppfit_xprof.so python tools/xprof.py (tools/build_variant.sh xprof -DPPF_XM_PROF=1)
 Runs bench.py's workload for one 2500-sub-int chunk (after a warmup call) and
 prints the cycles per section summed over all waves (shader clock)."""
 import ctypes

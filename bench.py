@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="processes for the all-core CPU aggregate (the GPU "
                     "box's CPU share is 16)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend at N > 1 (nccl = RCCL; gloo "
+                    "only to rehearse several ranks on one GPU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles",
                                                   "pmc_summary.json"))
     return ap.parse_args()
@@ -226,7 +229,7 @@ def bench_align(args):
     from types import SimpleNamespace
     from pulseportraiture_amd import dist, engine, ppalign, synth
     from pulseportraiture_amd.pplib import guess_fit_freq
-    rank, world, local = dist.init("nccl")
+    rank, world, local = dist.init(args.dist_backend)
     dev = torch.device("cuda", local)
     total = args.nsub * world
     first, count = dist.shard(total, rank, world)
@@ -340,7 +343,7 @@ def bench_gettoas(args):
     import torch
     from pulseportraiture_amd import dist, engine, pptoas, synth
     from pulseportraiture_amd.pplib import DataBunch, get_bin_centers
-    rank, world, local = dist.init("nccl")
+    rank, world, local = dist.init(args.dist_backend)
     dev = torch.device("cuda", local)
     nchan, nbin, per = args.nchan, args.nbin, args.arch_nsub
     nfile = max(1, args.nsub // per)
@@ -425,7 +428,7 @@ def main():
     import torch
     from pulseportraiture_amd import _lib, dist, engine, synth
     from pulseportraiture_amd.pplib import guess_fit_freq
-    rank, world, local = dist.init("nccl")
+    rank, world, local = dist.init(args.dist_backend)
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world),
               file=sys.stderr)

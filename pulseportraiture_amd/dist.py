@@ -51,6 +51,8 @@ def allgather_rows(local, n_total, world):
     collective, then trimmed)."""
     if world == 1:
         return local
+    if local.is_cuda and backend() == "gloo":      # (rehearsals: gloo is CPU-only)
+        return allgather_rows(local.cpu(), n_total, world).to(local.device)
     per = -(-n_total // world)
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
@@ -74,6 +76,8 @@ def max_over_ranks(x, device=None):
     """Max of a python float over ranks (used for timings)."""
     if not dist.is_initialized():
         return x
+    if backend() == "gloo":
+        device = None
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -89,7 +93,12 @@ def allreduce_sum_(*tensors):
     if not is_dist():
         return tensors
     for t in tensors:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if t.is_cuda and backend() == "gloo":       # (rehearsals)
+            c = t.cpu()
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return tensors
 
 
@@ -101,6 +110,8 @@ def raise_if_any_failed(err, device=None):
         if err is not None:
             raise err
         return
+    if backend() == "gloo":
+        device = None
     t = torch.tensor([1.0 if err is not None else 0.0], dtype=torch.float64,
                      device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

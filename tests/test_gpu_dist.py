@@ -98,3 +98,35 @@ def test_sharded_gettoas_equals_serial(name):
     for k in KEYS:
         np.testing.assert_array_equal(tabs[k], serial[k], err_msg=k)
     assert slines == lines
+
+
+def _bench_rank(rank, world, port, args):
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0")
+    return subprocess.Popen([sys.executable, os.path.join(
+        os.path.dirname(HERE), "bench.py")] + args, env=env,
+        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+@pytest.mark.parametrize("fit", ["phase+DM", "align"])
+def test_bench_two_ranks_rehearsal(fit):
+    """bench.py's N > 1 path (sharding, the result all-gather, max-over-ranks
+    timing, rank-0 JSON) run as two processes on the box's one GPU over gloo,
+    as the driver's multi-GPU runs use it over RCCL (one rank per GPU)."""
+    import json
+    port = _free_port()
+    args = ["--gpus", "2", "--dist-backend", "gloo", "--nsub", "48",
+            "--nchan", "64", "--nbin", "512", "--steps", "1", "--warmup",
+            "1", "--passes", "1", "--cpu-sample", "0", "--fit", fit]
+    procs = [_bench_rank(r, 2, port, args) for r in range(2)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[0]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert not any(ln.startswith("{") for ln in outs[1].splitlines())
+    if fit == "phase+DM":
+        assert d["fits_converged_frac"] == 1.0

@@ -659,7 +659,7 @@ def main():
                dtype="f64", data="synthetic (device-generated example.gmodel "
                "portraits + white noise; float32 amplitudes)",
                config=dict(workload="configs[%d]: %d subints/GPU x %dch x "
-                           "%dbin, %s wideband fit (GetTOAs path)%s" %
+                           "%dbin, %s wideband fit (GetTOAs fit stage: guess + fit + post-fit of HBM-resident sub-ints; --fit gettoas times the host path)%s" %
                            (FIT["cfg"], args.nsub, nchan, nbin, args.fit,
                             "" if not scat_fit else
                             ", injected tau %g rot at %g MHz" %

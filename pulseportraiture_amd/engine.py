@@ -7,6 +7,7 @@ returns device tensors; the drop-in modules (pplib / pptoaslib / pptoas)
 convert to the reference's numpy/DataBunch forms.
 """
 import ctypes
+import warnings
 
 import numpy as np
 import torch
@@ -36,7 +37,14 @@ def to_dev(x, dev, dtype):
         return None
     if isinstance(x, torch.Tensor):
         return x.to(device=dev, dtype=dtype).contiguous()
-    return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype).to(dev)
+    a = np.ascontiguousarray(x)
+    if not a.flags.writeable:
+        # the host array is only read (copied to the device): torch's
+        # warning about non-writable NumPy memory does not apply
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            return torch.as_tensor(a, dtype=dtype).to(dev)
+    return torch.as_tensor(a, dtype=dtype).to(dev)
 
 
 def _p(t):

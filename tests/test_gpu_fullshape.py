@@ -373,3 +373,41 @@ def test_spline_portrait_matches_reference(name):
     assert got.shape == ref.shape
     np.testing.assert_allclose(got, ref, rtol=0,
                                atol=1e-11 * np.abs(ref).max())
+
+
+@pytest.mark.gpu
+def test_no_x_option_and_x_slots():
+    """PPF_OPT_NO_X (engine.fit_batch with no scattering fit in the batch):
+    phase+DM results are bit-identical to a call that reserves X slots, and
+    a scattering sub-int in a call that promised none, or past the reserved
+    X slots, ends with PPF_ST_NOSPACE instead of reading an unwritten X."""
+    from pulseportraiture_amd import _lib, engine, synth
+    nsub, nchan, nbin = 6, 64, 512
+    b = synth.make_batch(nsub, nchan, nbin, first=4242)
+    init = np.zeros((nsub, 5))
+    init[:, 1] = synth.DM0
+    kw = dict(nu_fits=np.full((nsub, 3), 1500.0),
+              nu_outs=np.full((nsub, 3), np.nan))
+    freqs = np.tile(b["freqs"], (nsub, 1))
+    I = _lib.RESULT_INDEX
+    a = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], freqs, b["P"], init, [1, 1, 0, 0, 0], n_x=0,
+        **kw))
+    c = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], freqs, b["P"], init, [1, 1, 0, 0, 0], n_x=2,
+        **kw))
+    np.testing.assert_array_equal(a["results"], c["results"])
+    assert not (a["results"][:, I["status"]].astype(int) & _lib.ST_NOSPACE).any()
+    flags = np.tile([1, 1, 0, 0, 0], (nsub, 1))
+    flags[2] = [1, 1, 0, 1, 1]
+    flags[4] = [1, 1, 0, 1, 1]
+    init_s = init.copy()
+    init_s[[2, 4], 3] = 1.0 / nbin          # linear tau (log10_tau=False)
+    init_s[[2, 4], 4] = -4.0
+    for n_x, bad in ((0, [2, 4]), (1, [4])):
+        r = engine.results_numpy(engine.fit_batch(
+            b["data"], b["model"], freqs, b["P"], init_s, flags, n_x=n_x,
+            log10_tau=False, **kw))
+        st = r["results"][:, I["status"]].astype(int)
+        got = [i for i in range(nsub) if st[i] & _lib.ST_NOSPACE]
+        assert got == bad, (n_x, st)

@@ -302,6 +302,12 @@ __device__ unsigned long long g_xprof[8];
 __device__ __forceinline__ double bin_centre(double phc, int nbin) {
     return rint(phc * (double)nbin);
 }
+__device__ __forceinline__ double readfirst_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)b, l);
@@ -357,8 +363,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     const bool act = s < a.nsub && st[s].mmode && st[s].need_mom;
     if (!__syncthreads_or(act)) return;                  // uniform per workgroup
     const int q = act ? st[s].mtarget : 0;
-    const double c0 = act ? st[s].mc[q][0] : 0.0, c1 = act ? st[s].mc[q][1] : 0.0,
-                 c2 = act ? st[s].mc[q][2] : 0.0;
+    // wave-uniform: held in SGPRs
+    const double c0 = readfirst_d(act ? st[s].mc[q][0] : 0.0),
+                 c1 = readfirst_d(act ? st[s].mc[q][1] : 0.0),
+                 c2 = readfirst_d(act ? st[s].mc[q][2] : 0.0);
     const int sv = __builtin_amdgcn_readfirstlane(act ? s : 0);
 
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
@@ -369,7 +377,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     const double2 *Mwave = a.Mft + (int64_t)mi * a.nchan * NH;
     const double *Pwave = a.Mpow + (int64_t)mi * a.nchan;
     double *mres = a.mres + ((int64_t)sv * 2 + q) * a.nchan;
-    const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    const double2 w_seed = a.T2[lane];
+    const double2 w_step = cmk(readfirst_d(a.T2[64].x), readfirst_d(a.T2[64].y));
     const double sqrtN = sqrt((double)N);
     double *mom = a.mom + (((int64_t)sv * 2 + q) * a.nchan) * kMoments * 2;
 
@@ -395,9 +404,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         if constexpr (!SH) return;
         const int nn = min(n, a.nchan - 1);
         const double2 *src = Mbase + (int64_t)nn * NH;
+        int tq = tid;                   // opaque: offsets not kept across rounds
+        asm volatile("" : "+v"(tq));
 #pragma unroll
         for (int i = 0; i < MPT; ++i) {
-            const int k = tid + 512 * i;
+            const int k = tq + 512 * i;
             const double2 v = src[k < NH ? k : 0];
             mp[i] = vd2{v.x, v.y};
         }
@@ -491,8 +502,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             // pad(N - k), k = lane + 64 i (k = 0: the pair (0, N) -> pad(0),
             // pad(N/2), read above as Dm)
             double pn = 0.0, pd = 0.0;
+            // the pair's LDS addresses and u_k re-derived from an opaque lane
+            // every round: hoisted out of the channel loop they took ~32
+            // VGPRs, spilled, and each scratch reload waited for the
+            // in-flight row prefetch
+            int lpp = lane;
+            asm volatile("" : "+v"(lpp));
             auto pair = [&](const double2 *Mr, int i, double2 &w) {
-                    const int klo = lane + 64 * i, khi = N - klo;
+                    const int klo = lpp + 64 * i, khi = N - klo;
                     double2 Dlo, Dhi;
                     rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
                     w = cmul(w, w_step);

@@ -285,7 +285,8 @@ def bench_align(args):
         I = _lib.RESULT_INDEX
         lr = lr.cpu().numpy()
         fitstats = dict(mean_passes_per_fit=round(float(lr[:, I["npass"]].mean()), 3),
-                        mean_evals_per_fit=round(float(lr[:, I["nfeval"]].mean()), 3))
+                        mean_evals_per_fit=round(float(lr[:, I["nfeval"]].mean()), 3),
+                        passes_hist=np.bincount(lr[:, I["npass"]].astype(int)).tolist())
     out = dict(metric="archive fits+aligns/sec (ppalign iteration, %dch×"
                       "%dbin) at 1/2/4/8 MI355X" % (nchan, nbin),
                value=round(value, 2), unit="archive-iterations/s",

@@ -91,7 +91,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 
 struct FitLayout {
     size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, MP, KC,
-        needx, xslot, Bt, total;
+        needx, xslot, rclist, Bt, total;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
     int xcap;     // X slots
@@ -127,6 +127,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.needx = o; o += align256(nsub);
     L.xslot = o; o += align256(sizeof(int32_t) * nsub);
+    L.rclist = o; o += align256(sizeof(int32_t) * nsub);
     L.Bt = o;    o += align256(sizeof(double) * (nharm - 1) / 2 * 16);
     if (d->guess) {
         L.gP = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * (size_t)d->nbin);
@@ -411,6 +412,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.state = (ppf::TRState *)(ws + L.state);
     sa.partials = (double *)(ws + L.partials);
     sa.active = (unsigned *)(ws + L.active);
+    sa.rc_count = sa.active + 1;             // reset together with active
+    sa.rc_list = (int32_t *)(ws + L.rclist);
     sa.kinds = (unsigned *)(ws + L.active + 16);
     if (!ctx->host_active) {
         e = hipHostMalloc((void **)&ctx->host_active, 4 * sizeof(unsigned));
@@ -440,6 +443,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ma.mom = (double *)sa.mom;
     ma.Bt = (const double *)(ws + L.Bt);
     ma.kc = kc; ma.errs = d->errs; ma.Mpow = Mpow; ma.mres = sa.mres; ma.nmodel = d->nmodel;
+    ma.rc_count = sa.rc_count; ma.rc_list = sa.rc_list;
     ma.KC = (const int32_t *)(ws + L.KC);
     if (fused && (e = ppf::launch_btab(d->nbin / 2, (double *)(ws + L.Bt), st)) != hipSuccess)
         return hip_fail(ctx, e, "k_btab");
@@ -480,7 +484,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
                     ctx->ran[slot][4] = true;
                 }
             }
-            if ((e = hipMemsetAsync(sa.active, 0, sizeof(unsigned), st)) != hipSuccess)
+            if ((e = hipMemsetAsync(sa.active, 0, 2 * sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");
             if (any_pass && (e = ppf::launch_tr_step(sa, st)) != hipSuccess)
                 return hip_fail(ctx, e, "k_tr_step");

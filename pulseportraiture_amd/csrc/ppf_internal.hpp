@@ -65,6 +65,10 @@ struct XmomArgs {
     const double *Mpow;          // [nmodel][nchan]
     double *mres;                // [nsub][2][nchan] centre residual phi_c,n - s_n/nbin
     const int32_t *KC;           // [nchan] harmonic cutoff of the (single) model, or null
+    // re-centring launches (FULL = false): the sub-ints of rc_list[0..*rc_count)
+    // packed eight to a workgroup; null: every sub-int whose need_mom is set
+    const unsigned *rc_count;
+    const int32_t *rc_list;
 };
 
 struct GuessArgs {
@@ -113,6 +117,8 @@ struct SolveArgs {
     double *dphi;                // [nsub][nchan][2]: d phi_n / d(DM, GM)
     double *mres;                // [nsub][2][nchan]: moment-centre residual per channel
     const int32_t *xslot;        // [nsub] X slot (k_classify; -1 none, -2 no room) or null
+    unsigned *rc_count;          // sub-ints k_tr_mom sent back for a new moment centre
+    int32_t *rc_list;            // [nsub] their indices (slot order of the atomic)
 };
 
 struct RotateArgs {

@@ -652,14 +652,17 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
 //   sum_k Y_k e^{2 pi i k Delta} = e^{i x} sum_m (i x)^m / m! mu_m,
 //   mu_m = sum_k Y_k u_k^m,  and k = h (1 + u) gives the k- and k^2-weighted
 // sums (C', C'') from mu_m + mu_{m+1} and mu_m + 2 mu_{m+1} + mu_{m+2}.
-// kMoments = 32 moments and |x| <= 3.2 bound the truncation of the
-// second-derivative series by 3.2^30 / 30! < 6e-18 of sum_k |Y_k|, so every
+// kMoments = 32 moments and |x| <= 4.5 bound the truncation of the
+// second-derivative series by 4.5^30 / 30! < 1.6e-13 of sum_k |Y_k| (the
+// largest term x^m / m! is 17, so rounding adds < 4e-15), so every
 // trust-region evaluation inside that radius costs O(nchan) instead of a pass
-// over the cross spectrum; a point outside it re-centres (k_moments).
+// over the cross spectrum; a point outside it re-centres (k_moments /
+// k_xmom_g).  (3.2 until round 2: 5e-18, but ppalign fits against a sharp
+// template then re-centred 3.2 times per fit instead of 2.3.)
 // Delta_n includes the per-channel centre residual mres (k_xmom_g rounds the
 // centre to a whole bin, |residual| <= 1/(2 nbin), i.e. |x| <= pi/4).
 // ===========================================================================
-constexpr double kXMax = 3.2;
+constexpr double kXMax = 4.5;
 constexpr int kMomChans = 64;                    // channels per k_moments workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -847,6 +850,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                 L.need_mom = 1;
                 L.nmom += 1;
                 atomicAdd(a.active, 1u);
+                if (a.rc_list) a.rc_list[atomicAdd(a.rc_count, 1u)] = s;
             }
             break;
         }

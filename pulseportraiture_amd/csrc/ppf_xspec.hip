@@ -358,7 +358,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     // SADDR + 32-bit lane offset load form instead of 64-bit VGPR pointers
     // (at 256 VGPRs those spilled, and every scratch reload waited for all
     // outstanding row prefetches)
-    const int s = __builtin_amdgcn_readfirstlane(g * XW + wave);
+    // re-centring launches take the sub-ints k_tr_mom listed, eight to a
+    // workgroup (a sub-int's moments do not depend on its group: MFMA rows
+    // and the fixed-order partial sums are per sub-int)
+    int s = g * XW + wave;
+    if (!FULL && a.rc_list) {
+        const unsigned cnt = *a.rc_count;
+        s = (unsigned)s < cnt ? a.rc_list[s] : a.nsub;
+    }
+    s = __builtin_amdgcn_readfirstlane(s);
     const TRState *st = reinterpret_cast<const TRState *>(a.state);
     const bool act = s < a.nsub && st[s].mmode && st[s].need_mom;
     if (!__syncthreads_or(act)) return;                  // uniform per workgroup

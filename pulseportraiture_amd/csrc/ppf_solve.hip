@@ -663,6 +663,9 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
 // centre to a whole bin, |residual| <= 1/(2 nbin), i.e. |x| <= pi/4).
 // ===========================================================================
 constexpr double kXMax = 4.5;
+// Below |x| = 2.3 the first 24 moments hold the same bound (2.3^22 / 22! <
+// 1.6e-13): the evaluation then skips the last quarter of the moments.
+constexpr double kX24 = 2.3;
 constexpr int kMomChans = 64;                    // channels per k_moments workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -819,6 +822,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
         // moment set whose centre is within the expansion radius for every channel
         int qsel = -1;
+        double xsel = 0.0;
         for (int t = 0; t < 2 && qsel < 0; ++t) {
             const int cand = t == 0 ? L.macc : 1 - L.macc;
             if (!L.mvalid[cand]) continue;
@@ -839,7 +843,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                     if (ok[j]) xm[0] = fmax(xm[0], fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
             }
             block_max<1>(xm, red);
-            if (kTwoPi * h * xm[0] <= kXMax) qsel = cand;
+            if (kTwoPi * h * xm[0] <= kXMax) {
+                qsel = cand;
+                xsel = kTwoPi * h * xm[0];
+            }
         }
         if (qsel < 0) {
             if (tid == 0) {
@@ -879,6 +886,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
             c_d1 = dp[2 * n]; c_d2 = dp[2 * n + 1]; c_rq = rq[n]; c_S = chan[n * 4 + 3];
             c_ok = mk[n];
         };
+        const bool q4 = xsel > kX24;           // uniform: all 32 moments needed
         ldq(0, 0, qa);
         ldc(0);
         for (int i = 0; i < nit; ++i) {
@@ -893,13 +901,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
             taylor_seg<0, KQ, 0>(qa, x, r0, r1, r2, G0, G1, G2);
             ldq(i, 2, qa);
             taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
-            ldq(i, 3, qb);
+            if (q4) ldq(i, 3, qb);
             taylor_seg<2 * KQ, 3 * KQ, 2 * KQ>(qa, x, r0, r1, r2, G0, G1, G2);
             if (i + 1 < nit) {
                 ldq(i + 1, 0, qa);
                 ldc(i + 1);
             }
-            taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+            if (q4) taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
             if (!valid) continue;
             const double2 eix = cexp2pi(h * del);
             const double2 F = cmul(eix, G0);

@@ -20,3 +20,4 @@ for lib in varlib/*.so; do
   echo "$nm tests: $(tail -1 gpurun_out/vp_${tag}_$nm.log)"
 done
 bash tools/vq.sh $tag
+bash tools/vq_al.sh $tag

@@ -60,6 +60,9 @@ def parse():
                     "--arch-nsub sub-ints (default --nsub 2048)")
     ap.add_argument("--arch-nsub", type=int, default=64,
                     help="sub-ints per archive for --fit gettoas")
+    ap.add_argument("--pinned", action="store_true",
+                    help="--fit gettoas: archives held in page-locked host "
+                    "memory (uploaded without the staging copy)")
     ap.add_argument("--zap-frac", type=float, default=0.0,
                     help="fraction of channels masked (zapped) in every "
                     "sub-int, as GetTOAs passes its ok_ichans (default 0)")
@@ -329,6 +332,18 @@ class _Epoch(object):
         return self.days - int(self.days)
 
 
+def _host_rows(data, pinned):
+    """The archive's amplitudes in host memory: pageable (as a plain
+    load_data gives them) or, with --pinned, page-locked (a loader reading
+    straight into pinned buffers)."""
+    from pulseportraiture_amd import engine
+    if not pinned:
+        return data.cpu().numpy()
+    out = engine.pinned_host_array(tuple(data.shape), np.float32)
+    out[...] = data.cpu().numpy()
+    return out
+
+
 def bench_gettoas(args):
     """End-to-end GetTOAs.get_TOAs (pptoas.py:161-792) over in-memory
     archives (float32 amplitudes in host memory, as load_data hands them
@@ -368,7 +383,8 @@ def bench_gettoas(args):
             phases=get_bin_centers(nbin), prof=None, prof_noise=1.0,
             prof_SNR=100.0, Ps=b["P"], SNRs=snrs[:, None],
             source="J1234-5678", state="Intensity",
-            subints=b["data"].cpu().numpy()[:, None], subtimes=[60.0] * per,
+            subints=_host_rows(b["data"], args.pinned)[:, None],
+            subtimes=[60.0] * per,
             telescope="GBT", telescope_code="1", weights=np.ones((per, nchan)))
         del b
     torch.cuda.synchronize(dev)
@@ -404,10 +420,12 @@ def bench_gettoas(args):
                ms_per_step=round(dt / args.steps * 1e3, 3),
                higher_is_better=True, scaling="strong", vs_baseline=None,
                dtype="f64", data="synthetic (device-generated example.gmodel "
-               "archives held in host memory as float32)",
+               "archives held in %s host memory as float32)" % (
+                   "page-locked" if args.pinned else "pageable"),
                config=dict(workload="configs[1]-shape archives: %d x %d "
                            "sub-ints x %dch x %dbin through GetTOAs.get_TOAs"
                            % (nfile, per, nchan, nbin), nfile=nfile,
+                           host_memory="pinned" if args.pinned else "pageable",
                            nsub_per_archive=per, nchan=nchan, nbin=nbin,
                            fit="gettoas", parallelism="dp%d" % world),
                toas=len(gt.TOA_list), host_gb=round(

@@ -340,6 +340,16 @@ def resid_chi2_rows(rows, phases, model_rows, model_index, scales, errs, dof,
     return out
 
 
+def pinned_host_array(shape, dtype=np.float32):
+    """A NumPy array in page-locked host memory (a torch pinned buffer; the
+    array keeps it alive).  An archive loaded into one is uploaded by
+    GetTOAs' stager straight from it, without the copy into its own pinned
+    buffers."""
+    t = torch.empty(tuple(shape), dtype=torch.from_numpy(
+        np.zeros(0, dtype=dtype)).dtype, pin_memory=True)
+    return t.numpy()
+
+
 def noise_rows(rows, frac=4, dev=None):
     """get_noise_PS per row of rows [..., nbin] -> [...] float64."""
     dev = device(dev)

@@ -103,6 +103,19 @@ class _Stager(object):
 
     def _stage(self, rows, dev):
         src = torch.from_numpy(rows)
+        if src.numel() and src.is_contiguous() and src.is_pinned():
+            # the loader put the archive in page-locked memory
+            # (engine.pinned_host_array): the copy engine reads it directly,
+            # no host-side copy (the caller leaves it unchanged during
+            # get_TOAs, as load_data's arrays are)
+            with torch.cuda.device(dev):
+                if self.stream is None:
+                    self.stream = torch.cuda.Stream(dev)
+                with torch.cuda.stream(self.stream):
+                    t = src.to(dev, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+            return t, ev
         if src.dtype != torch.float32:
             src = src.to(torch.float64)
             s32 = src.to(torch.float32)

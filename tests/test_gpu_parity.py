@@ -898,3 +898,29 @@ def test_harmonic_cutoff_fits_match_oracle(flags):
         assert abs(R[I["red_chi2"]] / ref["red_chi2"] - 1) < RCHI2
         np.testing.assert_allclose(R[I["param_errs"]], ref["param_errs"],
                                    rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_stager_pinned_and_pageable_sources_upload_the_same_rows():
+    """GetTOAs' stager: an archive already in page-locked memory
+    (engine.pinned_host_array, bench.py --fit gettoas --pinned) is uploaded
+    straight from it; a pageable one through the stager's own pinned
+    buffers (float64 rows that survive float32 go up as float32)."""
+    import torch
+    from pulseportraiture_amd import engine, pptoas
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((3, 16, 64)).astype(np.float32)
+    p = engine.pinned_host_array(a.shape, np.float32)
+    p[...] = a
+    assert torch.from_numpy(p).is_pinned()
+    st = pptoas._Stager()
+    try:
+        t_pin = st.stage(p).wait()
+        t_pag = st.stage(a).wait()
+        t_f64 = st.stage(a.astype(np.float64)).wait()
+        torch.cuda.synchronize()
+        for t in (t_pin, t_pag, t_f64):
+            assert t.dtype == torch.float32 and t.is_cuda
+            np.testing.assert_array_equal(t.cpu().numpy(), a)
+    finally:
+        st.close()

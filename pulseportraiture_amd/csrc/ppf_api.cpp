@@ -455,7 +455,12 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // sub-ints still needing work is read back between groups.
     const int maxiter = d->max_iter > 0 ? d->max_iter : 200 * 5;
     int iter = 0;
-    for (int group = sa.moments ? 3 : 6; any_mom || any_pass; group = sa.moments ? 2 : 4) {
+    // Moment-only batches read the counter after the first round: most
+    // phase+DM fits finish inside it (C2: 1.0 data passes per fit), so the
+    // empty re-centring launches that a longer first group would queue
+    // are not worth the one synchronisation they save.
+    for (int group = (sa.moments && !any_pass) ? 1 : (sa.moments ? 3 : 6); any_mom || any_pass;
+         group = sa.moments ? 2 : 4) {
         for (int g = 0; g < group; ++g) {
             if (any_pass) {
                 std::pair<hipEvent_t, hipEvent_t> *pe = nullptr;
@@ -477,7 +482,21 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             if (sa.moments && any_mom) {
                 const bool full = iter == 0 && g == 0;
                 if (full && fused) mark(5);
-                e = fused ? ppf::launch_xmom(ma, full, st) : ppf::launch_moments(sa, st);
+                if (fused && !full) {
+                    // re-centring passes: usually few sub-ints, so 8-channel
+                    // blocks (4x the workgroups, a quarter of the rounds
+                    // each) keep more CUs busy; a channel's moments do not
+                    // depend on its block
+                    ppf::XmomArgs mr = ma;
+                    if (mr.cb > 8) {
+                        mr.cb = 8;
+                        mr.nblk = (d->nchan + 7) / 8;
+                        mr.xcd_swizzle = (mr.nblk % 8 == 0) ? 1 : 0;
+                    }
+                    e = ppf::launch_xmom(mr, false, st);
+                } else {
+                    e = fused ? ppf::launch_xmom(ma, full, st) : ppf::launch_moments(sa, st);
+                }
                 if (e != hipSuccess) return hip_fail(ctx, e, fused ? "k_xmom" : "k_moments");
                 if (full && fused) {
                     mark(6);

@@ -16,5 +16,6 @@ timeout -k 10 200 python bench.py --fit full --nsub 2500 --steps 3 --warmup 1 --
 timeout -k 10 300 python bench.py --fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 2 --warmup 1 --cpu-sample 1 > gpurun_out/bench_c5_$tag.log 2>&1
 timeout -k 10 200 python bench.py --fit align --nsub 1000 --nchan 256 --nbin 1024 --cpu-sample 0 > gpurun_out/bench_c4_$tag.log 2>&1
 timeout -k 10 300 python bench.py --fit gettoas --steps 2 --warmup 1 > gpurun_out/bench_gettoas_$tag.log 2>&1
+timeout -k 10 300 python bench.py --fit gettoas --steps 2 --warmup 1 --pinned > gpurun_out/bench_gettoaspinned_$tag.log 2>&1
 bash tools/prof.sh c2$tag --nsub 2500 --passes 1 > /dev/null
-for c in c2 c3 c3nohcut c5 c4 gettoas; do echo "$c $(grep '^{' gpurun_out/bench_${c}_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('ms_per_step'), (d.get('roofline') or {}).get('frac'), (d.get('fp64_roofline') or {}).get('frac'), (d.get('parity') or {}).get('ok'))")"; done
+for c in c2 c3 c3nohcut c5 c4 gettoas gettoaspinned; do echo "$c $(grep '^{' gpurun_out/bench_${c}_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('ms_per_step'), (d.get('roofline') or {}).get('frac'), (d.get('fp64_roofline') or {}).get('frac'), (d.get('parity') or {}).get('ok'))")"; done

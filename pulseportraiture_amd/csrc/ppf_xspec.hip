@@ -29,6 +29,9 @@
 //   wave order through LDS (deterministic) and scaled by 1/sigma~_n^2.
 //   Output: mu[s][q][n][m] (k_tr_mom consumes it).  HBM traffic per sub-int:
 //   the data rows (nchan nbin s_in B) + the moments (nchan 32 16 B).
+//   The first launch of a ppf_fit_batch call (FULL) covers every moment-mode
+//   sub-int in index order; re-centring launches take the sub-ints k_tr_mom
+//   listed (rc_list), packed eight to a workgroup, on 8-channel blocks.
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>

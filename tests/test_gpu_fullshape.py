@@ -411,3 +411,38 @@ def test_no_x_option_and_x_slots():
         st = r["results"][:, I["status"]].astype(int)
         got = [i for i in range(nsub) if st[i] & _lib.ST_NOSPACE]
         assert got == bad, (n_x, st)
+
+
+def test_recentring_passes_batch_independent_and_deterministic():
+    """Re-centring launches take the sub-ints k_tr_mom listed through an
+    atomic slot counter, packed eight to a workgroup on 8-channel blocks, so
+    the packing differs from run to run and from batch to batch: a sub-int's
+    result must not (bitwise), in fits where most sub-ints re-centre."""
+    from pulseportraiture_amd import _lib, engine, synth
+    nsub, nchan, nbin = 48, 256, 1024
+    b = synth.make_batch(nsub, nchan, nbin, first=777)
+    dm_start = synth.DM0 + 6e-3            # ~3 bins from the fit at the band edge
+    freqs = np.tile(b["freqs"], (nsub, 1))
+    init = np.zeros((nsub, 5))
+    init[:, 1] = dm_start
+    nu_fit = float(np.mean(b["freqs"]))
+    errs = engine.noise_rows(b["data"]).cpu().numpy()
+
+    def fit(sl):
+        n = sl.stop - sl.start
+        return engine.results_numpy(engine.fit_batch(
+            b["data"][sl], b["model"], freqs[sl], b["P"][sl], init[sl],
+            [1, 1, 0, 0, 0], nu_fits=np.full((n, 3), nu_fit),
+            nu_outs=np.full((n, 3), np.nan), guess=True,
+            guess_weights=np.ones((n, nchan)),
+            guess_DM=np.full(n, dm_start), guess_Ns=nbin, guess_ref=1,
+            errs=errs[sl]))
+    I = _lib.RESULT_INDEX
+    full = fit(slice(0, nsub))
+    again = fit(slice(0, nsub))
+    part = fit(slice(5, 21))
+    npass = full["results"][:, I["npass"]]
+    assert (npass >= 2).sum() >= 8, npass
+    for k in ("results", "scales", "scale_errs", "channel_snrs", "covariance"):
+        np.testing.assert_array_equal(full[k], again[k])
+        np.testing.assert_array_equal(full[k][5:21], part[k])

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PPF_ABI_VERSION 2
+#define PPF_ABI_VERSION 3
 
 enum ppf_error {
     PPF_OK = 0,
@@ -155,6 +155,19 @@ typedef struct ppf_fit_desc {
                                      frequency, phase then moved to nu_fit
                                      (GetTOAs, pptoas.py:461-499); 1 = nu_fit
                                      itself (ppalign, ppalign.py:214-219) */
+    /* ABI 3 */
+    const double *bounds;         /* [nsub][5][2] lower, upper bound of each
+                                     parameter (NaN: none), or NULL for an
+                                     unbounded fit.  method='TNC' of
+                                     fit_portrait_full / get_TOAs
+                                     (pptoaslib.py:1041-1053, pptoas.py:503-513):
+                                     the initial point is clipped into the box
+                                     and the trust-region steps are projected
+                                     (parameters at a bound whose descent
+                                     direction leaves the box are held there,
+                                     the step over the others is cut at the
+                                     first bound it crosses), so the fit ends
+                                     at the bounded stationary point. */
 } ppf_fit_desc;
 
 int ppf_abi_version(void);

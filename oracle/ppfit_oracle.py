@@ -9,6 +9,7 @@ O(nchan) Schur complement that is algebraically identical to the reference's
 dense (5+n)x(5+n)xn block inversion (pptoaslib.py:731-766).
 """
 import time
+import warnings
 
 import numpy as np
 import scipy.optimize as opt
@@ -365,7 +366,13 @@ def _spectra(data_port, model_port):
 def fit_portrait_full(data_port, model_port, init_params, P, freqs,
                       nu_fits=(None, None, None), nu_outs=(None, None, None),
                       errs=None, fit_flags=(1, 1, 1, 1, 1), log10_tau=True,
-                      option=0, is_toa=True, messages=None):
+                      option=0, is_toa=True, messages=None,
+                      method="trust-ncg", bounds=None, x_fit=None):
+    """pptoaslib.py:974-1144 (Schur covariance instead of the dense cube).
+    method 'TNC' minimises with scipy TNC under `bounds` exactly as
+    pptoaslib.py:1041-1060 does (minfev = dof - Sd, xtol 1e-10; maxiter is
+    not a TNC option and scipy ignores it); x_fit (test infrastructure)
+    skips the minimiser and reports the post-fit quantities at x_fit."""
     data_port = np.asarray(data_port, dtype=np.float64)
     model_port = np.asarray(model_port, dtype=np.float64)
     freqs = np.asarray(freqs, dtype=np.float64)
@@ -393,10 +400,25 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
         return cache[key]
 
     t0 = time.time()
-    res = opt.minimize(lambda x: objective(terms(x)), np.asarray(
-        init_params, dtype=float), method="trust-ncg",
-        jac=lambda x: gradient(terms(x), flags),
-        hess=lambda x: hessian(terms(x), flags), options={"gtol": -1})
+    if x_fit is not None:
+        x = np.asarray(x_fit, dtype=float)
+        res = opt.OptimizeResult(x=x, fun=objective(terms(x)), nfev=0,
+                                 status=0)
+    elif method == "TNC":
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", opt.OptimizeWarning)
+            res = opt.minimize(
+                lambda x: objective(terms(x)), np.asarray(init_params,
+                                                          dtype=float),
+                method="TNC", jac=lambda x: gradient(terms(x), flags),
+                bounds=bounds, options={"maxiter": 2000, "disp": False,
+                                        "xtol": 1e-10,
+                                        "minfev": dof - Sd})
+    else:
+        res = opt.minimize(lambda x: objective(terms(x)), np.asarray(
+            init_params, dtype=float), method="trust-ncg",
+            jac=lambda x: gradient(terms(x), flags),
+            hess=lambda x: hessian(terms(x), flags), options={"gtol": -1})
     duration = time.time() - t0
     phi_fit, DM_fit, GM_fit, tau_fit, alpha_fit = res.x
     nu_out = list(nu_outs)
@@ -625,12 +647,15 @@ def fit_phase_shift(data, model, noise=None, bounds=(-0.5, 0.5), Ns=100):
 def get_toas_archive(subints, models, freqs, weights, SNRs, Ps, DM_stored,
                      doppler_factors, ok_isubs=None, noise_stds=None,
                      fit_flags=(1, 1, 0, 0, 0), bary=True, DM0=None,
-                     tau_guess=0.0, alpha_guess=-4.0, log10_tau=True):
+                     tau_guess=0.0, alpha_guess=-4.0, log10_tau=True,
+                     scat_guess=None):
     """subints [nsub, nchan, nbin]; models [nsub, nchan, nbin] (or one
     [nchan, nbin] shared); weights / SNRs [nsub, nchan].  With a scattering
     fit (fit_flags[3] or [4]) the guesses follow pptoas.py:467-492: tau_guess
     [rot] at nu_fit scatters the mean model profile of the phase guess, and
-    with log10_tau a zero tau_guess becomes log10(1 / nbin)."""
+    with log10_tau a zero tau_guess becomes log10(1 / nbin); scat_guess =
+    (tau [s], its reference frequency [MHz], alpha) overrides them per
+    sub-int as pptoas.py:469-472 does."""
     nsub, nchan, nbin = subints.shape
     if ok_isubs is None:
         ok_isubs = np.arange(nsub)
@@ -660,6 +685,9 @@ def get_toas_archive(subints, models, freqs, weights, SNRs, Ps, DM_stored,
         tg, ag = 0.0, 0.0
         if scat:
             tg, ag = float(tau_guess), float(alpha_guess)
+            if scat_guess is not None:
+                ag = float(scat_guess[2])
+                tg = (scat_guess[0] / P) * (nu_fit / scat_guess[1]) ** ag
             B = _scat_B(np.array([tg]), nbin // 2 + 1)[0]
             mprof = np.fft.irfft(B * np.fft.rfft(mprof), n=nbin)
         phi_guess = fit_phase_shift(rot_prof, mprof, Ns=100)["phase"]

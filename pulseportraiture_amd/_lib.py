@@ -22,7 +22,7 @@ ST_NO_ROOT, ST_SINGULAR, ST_NONFINITE, ST_NOFIT = 0x100, 0x200, 0x400, 0x800
 ST_NOSPACE = 0x1000
 OPT_NO_HCUT = 1           # ppf_fit_desc.options
 OPT_NO_X = 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # ppf_result: 32 doubles (include/ppfit.h)
 RESULT_FIELDS = (
@@ -64,6 +64,7 @@ class FitDesc(ctypes.Structure):
         ("channel_snrs", _vp), ("covariance", _vp), ("workspace", _vp),
         ("workspace_bytes", ctypes.c_size_t),
         ("x_subints", _i32), ("options", _i32), ("guess_ref", _i32),  # ABI 2
+        ("bounds", _vp),                                               # ABI 3
     ]
 
 

@@ -403,6 +403,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.KC = (const int32_t *)(ws + L.KC);
     sa.freqs = d->freqs; sa.P = d->P; sa.mask = d->chan_mask; sa.init = d->init;
     sa.fit_flags = d->fit_flags; sa.nu_fits = d->nu_fits; sa.nu_outs = d->nu_outs;
+    sa.bounds = d->bounds;
     sa.log10_tau = d->log10_tau; sa.option = d->option; sa.is_toa = d->is_toa; sa.mode = d->mode;
     sa.max_iter = d->max_iter; sa.guess = d->guess; sa.x0 = (double *)(ws + L.x0);
     sa.stats = (double *)(ws + L.stats); sa.results = d->results; sa.scales = d->scales;

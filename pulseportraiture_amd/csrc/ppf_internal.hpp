@@ -101,6 +101,7 @@ struct SolveArgs {
     const double *init;
     const int32_t *fit_flags;
     const double *nu_fits, *nu_outs;
+    const double *bounds;        // [nsub][5][2] (NaN: none) or null
     int log10_tau, option, is_toa, mode, max_iter, guess;
     const double *x0;
     double *stats;               // [nsub][2][nchan][10]

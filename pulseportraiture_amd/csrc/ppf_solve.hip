@@ -203,6 +203,21 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
     double x[5];
     for (int i = 0; i < 5; ++i) x[i] = a.init[(int64_t)s * 5 + i];
     if (a.guess) x[0] = a.x0[(int64_t)s * 8 + 0];
+    // method='TNC' box (NaN: no bound): scipy's TNC starts from x0 clipped
+    // into it
+    double lo[5], hi[5];
+    int bnd = 0;
+    for (int i = 0; i < 5; ++i) {
+        lo[i] = -INFINITY;
+        hi[i] = INFINITY;
+        if (a.bounds) {
+            const double l = a.bounds[((int64_t)s * 5 + i) * 2], u = a.bounds[((int64_t)s * 5 + i) * 2 + 1];
+            if (l == l) lo[i] = l;
+            if (u == u) hi[i] = u;
+        }
+        x[i] = fmin(fmax(x[i], lo[i]), hi[i]);
+        if ((flagmask >> i & 1) && (lo[i] > -INFINITY || hi[i] < INFINITY)) bnd = 1;
+    }
     const double tau0 = a.log10_tau ? pow(10.0, x[3]) : x[3];
     const int scat = ((flagmask & 0x18) || tau0 != 0.0) ? 1 : 0;
     const double nu_mean = sf / cnt;
@@ -242,6 +257,8 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         S.scat = scat;
         S.hb = 0;
         S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga;
+        for (int i = 0; i < 5; ++i) { S.lo[i] = lo[i]; S.hi[i] = hi[i]; }
+        S.bnd = bnd;
         if (nf == 0 || cnt == 0.0) {
             S.phase = PH_DONE;
             S.status = PPF_ST_NOFIT;
@@ -503,13 +520,67 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 }
 
 // ===========================================================================
+// method='TNC' box bounds (pptoas.py:503-513, pptoaslib.py:1041-1053): the
+// trust-region step projected onto the box.  Fitted parameters sitting at a
+// bound whose descent direction (or CG step) leaves the box are held there;
+// the CG-Steihaug step over the others is cut at the first bound it crosses.
+// The fit then stops, as the unbounded one does, when no step predicts a
+// decrease: at the bounded stationary point TNC converges to.
+// ===========================================================================
+template <int NF>
+__device__ __forceinline__ void tr_box_step(const TRState &S, TRModel &m, const int (&idx)[5],
+                                            double *p, double *pv, int *hbo) {
+    // held: a bit per subspace parameter; its gradient entry and Hessian
+    // row/column are replaced by (0, unit) in place, which leaves the model
+    // value of a step that does not move it unchanged
+    int held = 0;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+        const double x = S.x[idx[q]];
+        if ((x <= S.lo[idx[q]] && m.g[q] > 0.0) || (x >= S.hi[idx[q]] && m.g[q] < 0.0)) held |= 1 << q;
+    }
+    bool hb = false;
+    for (int pass = 0; pass <= NF; ++pass) {
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            if (!(held >> q & 1)) continue;
+            m.g[q] = 0.0;
+#pragma unroll
+            for (int r = 0; r < NF; ++r) m.H[q][r] = m.H[r][q] = (q == r ? 1.0 : 0.0);
+        }
+        hb = cg_steihaug<NF>(m, sqrt(dotn<NF>(m.g, m.g)), S.radius, p);
+        int more = 0;
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            const double x = S.x[idx[q]];
+            if (!(held >> q & 1) && ((x <= S.lo[idx[q]] && p[q] < 0.0) || (x >= S.hi[idx[q]] && p[q] > 0.0)))
+                more |= 1 << q;
+        }
+        if (!more) break;
+        held |= more;
+    }
+    double t = 1.0;
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+        if (held >> q & 1) p[q] = 0.0;
+        const double x = S.x[idx[q]];
+        if (p[q] < 0.0 && x + p[q] < S.lo[idx[q]]) t = fmin(t, (S.lo[idx[q]] - x) / p[q]);
+        if (p[q] > 0.0 && x + p[q] > S.hi[idx[q]]) t = fmin(t, (S.hi[idx[q]] - x) / p[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NF; ++q) p[q] *= t;
+    *pv = model_value<NF>(m, p);
+    *hbo = hb ? 1 : 0;
+}
+
+// ===========================================================================
 // one iteration of scipy _minimize_trust_region (scipy/optimize/_trustregion.py)
 // with CGSteihaugSubproblem (_trustregion_ncg.py): consume the evaluation o
 // (f, g[5], H[15]) of S.th, accept/reject, then propose the next point.
 // gtol = -1 (pptoaslib.py:1047-1048), eta 0.15, initial radius 1, max radius
 // 1000, maxiter 200 * len(x0).  Returns 1 when a new proposal is pending.
 // ===========================================================================
-template <int NF>
+template <int NF, bool BOX>
 __device__ int tr_update_t(TRState &S, const double *o, int max_iter, const int (&idx)[5]) {
     const int phase = S.phase;
     const int maxiter = max_iter > 0 ? max_iter : 200 * 5;
@@ -553,16 +624,26 @@ __device__ int tr_update_t(TRState &S, const double *o, int max_iter, const int 
                 m.H[q][r] = S.H[uidx(i, j)];
             }
         }
-        double p[5];
-        const double jm = sqrt(dotn<NF>(m.g, m.g));
-        const bool hb = cg_steihaug<NF>(m, jm, S.radius, p);
-        const double pv = model_value<NF>(m, p);
+        double p[5], pv;
+        bool hb;
+        if (BOX && S.bnd) {
+            int h;
+            tr_box_step<NF>(S, m, idx, p, &pv, &h);
+            hb = h != 0;
+        } else {
+            const double jm = sqrt(dotn<NF>(m.g, m.g));
+            hb = cg_steihaug<NF>(m, jm, S.radius, p);
+            pv = model_value<NF>(m, p);
+        }
         if (m.f - pv <= 0.0) {
             done = true;                 // warnflag 2: no predicted improvement
         } else {
             for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
 #pragma unroll
-            for (int q = 0; q < NF; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q];
+            for (int q = 0; q < NF; ++q) {
+                const double v = S.x[idx[q]] + p[q];
+                S.th[idx[q]] = (BOX && S.bnd) ? fmin(fmax(v, S.lo[idx[q]]), S.hi[idx[q]]) : v;
+            }
             S.pred = pv;
             S.hb = hb ? 1 : 0;
             S.slot_eval = S.slot_cur ^ 1;
@@ -574,8 +655,8 @@ __device__ int tr_update_t(TRState &S, const double *o, int max_iter, const int 
 }
 // MAXNF: the largest subspace the caller can meet (3 for the moment path,
 // which never fits tau/alpha; instantiating only those keeps its registers
-// down)
-template <int MAXNF = 5>
+// down).  BOX: the instantiation also handles method='TNC' bounds.
+template <int MAXNF = 5, bool BOX = true>
 __device__ int tr_update(TRState &S, const double *o, int max_iter) {
     const int flagmask = S.flagmask;
     int idx[5] = {0, 0, 0, 0, 0}, nf = 0;
@@ -583,14 +664,14 @@ __device__ int tr_update(TRState &S, const double *o, int max_iter) {
     for (int i = 0; i < 5; ++i)
         if (flagmask >> i & 1) idx[nf++] = i;
     switch (nf) {
-        case 1: return tr_update_t<1>(S, o, max_iter, idx);
-        case 2: return tr_update_t<2>(S, o, max_iter, idx);
+        case 1: return tr_update_t<1, BOX>(S, o, max_iter, idx);
+        case 2: return tr_update_t<2, BOX>(S, o, max_iter, idx);
         default:
-            if constexpr (MAXNF <= 3) return tr_update_t<3>(S, o, max_iter, idx);
+            if constexpr (MAXNF <= 3) return tr_update_t<3, BOX>(S, o, max_iter, idx);
             else {
-                if (nf == 3) return tr_update_t<3>(S, o, max_iter, idx);
-                if (nf == 4) return tr_update_t<4>(S, o, max_iter, idx);
-                return tr_update_t<5>(S, o, max_iter, idx);
+                if (nf == 3) return tr_update_t<3, BOX>(S, o, max_iter, idx);
+                if (nf == 4) return tr_update_t<4, BOX>(S, o, max_iter, idx);
+                return tr_update_t<5, BOX>(S, o, max_iter, idx);
             }
     }
 }
@@ -601,6 +682,9 @@ __device__ int tr_update(TRState &S, const double *o, int max_iter) {
 // (_trustregion_ncg.py), gtol = -1 (pptoaslib.py:1047-1048), eta 0.15,
 // initial radius 1, max radius 1000, maxiter 200 * len(x0).
 // ===========================================================================
+// BOX: the bounded (method='TNC') instantiation, launched only when the call
+// has bounds, so the unbounded one keeps its 3 waves per SIMD
+template <bool BOX>
 __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     __shared__ double thb[kWaves][8];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -622,7 +706,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     for (int i = 0; i < 21; ++i) o[i] = wave_sum(o[i]);
     int cmd = 0;
     if (lane == 0) {
-        cmd = tr_update(S, o, a.max_iter);
+        cmd = tr_update<5, BOX>(S, o, a.max_iter);
         for (int i = 0; i < 5; ++i) thb[wave][i] = S.th[i];
         thb[wave][5] = (double)cmd;
     }
@@ -1420,8 +1504,11 @@ hipError_t launch_pass(const SolveArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_tr_step, dim3((unsigned)((a.nsub + kWaves - 1) / kWaves)), dim3(kBlock), 0,
-                       st, a);
+    const dim3 g((unsigned)((a.nsub + kWaves - 1) / kWaves));
+    if (a.bounds)
+        hipLaunchKernelGGL(k_tr_step<true>, g, dim3(kBlock), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_tr_step<false>, g, dim3(kBlock), 0, st, a);
     return hipGetLastError();
 }
 

@@ -24,6 +24,10 @@ struct TRState {
     int mmode, need_mom, mtarget, macc;
     int mvalid[2], meval, nmom;
     double mc[2][3];
+    // box bounds of method='TNC' (pptoas.py:503-513, pptoaslib.py:1041-1053);
+    // bnd = 0: none on any fitted parameter (lo = -inf, hi = +inf)
+    double lo[5], hi[5];
+    int bnd, pad3;
 };
 
 __device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j

@@ -87,7 +87,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               log10_tau=False, option=0, is_toa=True, mode=_lib.PPF_MODE_FULL,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
               guess_Ns=100, guess_tau=None, dev=None, workspace=None,
-              n_x=None, no_hcut=False, max_workspace=None, guess_ref=0):
+              n_x=None, no_hcut=False, max_workspace=None, guess_ref=0,
+              bounds=None):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
@@ -96,6 +97,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     it from fit_flags / init (x_subints).  no_hcut: sum every harmonic
     (PPF_OPT_NO_HCUT).  guess_ref: frame of the guess profile (0: mean
     frequency then phase_transform to nu_fit, GetTOAs; 1: nu_fit, ppalign).
+    bounds: method='TNC' box, [5, 2] or [nsub, 5, 2] (lower, upper; None or
+    NaN = unbounded), or None for an unbounded fit.
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
@@ -106,6 +109,12 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     covariance [nsub, 5, 5], and the workspace (reusable)."""
     dev = device(dev)
     f64 = torch.float64
+    if n_x is None and not isinstance(init, torch.Tensor) and \
+            not isinstance(fit_flags, torch.Tensor):
+        # counted from the host arrays before the upload (no device
+        # round trip)
+        n_x = x_subints(fit_flags, init, log10_tau,
+                        int(np.asarray(init).size // 5))
     data_t = to_dev(data, dev, _data_dtype(data))
     if data_t.dim() != 3:
         raise ValueError("data must be [nsub, nchan, nbin]")
@@ -149,10 +158,18 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
         gdm_t = to_dev(guess_DM, dev, f64).reshape(-1)
         if gdm_t.numel() == 1:
             gdm_t = gdm_t.repeat(nsub)
+    bnd_t = None
+    if bounds is not None:
+        b = np.array([[np.nan if v is None else float(v) for v in lu]
+                      for lu in np.asarray(bounds, dtype=object).reshape(-1, 2)
+                      ], dtype=float).reshape(-1, 5, 2)
+        if b.shape[0] == 1:
+            b = np.repeat(b, nsub, axis=0)
+        bnd_t = to_dev(b.reshape(nsub, 5, 2), dev, f64)
     per_sub = dict(data=data_t, freqs=freqs_t, P=P_t, init=init_t,
                    flags=flags_t, nu_fits=nu_fits_t, nu_outs=nu_outs_t,
                    errs=errs_t, mask=mask_t, mi=mi_t, gw=gw_t, gdm=gdm_t,
-                   gtau=gtau_t)
+                   gtau=gtau_t, bounds=bnd_t)
     if n_x is None:
         n_x = x_subints(flags_t, init_t, log10_tau, nsub)
     xsel = None
@@ -161,10 +178,13 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
                guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref)
     lib = _lib.load()
     need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
+    if need <= (64 << 20) or nsub == 1:
+        # small batches (the single-call APIs) skip the free-memory query
+        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
     if max_workspace is None:
         free, _ = torch.cuda.mem_get_info(dev)
         max_workspace = free // 2
-    if need <= max_workspace or nsub == 1:
+    if need <= max_workspace:
         return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
     # chunks of equal size whose workspace fits the budget
     per = max(1, int(nsub * max_workspace // max(need, 1)))
@@ -222,6 +242,7 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.options = (_lib.OPT_NO_HCUT if cfg["no_hcut"] else 0) | \
         (_lib.OPT_NO_X if n_x == 0 else 0)
     d.guess_ref = int(cfg["guess_ref"])
+    d.bounds = pp(per_sub["bounds"])
     return d
 
 

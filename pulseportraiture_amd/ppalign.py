@@ -262,7 +262,8 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     r = res["results"]
     dc["last_results"] = r               # (diagnostics: bench.py --fit align)
     st = r[:, I["status"]].to(torch.int64).cpu().numpy()
-    bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR))[0]
+    bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR |
+                         _lib.ST_NOSPACE))[0]
     if len(bad):
         from .pplib import _raise_status
         _raise_status(int(st[bad[0]]))

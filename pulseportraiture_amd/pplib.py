@@ -387,8 +387,9 @@ def fit_portrait(data, model, init_params, P, freqs, nu_fit=None, nu_out=None,
     The reference minimises with scipy TNC; the device runs the trust-region
     Newton solver of fit_portrait_full on the same objective
     (pplib.py:1335-1447), which converges to the same stationary point
-    (SURVEY.md Appendix A.5).  ``bounds`` is accepted and ignored, as in the
-    unbounded default."""
+    (SURVEY.md Appendix A.5).  ``bounds`` on (phase, DM) hold as TNC's
+    do: the device trust-region steps are projected onto the box
+    (ppf_fit_desc.bounds)."""
     data = np.asarray(data)
     freqs = np.asarray(freqs, dtype=float)
     nchan, nbin = data.shape
@@ -402,7 +403,7 @@ def fit_portrait(data, model, init_params, P, freqs, nu_fit=None, nu_out=None,
         init, [1, 1, 0, 0, 0], nu_fits=np.full((1, 3), nu_fit),
         nu_outs=np.full((1, 3), np.nan if nu_out is None else nu_out),
         errs=None if errs is None else np.asarray(errs, dtype=float)[None],
-        mode=_lib.PPF_MODE_LEGACY2)
+        mode=_lib.PPF_MODE_LEGACY2, bounds=_box(bounds, 2))
     r = engine.results_numpy(res)
     duration = time.time() - t0
     R, I = r["results"][0], _lib.RESULT_INDEX
@@ -422,6 +423,21 @@ def fit_portrait(data, model, init_params, P, freqs, nu_fit=None, nu_out=None,
                      nfeval=int(R[I["nfeval"]]), return_code=rc)
 
 
+def _box(bounds, n):
+    """[5, 2] device bounds from the first n (lower, upper) pairs of a
+    scipy bounds list (None: unbounded); None when nothing is bounded."""
+    if bounds is None:
+        return None
+    b = np.full((5, 2), np.nan)
+    for i, lu in enumerate(list(bounds)[:n]):
+        if lu is None:
+            continue
+        for j in (0, 1):
+            if lu[j] is not None:
+                b[i, j] = float(lu[j])
+    return None if np.isnan(b).all() else b
+
+
 def _raise_status(status):
     """Map device status bits to the exceptions the reference raises."""
     if status & _lib.ST_NO_ROOT:
@@ -431,6 +447,12 @@ def _raise_status(status):
         raise np.linalg.LinAlgError("Singular matrix")
     if status & _lib.ST_NOFIT:
         raise ValueError("nothing to fit (no fit flag set or no channel)")
+    if status & _lib.ST_NOSPACE:
+        # the workspace had fewer cross-spectrum slots than fits that stream
+        # it (the host's count disagreed with the device's k_classify): an
+        # internal error, never a fit outcome
+        raise RuntimeError("internal error: no cross-spectrum slot for a "
+                           "scattering fit (PPF_ST_NOSPACE)")
 
 
 # ------------------------------------------------------------- TOA output --

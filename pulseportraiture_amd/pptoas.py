@@ -23,7 +23,7 @@ from . import pplib as _pplib
 from .pplib import (DataBunch, file_is_type, guess_fit_freq, read_model,
                     scattering_alpha, write_TOAs, weighted_mean,
                     scattering_times, scattering_portrait_FT,
-                    gen_gaussian_portrait, _raise_status)
+                    gen_gaussian_portrait, _raise_status, _box)
 from . import pptoaslib as _pptl
 from .pptoaslib import unpack_result, _status_message, _nu_zero_messages
 
@@ -340,6 +340,7 @@ class GetTOAs(object):
         self.add_instrumental_response = add_instrumental_response
         self._ff = [None]   # fit_flags carried across sub-ints (pptoas.py:519-529)
         ctx = dict(quiet=quiet, tscrunch=tscrunch, fit_scat=fit_scat,
+                   method=method, bounds=[bounds],
                    nu_fit_tuple=nu_fit_tuple, nu_ref_tuple=nu_ref_tuple,
                    bary=bary, print_phase=print_phase, print_flux=print_flux,
                    print_parangle=print_parangle,
@@ -497,21 +498,33 @@ class GetTOAs(object):
                         tau_guess = nbin ** -1
                     tau_guess = np.log10(tau_guess)
             init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
+            if ctx["bounds"][0] is None and ctx["method"] == "TNC":
+                # pptoas.py:503-513: set once, at the first sub-int fitted
+                ctx["bounds"][0] = [
+                    (None, None), (None, None), (None, None),
+                    (0.0, None) if not self.log10_tau else
+                    (np.log10((10 * nbin) ** -1), None), (-10.0, 10.0)]
+            # the reference's fit_flags is one list that lives across
+            # sub-ints and archives: the 2-channel rule edits whatever the
+            # previous sub-int left in it (pptoas.py:519-529, SURVEY.md
+            # appendix B)
             if len(freqsx) == 1:
-                fit_flags = [1, 0, 0, 0, 0]
+                self._ff[0] = [1, 0, 0, 0, 0]
                 if not quiet:
                     print("TOA #%d only has 1 frequency channel...fitting "
                           "for phase only..." % (j + 1))
             elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
-                if fit_flags is None:
+                if self._ff[0] is None:
                     raise UnboundLocalError(
                         "local variable 'fit_flags' referenced before "
                         "assignment (pptoas.py:525)")
-                fit_flags = list(fit_flags)
-                fit_flags[2] = 0
+                self._ff[0][2] = 0
+                if not quiet:
+                    print("TOA #%d only has 2 frequency channels...fitting "
+                          "for phase and DM only..." % (j + 1))
             else:
-                fit_flags = list(np.copy(self.fit_flags))
-            flags_b[j] = fit_flags
+                self._ff[0] = list(np.copy(self.fit_flags))
+            flags_b[j] = self._ff[0]
         rank, world = _rank_world()
         first, count = _dist.shard(nok, rank, world)
         sel = ok_isubs[first:first + count]
@@ -531,6 +544,7 @@ class GetTOAs(object):
                     model_index=model_index, mask=mask, init=init,
                     flags_b=flags_b, nu_fit_b=nu_fit_b, nu_out_b=nu_out_b,
                     guess_tau=guess_tau, first=first, count=count,
+                    bounds=ctx["bounds"][0],
                     world=world, staged=stager.stage(rows),
                     fit_duration=fit_duration)
 
@@ -585,6 +599,7 @@ class GetTOAs(object):
             guess_weights=np.asarray(d.weights)[isubs],
             guess_DM=np.full(count, job["DM_stored"]), guess_Ns=100,
             guess_tau=job["guess_tau"][sl] if ctx["fit_scat"] else None,
+            bounds=_box(job["bounds"], 5) if ctx["method"] == "TNC" else None,
             dev=dev)
         return _pack(res)
 

@@ -15,7 +15,7 @@ import time
 import numpy as np
 
 from . import _lib, engine
-from .pplib import (DataBunch, Dconst, RCSTRINGS, _raise_status,  # noqa: F401
+from .pplib import (DataBunch, Dconst, RCSTRINGS, _raise_status, _box,  # noqa: F401
                     scattering_times, scattering_portrait_FT, phase_transform,
                     get_bin_centers, guess_fit_freq, rotate_data)
 
@@ -130,8 +130,11 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
     """pptoaslib.py:974-1144 on the GPU (single sub-integration).
 
     ``method`` 'trust-ncg' is the reference default and what the device
-    solver replicates; 'TNC' / 'Newton-CG' run the same solver (they converge
-    to the same stationary point), ``bounds`` is ignored as for trust-ncg."""
+    solver replicates; 'Newton-CG' runs the same solver (it converges to the
+    same stationary point).  'TNC' applies ``bounds`` as the reference does
+    (pptoaslib.py:1041-1046: only for TNC): the device trust-region steps
+    are projected onto the box, so the fit ends at the bounded stationary
+    point TNC converges to."""
     if method not in METHODS:
         print("Method '%s' is not implemented." % method)
         sys.exit()
@@ -149,7 +152,8 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
         [P], init, [int(bool(f)) for f in fit_flags], nu_fits=nu_f[None],
         nu_outs=nu_o[None],
         errs=None if errs is None else np.asarray(errs, dtype=float)[None],
-        log10_tau=log10_tau, option=option, is_toa=is_toa)
+        log10_tau=log10_tau, option=option, is_toa=is_toa,
+        bounds=_box(bounds, 5) if method == "TNC" else None)
     r = engine.results_numpy(res)
     duration = time.time() - t0
     _nu_zero_messages(fit_flags, nu_outs)

@@ -45,13 +45,17 @@ def c5_case(name):
     return c, data.astype(np.float32), model, freqs, P
 
 
+def toa_conf(name):
+    """The full_inputs.TOAS entry of a get_TOAs case."""
+    return _conf(FI.TOAS, name)
+
+
 def toa_case(name):
     """(golden case, [per-archive dict(subints f32 [nsub, nchan, nbin],
-    weights, dfs, epochs, noise, snrs)], freqs, gmodel path)."""
+    weights, dfs, epochs, parangles, noise, snrs)], freqs, template path)."""
     c = case("toas", name)
-    conf = _conf(FI.TOAS, name)
-    if conf.get("narrow"):
-        FI.write_narrow()
+    conf = toa_conf(name)
+    gm = FI.toa_gmodel(conf)
     files, freqs = FI.toa_inputs(conf)
     out = []
     for f, fi in enumerate(files):
@@ -60,11 +64,16 @@ def toa_case(name):
             "rebuilt inputs of %s archive %d differ" % (name, f)
         np.testing.assert_array_equal(fi["weights"], c["f%d_weights" % f])
         out.append(dict(subints=sub, weights=fi["weights"], dfs=fi["dfs"],
-                        epochs=fi["epochs"], noise=c["f%d_noise" % f],
-                        snrs=c["f%d_snrs" % f]))
-    gm = FI.NARROW_GMODEL if conf.get("narrow") else FI.SPLINE_MODEL if \
-        conf.get("spline") else os.path.join(G.GOLDEN, "example.gmodel")
+                        epochs=fi["epochs"], parangles=fi["parangles"],
+                        noise=c["f%d_noise" % f], snrs=c["f%d_snrs" % f]))
     return c, out, freqs, gm
+
+
+def toa_archive_fields(name, fi, freqs):
+    """load_data DataBunch fields of one rebuilt archive (as the golden
+    generator handed them to the reference), minus epochs / phases."""
+    return FI.archive_fields(toa_conf(name), fi, freqs, fi["noise"],
+                             fi["snrs"])
 
 
 def align_case(name):

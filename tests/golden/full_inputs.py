@@ -112,6 +112,23 @@ def _phase_transform(phi, DM, nu1, nu2, P):
     return x - 1.0 if x >= 0.5 else x
 
 
+SCAT_GMODEL = os.path.join(HERE, "scat.gmodel")
+# example.gmodel with a nonzero TAU [s] at its FREQ (1300 MHz): GetTOAs'
+# scattering branch takes its tau guess from it (pptoas.py:478-480) and
+# phase-fits the mean model scattered by that guess (pptoas.py:484-489)
+SCAT_TAU_S = 1.5e-3 * S.P0 * (1300.0 / 1500.0) ** -4
+
+
+def write_scat(path=SCAT_GMODEL):
+    """tests/golden/scat.gmodel (committed; rewritten only if missing)."""
+    if os.path.exists(path):
+        return
+    code, nu_ref, params, alpha = S.read_gmodel()
+    params = params.copy()
+    params[1] = SCAT_TAU_S
+    S.write_gmodel(path, code, nu_ref, params, alpha, name="PSR_SCAT")
+
+
 TOAS = [
     dict(name="c1", nfile=5, nsub=10, nchan=64, nbin=512, scint=True,
          seed=201, DM0=True),
@@ -121,7 +138,65 @@ TOAS = [
     # get_TOAs with a spline template (pptoas.py:416-419), 512 -> 1024 bins
     dict(name="spline", nfile=2, nsub=4, nchan=64, nbin=1024, seed=204,
          spline=True),
+    # ---- the non-default branches of get_TOAs (round 3) ----------------
+    # (a) configs[2]'s drop-in entry: fit_GM + fit_scat at 512 x 2048 with a
+    # .gmodel whose TAU != 0 (tau guess from gparams, phase guess against
+    # the scattered mean model, pptoas.py:467-492; gm / scat_time /
+    # log10_scat_time / scat_ind flags, pptoas.py:659-677)
+    dict(name="scatgm", nfile=1, nsub=3, nchan=512, nbin=2048, seed=205,
+         gmodel="scat", tau=2e-3, kw=dict(fit_GM=True, fit_scat=True)),
+    # (b) configs[4]'s band (400-800 MHz): fit_scat with scat_guess and
+    # fix_alpha (pptoas.py:469-472, 236), flux of the scattered model
+    # (print_flux, pptoas.py:598-624)
+    dict(name="scatfix", nfile=1, nsub=4, nchan=128, nbin=1024, seed=206,
+         lo=400.0, bw=400.0, nu0=600.0, tau=5e-3, nu_tau=600.0,
+         kw=dict(fit_scat=True, fix_alpha=True, print_flux=True,
+                 scat_guess=[4e-3 * S.P0, 600.0, -4.0])),
+    # (c) user nu_refs and nu_fits (pptoas.py:440-456, 691-693),
+    # print_phase / print_flux / print_parangle and extra flags
+    dict(name="opts", nfile=2, nsub=4, nchan=64, nbin=512, seed=207,
+         parangle=True,
+         kw=dict(nu_refs=(1400.0, 1450.0), nu_fits=(1350.0, 1380.0),
+                 print_phase=True, print_flux=True, print_parangle=True,
+                 addtnl_toa_flags={"pta": "TEST", "ver": 0.1})),
+    # (d) 1- and 2-channel sub-ints under fit_GM (pptoas.py:519-529): the
+    # fit_flags list carries over from one sub-int (and archive) to the next
+    dict(name="chan12", nfile=2, nsub=5, nchan=64, nbin=512, seed=208,
+         chans={0: [None, 2, 1, 2, None], 1: [2, None, 1, None, 2]},
+         kw=dict(fit_GM=True)),
+    # (e) tscrunch=True (forwarded to load_data) and bary=False, with a
+    # linear-tau scattering fit (scat_time_err, pptoas.py:669-673)
+    dict(name="tscr", nfile=2, nsub=3, nchan=128, nbin=512, seed=209,
+         gmodel="scat", tau=3e-3, same_phi=True, tscrunch=True,
+         kw=dict(tscrunch=True, bary=False, fit_scat=True, log10_tau=False)),
+    # (f) method='TNC' (bounded, pptoas.py:503-513; pptoaslib.py:1041-1053):
+    # phase + DM (default bounds); a scattering fit with user bounds whose
+    # alpha bound is active at the solution
+    dict(name="tnc", nfile=1, nsub=4, nchan=64, nbin=512, seed=210,
+         kw=dict(method="TNC")),
+    dict(name="tncscat", nfile=1, nsub=4, nchan=128, nbin=512, seed=211,
+         gmodel="scat", tau=3e-3,
+         kw=dict(method="TNC", fit_scat=True,
+                 bounds=[(None, None), (None, None), (None, None),
+                         (-3.5, None), (-10.0, -4.4)])),
+    # (g) method='Newton-CG' (pptoaslib.py:1049-1050)
+    dict(name="ncg", nfile=1, nsub=2, nchan=64, nbin=512, seed=212,
+         kw=dict(method="Newton-CG")),
 ]
+
+
+def toa_gmodel(c):
+    """The template file of a get_TOAs case."""
+    if c.get("narrow"):
+        write_narrow()
+        return NARROW_GMODEL
+    if c.get("spline"):
+        write_spline()
+        return SPLINE_MODEL
+    if c.get("gmodel") == "scat":
+        write_scat()
+        return SCAT_GMODEL
+    return S.GMODEL
 
 # gen_spline_portrait cases: (name, nchan, lo, bw, nbin [None = model's])
 SPLINES = [("same", 64, 1100.0, 800.0, None), ("n512", 48, 1150.0, 700.0, 512),
@@ -136,26 +211,72 @@ def toa_inputs(c):
     doppler factors, epochs; plus freqs.  Rebuilt identically by the tests."""
     rng = np.random.default_rng(20251016 + c["seed"])
     nchan, nbin, nsub = c["nchan"], c["nbin"], c["nsub"]
-    model, freqs = S.template(nchan, nbin, gmodel=NARROW_GMODEL if
-                              c.get("narrow") else None)
+    model, freqs = S.template(nchan, nbin, lo=c.get("lo", 1100.0),
+                              bw=c.get("bw", 800.0),
+                              gmodel=NARROW_GMODEL if c.get("narrow")
+                              else None)
     files = []
     for f in range(c["nfile"]):
         dDM = rng.normal(3e-4, 2e-4)            # example.py: one per archive
         subs = np.zeros((nsub, nchan, nbin))
+        if c.get("same_phi"):
+            phi0 = rng.uniform(-0.5, 0.5)
         for s in range(nsub):
-            phi = rng.uniform(-0.5, 0.5)
+            phi = phi0 if c.get("same_phi") else rng.uniform(-0.5, 0.5)
             subs[s] = S.subint(c["seed"] * 1000 + f * 100 + s, model, freqs,
-                               phi, S.DM0 + dDM, S.P0, scint=c.get("scint",
-                                                                   False))
+                               phi, S.DM0 + dDM, S.P0,
+                               nu0=c.get("nu0", 1500.0),
+                               tau=c.get("tau", 0.0),
+                               nu_tau=c.get("nu_tau", 1500.0),
+                               scint=c.get("scint", False))
         weights = np.ones((nsub, nchan))
         if f == 1 or c["nfile"] == 1:           # zap a few channels
             for s in range(nsub):
                 weights[s, rng.choice(nchan, 3 + s % 4, replace=False)] = 0.0
+        for s, nk in enumerate(c.get("chans", {}).get(f, [])):
+            if nk is not None:                  # keep only nk channels
+                weights[s] = 0.0
+                weights[s, rng.choice(nchan, nk, replace=False)] = 1.0
         dfs = 1.0 + 1e-4 * rng.normal(size=nsub)
         epochs = 57202.0 + 20.0 * f + np.arange(nsub) * 60.0 / 86400.0
+        pa = (np.linspace(-40.0, 40.0, nsub) + 7.0 * f if c.get("parangle")
+              else np.zeros(nsub))
+        if c.get("tscrunch"):
+            # what load_data(tscrunch=True) hands over: one sub-int, the
+            # mean of the sub-ints (same phase), channels usable in all
+            subs = S.f32(subs.mean(axis=0))[None]
+            weights = weights.min(axis=0)[None]
+            dfs, epochs, pa = dfs[:1], epochs.mean()[None], pa[:1]
         files.append(dict(subints=subs, weights=weights, dfs=dfs,
-                          epochs=epochs, dDM=dDM))
+                          epochs=epochs, dDM=dDM, parangles=pa))
     return files, freqs
+
+
+def archive_fields(c, fi, freqs, noise, snrs):
+    """The load_data DataBunch fields (pplib.py:2904-2914) of one synthetic
+    archive, apart from `epochs` (PSRCHIVE MJD objects, built by the
+    caller); noise [nsub, nchan], snrs [nsub, nchan]."""
+    subints = np.asarray(fi["subints"], dtype=np.float64)[:, None]
+    nsub = subints.shape[0]
+    nbin = int(c["nbin"])
+    nchan = len(freqs)
+    wn = np.where(fi["weights"] == 0.0, 0.0, 1.0)
+    return dict(
+        arch=None, backend="fake_be", backend_delay=0.0,
+        bw=float(c.get("bw", 800.0)), doppler_factors=fi["dfs"], DM=S.DM0,
+        dmc=0, flux_prof=np.array([]), freqs=np.tile(freqs, (nsub, 1)),
+        frontend="fake_rx", integration_length=60.0 * nsub,
+        masks=np.einsum("ij,k", wn, np.ones(nbin))[:, None], nbin=nbin,
+        nchan=nchan, noise_stds=np.asarray(noise)[:, None], npol=1,
+        nsub=nsub, nu0=float(c.get("lo", 1100.0) + c.get("bw", 800.0) / 2),
+        ok_ichans=[np.compress(wn[i], list(range(nchan)))
+                   for i in range(nsub)],
+        ok_isubs=np.arange(nsub), parallactic_angles=fi["parangles"],
+        prof=None, prof_noise=1.0, prof_SNR=100.0,
+        Ps=np.ones(nsub) * S.P0, SNRs=np.asarray(snrs)[:, None],
+        source="J1234-5678", state="Intensity", subints=subints,
+        subtimes=[60.0] * nsub, telescope="GBT", telescope_code="1",
+        weights=fi["weights"])
 
 
 ALIGNS = [

@@ -43,9 +43,10 @@ import make_golden as mg  # noqa: E402  (imports the reference with the shims)
 import make_golden_align as mga  # noqa: E402
 import numpy as np  # noqa: E402
 import synth_np as S  # noqa: E402
-from full_inputs import (FITS, TOAS, ALIGNS, NARROW_GMODEL, fit_inputs,  # noqa: E402
+from full_inputs import (FITS, TOAS, ALIGNS, fit_inputs,  # noqa: E402
                          toa_inputs, align_inputs, write_narrow, SPLINES,
-                         SPLINE_MODEL, write_spline)
+                         SPLINE_MODEL, write_spline, write_scat, toa_gmodel,
+                         archive_fields)
 
 OUT = os.path.join(HERE, "full.npz")
 
@@ -80,42 +81,35 @@ def run_toas(c):
     from pplib import DataBunch
     import psrchive as pr
     files_in, freqs = toa_inputs(c)
-    nchan, nbin, nsub = c["nchan"], c["nbin"], c["nsub"]
+    nbin = c["nbin"]
     files = {}
     out = {}
     hashes = []
     for f, fi in enumerate(files_in):
         subints = fi["subints"][:, None]
-        noise = np.array([[mg.pplib.get_noise(subints[i, 0], chans=True)]
-                          for i in range(nsub)])
-        snrs = np.abs(subints.max(axis=-1)) / noise * 3.0
-        wnorm = np.where(fi["weights"] == 0.0, 0.0, 1.0)
+        nsub_f = subints.shape[0]
+        noise = np.array([mg.pplib.get_noise(subints[i, 0], chans=True)
+                          for i in range(nsub_f)])
+        snrs = np.abs(subints[:, 0].max(axis=-1)) / noise * 3.0
         name = "%s_%d.fits" % (c["name"], f)
         files[name] = DataBunch(
-            arch=None, backend="fake_be", backend_delay=0.0, bw=800.0,
-            doppler_factors=fi["dfs"], DM=S.DM0, dmc=0,
             epochs=[pr.MJD(e) for e in fi["epochs"]], filename=name,
-            flux_prof=np.array([]), freqs=np.tile(freqs, (nsub, 1)),
-            frontend="fake_rx", integration_length=60.0 * nsub,
-            masks=np.einsum("ij,k", wnorm, np.ones(nbin))[:, None],
-            nbin=nbin, nchan=nchan, noise_stds=noise, npol=1, nsub=nsub,
-            nu0=1500.0, ok_ichans=[np.compress(wnorm[i], list(range(nchan)))
-                                   for i in range(nsub)],
-            ok_isubs=np.arange(nsub), parallactic_angles=np.zeros(nsub),
-            phases=mg.pplib.get_bin_centers(nbin), prof=None, prof_noise=1.0,
-            prof_SNR=100.0, Ps=np.ones(nsub) * S.P0, SNRs=snrs,
-            source="J1234-5678", state="Intensity", subints=subints,
-            subtimes=[60.0] * nsub, telescope="GBT", telescope_code="1",
-            weights=fi["weights"])
+            phases=mg.pplib.get_bin_centers(nbin),
+            **archive_fields(c, fi, freqs, noise, snrs))
         hashes.append(S.sha(fi["subints"].astype(np.float32)))
-        out["f%d_noise" % f] = noise[:, 0]
-        out["f%d_snrs" % f] = snrs[:, 0]
-    mg.pptoas.load_data = lambda filename, **kw: files[filename]
+        out["f%d_noise" % f] = noise
+        out["f%d_snrs" % f] = snrs
+
+    def loader(filename, **kw):
+        # load_data must be asked for the tscrunched archive exactly when
+        # get_TOAs was (pptoas.py:262-266)
+        assert bool(kw.get("tscrunch")) == bool(c.get("tscrunch")), kw
+        return files[filename]
+    mg.pptoas.load_data = loader
     gt = mg.pptoas.GetTOAs.__new__(mg.pptoas.GetTOAs)
     gt.datafiles = list(files.keys())
     gt.is_FITS_model = False
-    gt.modelfile = (NARROW_GMODEL if c.get("narrow") else SPLINE_MODEL if
-                    c.get("spline") else mg.GMODEL)
+    gt.modelfile = mg.GMODEL if toa_gmodel(c) == S.GMODEL else toa_gmodel(c)
     for attr in ["obs", "doppler_fs", "nu0s", "nu_fits", "nu_refs",
                  "ok_idatafiles", "ok_isubs", "epochs", "MJDs", "Ps", "phis",
                  "phi_errs", "TOAs", "TOA_errs", "DM0s", "DMs", "DM_errs",
@@ -131,13 +125,15 @@ def run_toas(c):
     gt.quiet = True
     t0 = time.time()
     with contextlib.redirect_stdout(io.StringIO()):
-        gt.get_TOAs(quiet=True, DM0=S.DM0 if c.get("DM0") else None)
+        gt.get_TOAs(quiet=True, DM0=S.DM0 if c.get("DM0") else None,
+                    **c.get("kw", {}))
     dt = time.time() - t0
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         mg.pplib.write_TOAs(gt.TOA_list)
-    out.update(nfile=np.int64(c["nfile"]), nsub=np.int64(nsub),
-               nchan=np.int64(nchan), nbin=np.int64(nbin),
+    out.update(nfile=np.int64(c["nfile"]),
+               nsub=np.int64(files_in[0]["subints"].shape[0]),
+               nchan=np.int64(c["nchan"]), nbin=np.int64(nbin),
                seed=np.int64(c["seed"]), scint=np.int64(bool(c.get("scint"))),
                narrow=np.int64(bool(c.get("narrow"))),
                DM0_given=np.int64(bool(c.get("DM0"))), P=np.float64(S.P0),
@@ -149,7 +145,10 @@ def run_toas(c):
         out["f%d_epochs" % f] = fi["epochs"]
     for key in ["phis", "phi_errs", "DMs", "DM_errs", "red_chi2s", "snrs",
                 "scales", "scale_errs", "channel_snrs", "covariances",
-                "DeltaDM_means", "DeltaDM_errs"]:
+                "DeltaDM_means", "DeltaDM_errs", "GMs", "GM_errs", "taus",
+                "tau_errs", "alphas", "alpha_errs", "fluxes", "flux_errs",
+                "flux_freqs", "profile_fluxes", "profile_flux_errs",
+                "nu_fits", "rcs", "nfevals"]:
         out["out_" + key] = np.array(getattr(gt, key), dtype=np.float64)
     out["out_nu_refs"] = np.array(gt.nu_refs, dtype=np.float64)
     out["out_tim_lines"] = np.array(buf.getvalue().splitlines())
@@ -201,8 +200,9 @@ def run_align(c):
                                    fit_dm=True, niter=c["niter"],
                                    outfile="aligned.fits", quiet=True)
     dt = time.time() - t0
-    out.update(nfile=np.int64(c["nfile"]), nsub=np.int64(nsub),
-               nchan=np.int64(nchan), nbin=np.int64(nbin),
+    out.update(nfile=np.int64(c["nfile"]),
+               nsub=np.int64(files_in[0]["subints"].shape[0]),
+               nchan=np.int64(c["nchan"]), nbin=np.int64(nbin),
                niter=np.int64(c["niter"]), seed=np.int64(c["seed"]),
                tmpl_nchan=np.int64(tn), P=np.float64(S.P0),
                DM0=np.float64(S.DM0), freqs=freqs, tfreqs=tfreqs,
@@ -278,6 +278,7 @@ def main():
         only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     write_narrow()
     write_spline()
+    write_scat()
     old = {}
     if os.path.exists(OUT):
         z = np.load(OUT)

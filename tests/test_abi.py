@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_struct_layouts_match():
     lib = _lib.load()
-    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 3
     assert lib.ppf_sizeof_fit_desc() == ctypes.sizeof(_lib.FitDesc)
     assert lib.ppf_sizeof_result() == 8 * _lib.RESULT_DOUBLES == 256
 
@@ -112,3 +112,33 @@ def test_x_subints_host_rule():
     assert engine.x_subints(flags, init, False, 4) == 3
     assert engine.x_subints(flags, init, True, 4) == 4       # 10**0 = 1
     assert engine.x_subints([1, 1, 0, 0, 0], np.zeros((3, 5)), False, 3) == 0
+
+
+def test_nospace_status_raises():
+    """PPF_ST_NOSPACE (a scattering fit without a cross-spectrum slot) is an
+    internal error: the host raises instead of writing an all-zero TOA
+    (ADVICE round 2)."""
+    import pytest
+    from pulseportraiture_amd import _lib
+    from pulseportraiture_amd.pplib import _raise_status
+    with pytest.raises(RuntimeError):
+        _raise_status(_lib.ST_NOSPACE | 2)
+    _raise_status(2)
+
+
+def test_box_bounds():
+    """scipy bounds lists -> the [5, 2] device box (NaN = unbounded)."""
+    import numpy as np
+    from pulseportraiture_amd.pplib import _box
+    assert _box(None, 5) is None
+    assert _box([(None, None)] * 5, 5) is None
+    b = _box([(None, None), (None, 40.0), (None, None), (-3.7, None),
+              (-10.0, 10.0)], 5)
+    assert b.shape == (5, 2)
+    np.testing.assert_array_equal(b[1], [np.nan, 40.0])
+    np.testing.assert_array_equal(b[3], [-3.7, np.nan])
+    np.testing.assert_array_equal(b[4], [-10.0, 10.0])
+    # pplib.fit_portrait: only (phase, DM)
+    b2 = _box([(-0.5, 0.5), (None, None), (0.0, 1.0)], 2)
+    np.testing.assert_array_equal(b2[0], [-0.5, 0.5])
+    assert np.isnan(b2[2]).all()

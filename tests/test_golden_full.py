@@ -22,7 +22,7 @@ def test_fit_inputs_rebuild(name):
     F.fit_case(name)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "narrow", "spline"])
+@pytest.mark.parametrize("name", [c["name"] for c in F.FI.TOAS])
 def test_toa_inputs_rebuild(name):
     F.toa_case(name)
 
@@ -77,6 +77,32 @@ def test_oracle_matches_reference_example_gettoas():
                                    rtol=RCHI2)
         assert abs(o["DeltaDM_mean"] - c["out_DeltaDM_means"][f]) < \
             SIG * c["out_DeltaDM_errs"][f]
+
+
+def test_oracle_matches_reference_scatfix_gettoas():
+    """configs[4]'s band (400-800 MHz, 128 x 1024): the oracle's GetTOAs loop
+    with scat_guess and alpha held (fit_flags [1, 1, 0, 1, 0]) against the
+    reference's get_TOAs(fit_scat=True, fix_alpha=True, scat_guess=...)."""
+    c, files, freqs, gm = F.toa_case("scatfix")
+    kw = F.toa_conf("scatfix")["kw"]
+    model = _gmodel_portrait(gm, freqs, int(c["nbin"]))
+    fi = files[0]
+    nsub = fi["subints"].shape[0]
+    o = O.get_toas_archive(fi["subints"].astype(np.float64), model,
+                           np.tile(freqs, (nsub, 1)), fi["weights"],
+                           fi["snrs"], np.full(nsub, float(c["P"])),
+                           float(c["DM0"]), fi["dfs"], noise_stds=fi["noise"],
+                           fit_flags=(1, 1, 0, 1, 0), log10_tau=True,
+                           scat_guess=kw["scat_guess"])
+    dphi = np.abs(G.phase_diff(o["phis"], c["out_phis"][0]))
+    assert np.all(dphi < SIG * c["out_phi_errs"][0])
+    for key, ix in (("DMs", 1), ("taus", 3)):
+        err = c["out_" + key[:-1] + "_errs"][0]
+        assert np.all(np.abs(o[key] - c["out_" + key][0]) < SIG * err), key
+        np.testing.assert_allclose(o["param_errs"][:, ix], err, rtol=1e-5)
+    np.testing.assert_array_equal(o["alphas"], c["out_alphas"][0])
+    np.testing.assert_allclose(o["red_chi2s"], c["out_red_chi2s"][0],
+                               rtol=RCHI2)
 
 
 def _gmodel_portrait(path, freqs, nbin):

@@ -106,29 +106,14 @@ class _MJD(object):
 def _archives(name):
     from pulseportraiture_amd.pplib import DataBunch, get_bin_centers
     c, files, freqs, gm = F.toa_case(name)
-    nchan, nbin = int(c["nchan"]), int(c["nbin"])
+    nbin = int(c["nbin"])
     out = {}
     for f, fi in enumerate(files):
-        nsub = fi["subints"].shape[0]
-        wn = np.where(fi["weights"] == 0.0, 0.0, 1.0)
         fname = "%s_%d.fits" % (name, f)
         out[fname] = DataBunch(
-            arch=None, backend="fake_be", backend_delay=0.0, bw=800.0,
-            doppler_factors=fi["dfs"], DM=float(c["DM0"]), dmc=0,
             epochs=[_MJD(e) for e in fi["epochs"]], filename=fname,
-            flux_prof=np.array([]), freqs=np.tile(freqs, (nsub, 1)),
-            frontend="fake_rx", integration_length=60.0 * nsub,
-            masks=np.einsum("ij,k", wn, np.ones(nbin))[:, None], nbin=nbin,
-            nchan=nchan, noise_stds=fi["noise"][:, None], npol=1, nsub=nsub,
-            nu0=1500.0, ok_ichans=[np.compress(wn[i], list(range(nchan)))
-                                   for i in range(nsub)],
-            ok_isubs=np.arange(nsub), parallactic_angles=np.zeros(nsub),
-            phases=get_bin_centers(nbin), prof=None, prof_noise=1.0,
-            prof_SNR=100.0, Ps=np.ones(nsub) * float(c["P"]),
-            SNRs=fi["snrs"][:, None, :], source="J1234-5678",
-            state="Intensity", subints=fi["subints"].astype(np.float64)[:, None],
-            subtimes=[60.0] * nsub, telescope="GBT", telescope_code="1",
-            weights=fi["weights"])
+            phases=get_bin_centers(nbin),
+            **F.toa_archive_fields(name, fi, freqs))
     return c, out, gm
 
 
@@ -176,22 +161,171 @@ def test_fullshape_gettoas_matches_reference(name, monkeypatch, tmp_path,
     capsys.readouterr()
     pplib.write_TOAs(gt.TOA_list)
     lines = capsys.readouterr().out.splitlines()
-    ref = list(c["out_tim_lines"])
+    # token 1, the TOA frequency, is the zero-covariance frequency nu_0,
+    # hypersensitive to the last bits of the per-channel Hessian sums
+    # ("Hard parts"); the phase AT it is held to 0.01 sigma
+    # above, nu_0 itself to 1e-8 (_tim_tokens_match)
+    _tim_tokens_match(lines, list(c["out_tim_lines"]))
+
+
+def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True):
     assert len(lines) == len(ref)
-    for a, b in zip(lines, ref):
+    for il, (a, b) in enumerate(zip(lines, ref)):
+        if il in skip_lines:
+            continue
         ta, tb = a.split(), b.split()
-        assert len(ta) == len(tb)
+        assert len(ta) == len(tb), (a, b)
         for i, (x, y) in enumerate(zip(ta, tb)):
             if x.endswith((".gmodel", ".spl")):   # -tmplt path differs
                 continue
+            if i in (1, 2) and not nu0_tokens:
+                continue
             if i == 1:
-                # the TOA frequency is the zero-covariance frequency nu_0,
-                # hypersensitive to the last bits of the per-channel Hessian
-                # sums ("Hard parts"); the phase AT it is held
-                # to 0.01 sigma above, nu_0 itself to 1e-8 here
+                # nu_0 (see test_fullshape_gettoas_matches_reference)
                 assert abs(float(x) / float(y) - 1) < 1e-8, (a, b)
                 continue
-            assert _same_printed_number(x, y), (a, b)
+            assert _same_printed_number(x, y), (i, a, b)
+
+
+BRANCHES = ["scatgm", "scatfix", "opts", "chan12", "tscr", "tnc", "tncscat",
+            "ncg"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", BRANCHES)
+def test_gettoas_branches_match_reference(name, monkeypatch, tmp_path,
+                                          capsys):
+    """GetTOAs.get_TOAs' non-default branches against the reference's own
+    runs (tests/golden/make_golden_full.py, full_inputs.TOAS):
+    fit_GM + fit_scat at 512 x 2048 with a .gmodel tau guess (configs[2]'s
+    entry), scat_guess + fix_alpha + print_flux at configs[4]'s band, user
+    nu_refs / nu_fits + print_phase / print_flux / print_parangle, 1- and
+    2-channel sub-ints under fit_GM (the carried-over fit_flags), tscrunch +
+    bary=False + linear tau, method='TNC' (default bounds; user bounds with
+    an active alpha bound) and method='Newton-CG'.  phi, DM, GM, tau, alpha
+    within 0.01 sigma of the reference's errors, chi2_red 1e-8, fluxes, and
+    every .tim token (gm, scat_time, log10_scat_time, scat_ind, phs, flux,
+    par_angle ...) to its printed precision.  Phases are compared at the
+    reference's nu_DM: a TNC fit stops within ~1e-9 of the
+    bounded stationary point, which moves nu_0 for phi + DM + tau + alpha
+    by ~1e-7 relative and the phase AT nu_0 by up to 0.2 sigma.  Sub-ints where the reference's
+    own TNC stopped unconverged (return code 3, MAXFUN: its maxfun of 100,
+    pptoaslib.py:1053 passes maxiter, which scipy ignores) are excluded from
+    the comparison and listed."""
+    from pulseportraiture_amd import pptoas, pplib
+    conf = F.toa_conf(name)
+    c, files, gm = _archives(name)
+
+    def loader(fn, **kw):
+        # tscrunch must reach load_data (pptoas.py:262-266)
+        assert bool(kw.get("tscrunch")) == bool(conf.get("tscrunch")), kw
+        return files[fn]
+    monkeypatch.setattr(pptoas, "load_data", loader)
+    monkeypatch.setattr(pptoas, "_MJD", _MJD)
+    meta = tmp_path / "meta.txt"
+    meta.write_text("".join(n + "\n" for n in files))
+    gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    kw = dict(conf.get("kw", {}))
+    gt.get_TOAs(quiet=True, **kw)
+    tnc = kw.get("method") == "TNC"
+    lt = bool(kw.get("fit_scat")) and kw.get("log10_tau", True)
+    P = float(c["P"])
+    skip, line = [], 0
+    for f in range(int(c["nfile"])):
+        conv = np.ones(len(c["out_phis"][f]), dtype=bool)
+        if tnc:
+            conv = c["out_rcs"][f] != 3
+        for i in np.where(~conv)[0]:
+            skip.append(line + int(i))
+        line += len(c["out_phis"][f])
+        dfs = files["%s_%d.fits" % (name, f)].doppler_factors \
+            if kw.get("bary", True) else np.ones(len(conv))
+        for s_ in np.where(conv)[0]:
+            # SURVEY.md A.5: the phase moved from this fit's nu_DM to the
+            # reference's with the fitted (topocentric) DM and GM, tau to
+            # its nu_tau with alpha
+            ferr = [c["out_" + k][f][s_] for k in
+                    ("phi_errs", "DM_errs", "GM_errs", "tau_errs",
+                     "alpha_errs")]
+            got = dict(params=[gt.phis[f][s_],
+                               gt.DMs[f][s_] / dfs[s_] if ferr[1] else
+                               gt.DMs[f][s_],
+                               gt.GMs[f][s_] / dfs[s_] ** 3 if ferr[2] else
+                               gt.GMs[f][s_], gt.taus[f][s_],
+                               gt.alphas[f][s_]])
+            got.update(zip(("nu_DM", "nu_GM", "nu_tau"),
+                           np.array(gt.nu_refs[f][s_], dtype=float)))
+            ref = dict(params=[c["out_phis"][f][s_],
+                               c["out_DMs"][f][s_] / dfs[s_] if ferr[1] else
+                               c["out_DMs"][f][s_],
+                               c["out_GMs"][f][s_] / dfs[s_] ** 3 if ferr[2]
+                               else c["out_GMs"][f][s_], c["out_taus"][f][s_],
+                               c["out_alphas"][f][s_]], param_errs=ferr)
+            ref.update(zip(("nu_DM", "nu_GM", "nu_tau"),
+                           c["out_nu_refs"][f][s_]))
+            dev = G.param_deviation_sigma(got, ref, P, lt)
+            assert dev.max() < SIG, (f, s_, dev)
+        for key in ("DMs", "GMs", "taus", "alphas"):
+            got, ref = np.asarray(getattr(gt, key)[f]), c["out_" + key][f]
+            err = c["out_" + key[:-1] + "_errs"][f]
+            # parameters a sub-int does not fit keep their initial value
+            held = conv & (err == 0)
+            np.testing.assert_allclose(got[held], ref[held], rtol=1e-12,
+                                       atol=1e-300, err_msg=key)
+            np.testing.assert_array_equal(
+                np.asarray(getattr(gt, key[:-1] + "_errs")[f])[held], 0.0)
+        np.testing.assert_allclose(gt.red_chi2s[f][conv],
+                                   c["out_red_chi2s"][f][conv], rtol=RCHI2)
+        np.testing.assert_allclose(gt.phi_errs[f][conv],
+                                   c["out_phi_errs"][f][conv], rtol=1e-5)
+        np.testing.assert_allclose(gt.snrs[f][conv], c["out_snrs"][f][conv],
+                                   rtol=1e-6)
+        np.testing.assert_allclose(
+            np.array(gt.nu_refs[f], dtype=float)[conv],
+            c["out_nu_refs"][f][conv], rtol=1e-6)
+        np.testing.assert_allclose(np.array(gt.nu_fits[f], dtype=float),
+                                   c["out_nu_fits"][f], rtol=1e-12)
+        cov, cref = np.asarray(gt.covariances[f])[conv], \
+            c["out_covariances"][f][conv]
+        np.testing.assert_allclose(cov, cref, rtol=1e-3,
+                                   atol=1e-6 * np.abs(cref).max())
+        if kw.get("print_flux"):
+            for key in ("fluxes", "flux_errs", "flux_freqs"):
+                np.testing.assert_allclose(
+                    np.asarray(getattr(gt, key)[f])[conv],
+                    c["out_" + key][f][conv], rtol=1e-5, err_msg=key)
+        if conv.all():
+            assert abs(gt.DeltaDM_means[f] - c["out_DeltaDM_means"][f]) < \
+                SIG * c["out_DeltaDM_errs"][f]
+    capsys.readouterr()
+    pplib.write_TOAs(gt.TOA_list)
+    lines = capsys.readouterr().out.splitlines()
+    # TNC: the reference's loosely converged x leaves nu_0 (token 1) and
+    # the TOA at it (token 2) off in their last printed digits; they are
+    # checked above through nu_refs (1e-6) and the transformed phase
+    _tim_tokens_match(lines, list(c["out_tim_lines"]), skip,
+                      nu0_tokens=not tnc)
+    if tnc and skip:
+        print("reference TNC unconverged (MAXFUN) on lines", skip)
+
+
+def test_gettoas_raises_when_x_slots_are_short(monkeypatch, tmp_path):
+    """A workspace with fewer cross-spectrum slots than scattering fits
+    (engine.x_subints' host count forced to 0) ends those fits with
+    PPF_ST_NOSPACE; get_TOAs raises instead of writing all-zero TOAs
+    (ADVICE round 2)."""
+    from pulseportraiture_amd import engine, pptoas
+    conf = F.toa_conf("tscr")
+    c, files, gm = _archives("tscr")
+    monkeypatch.setattr(pptoas, "load_data", lambda fn, **kw: files[fn])
+    monkeypatch.setattr(pptoas, "_MJD", _MJD)
+    monkeypatch.setattr(engine, "x_subints", lambda *a, **k: 0)
+    meta = tmp_path / "meta.txt"
+    meta.write_text("".join(n + "\n" for n in files))
+    gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    with pytest.raises(RuntimeError, match="NOSPACE"):
+        gt.get_TOAs(quiet=True, **conf["kw"])
+    assert gt.TOA_list == []
 
 
 # ------------------------------------------------------------ ppalign (C4) ---

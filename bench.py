@@ -50,14 +50,16 @@ def parse():
                     "GB of cross spectrum per call)")
     ap.add_argument("--fit", default="phase+DM",
                     choices=["phase+DM", "full", "scat", "align",
-                             "gettoas"],
+                             "gettoas", "single"],
                     help="phase+DM: configs[1] (the metric); full: configs[2] "
                     "fit (phi, DM, GM, tau, alpha) on data with injected "
                     "scattering; scat: configs[4] fit (phi, DM, tau, alpha), "
                     "CHIME-like band; align: configs[3] ppalign iteration "
                     "(--nsub archives, default shape 256 x 1024); gettoas: "
                     "end-to-end GetTOAs.get_TOAs over host archives of "
-                    "--arch-nsub sub-ints (default --nsub 2048)")
+                    "--arch-nsub sub-ints (default --nsub 2048); single: "
+                    "single-call latency of fit_portrait_full / fit_portrait /"
+                    " rotate_data at 64x512 and 512x2048")
     ap.add_argument("--arch-nsub", type=int, default=64,
                     help="sub-ints per archive for --fit gettoas")
     ap.add_argument("--pinned", action="store_true",
@@ -352,9 +354,11 @@ def bench_gettoas(args):
     the per-sub-int bookkeeping into TOA objects, pipelined across archives.
     One step = one get_TOAs call over every archive; the rate includes the
     PCIe upload and the host bookkeeping, so it is not
-    the kernel-path `value` of the headline line.  N > 1: every rank holds
-    every archive and fits its share of each archive's sub-ints, the tables
-    all-gathered (strong scaling: the archive set is fixed)."""
+    the kernel-path `value` of the headline line.  N > 1: the archives are
+    sharded over the ranks (GetTOAs' archive mode: a rank builds, loads and
+    fits only its own contiguous block of archives; the per-archive results
+    are gathered at the end; strong scaling: the archive set is fixed).
+    load_data is a dict lookup here: no PSRCHIVE read cost is charged."""
     import tempfile
     import torch
     from pulseportraiture_amd import dist, engine, pptoas, synth
@@ -364,11 +368,15 @@ def bench_gettoas(args):
     nchan, nbin, per = args.nchan, args.nbin, args.arch_nsub
     nfile = max(1, args.nsub // per)
     files = {}
+    a0, na = dist.shard(nfile, rank, world) if nfile >= world else (0, nfile)
     for f in range(nfile):
+        name = "synthetic_%04d.fits" % f
+        if not a0 <= f < a0 + na:
+            files[name] = None          # another rank's archive: never loaded
+            continue
         b = synth.make_batch(per, nchan, nbin, first=f * per, dev=dev)
         noise = engine.noise_rows(b["data"]).cpu().numpy()
         snrs = (b["data"].amax(dim=-1).double().cpu().numpy() / noise * 3.0)
-        name = "synthetic_%04d.fits" % f
         files[name] = DataBunch(
             arch=None, backend="fake_be", backend_delay=0.0, bw=800.0,
             doppler_factors=np.ones(per), DM=synth.DM0, dmc=0,
@@ -388,7 +396,12 @@ def bench_gettoas(args):
             telescope="GBT", telescope_code="1", weights=np.ones((per, nchan)))
         del b
     torch.cuda.synchronize(dev)
-    pptoas.load_data = lambda fn, **kw: files[fn]
+    def load(fn, **kw):
+        if files[fn] is None:
+            raise AssertionError("rank %d loaded another rank's archive %s"
+                                 % (rank, fn))
+        return files[fn]
+    pptoas.load_data = load
     pptoas._MJD = _Epoch
     tmp = tempfile.mkdtemp()
     gm = synth.write_gmodel(os.path.join(tmp, "example.gmodel"))
@@ -427,7 +440,11 @@ def bench_gettoas(args):
                            % (nfile, per, nchan, nbin), nfile=nfile,
                            host_memory="pinned" if args.pinned else "pageable",
                            nsub_per_archive=per, nchan=nchan, nbin=nbin,
-                           fit="gettoas", parallelism="dp%d" % world),
+                           fit="gettoas", parallelism="dp%d" % world,
+                           sharding="archives" if nfile >= world and
+                           world > 1 else "sub-ints" if world > 1 else None,
+                           load_data="in-memory dict lookup (no PSRCHIVE "
+                           "read cost charged)"),
                toas=len(gt.TOA_list), host_gb=round(
                    nfile * per * nchan * nbin * 4 / 1e9, 2),
                roofline=None, cpu_baseline=None)
@@ -436,8 +453,97 @@ def bench_gettoas(args):
     dist.barrier()
 
 
+def bench_single(args):
+    """Single-call latency of the drop-in APIs, one sub-integration per call
+    as ppgauss.py:318 (fit_portrait), DataPortrait (pplib.py:362-370,
+    rotate_data) and scripts calling fit_portrait_full directly use them:
+    each call uploads its host arrays, runs the batch-of-one device path and
+    returns host results (synchronised).  Shapes: configs[0]'s 64 x 512 and
+    configs[1]'s 512 x 2048.  Beside each, the oracle's time for the same
+    call on one core (its fit_portrait_full / fit_portrait / rotate_data
+    restatements of the reference)."""
+    import torch
+    import oracle.ppfit_oracle as O
+    from threadpoolctl import threadpool_limits
+    from pulseportraiture_amd import pplib, pptoaslib, synth
+    dev = torch.device("cuda", 0)
+    calls = {}
+    for nchan, nbin in ((64, 512), (512, 2048)):
+        b = synth.make_batch(1, nchan, nbin, dev=dev)
+        data = b["data"][0].cpu().numpy()
+        model, freqs, P = b["model"], b["freqs"], float(b["P"][0])
+        nu_fit = pplib.guess_fit_freq(freqs)
+        init = [float(b["phi_true"][0]) + 1e-3, synth.DM0, 0.0, 0.0, 0.0]
+        init[0] = float(O.phase_transform(init[0], synth.DM0, 1500.0, nu_fit,
+                                          P, mod=True))
+        errs = O.noise_ps(data.astype(np.float64))
+        ffl = [1, 1, 0, 0, 0]
+        api = {
+            "fit_portrait_full": (
+                lambda: pptoaslib.fit_portrait_full(
+                    data, model, init, P, freqs, [nu_fit] * 3, [None] * 3,
+                    errs, ffl, log10_tau=False),
+                lambda: O.fit_portrait_full(
+                    data.astype(np.float64), model, init, P, freqs,
+                    [nu_fit] * 3, [None] * 3, errs, ffl, log10_tau=False)),
+            "fit_portrait": (
+                lambda: pplib.fit_portrait(data, model, init[:2], P, freqs,
+                                           nu_fit, None, errs),
+                lambda: O.fit_portrait(data.astype(np.float64), model,
+                                       init[:2], P, freqs, nu_fit, None,
+                                       errs)),
+            "rotate_data": (
+                lambda: pplib.rotate_data(data, 0.1, synth.DM0, P, freqs,
+                                          1500.0),
+                lambda: O.rotate_data(data.astype(np.float64), 0.1,
+                                      synth.DM0, P, freqs, 1500.0)),
+        }
+        for name, (gpu, cpu) in api.items():
+            for _ in range(max(2, args.warmup)):
+                gpu()
+            torch.cuda.synchronize(dev)
+            ts = []
+            for _ in range(max(5, args.steps)):
+                t0 = time.perf_counter()
+                gpu()
+                ts.append(time.perf_counter() - t0)
+            with threadpool_limits(1):
+                cpu()
+                tc = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    cpu()
+                    tc.append(time.perf_counter() - t0)
+            calls["%s_%dx%d" % (name, nchan, nbin)] = dict(
+                gpu_ms_median=round(1e3 * float(np.median(ts)), 3),
+                gpu_ms_min=round(1e3 * float(np.min(ts)), 3),
+                cpu_oracle_ms_median=round(1e3 * float(np.median(tc)), 3),
+                speedup=round(float(np.median(tc) / np.median(ts)), 2))
+    key = "fit_portrait_full_64x512"
+    out = dict(metric="single-call latency of the drop-in APIs (one "
+                      "sub-integration per call, host arrays in and out)",
+               value=calls[key]["gpu_ms_median"], unit="ms",
+               n_gpus=1, steps=max(5, args.steps), warmup=max(2, args.warmup),
+               higher_is_better=False, scaling=None, vs_baseline=None,
+               dtype="f64", data="synthetic (example.gmodel portraits + "
+               "white noise; float32 amplitudes)",
+               config=dict(workload="fit_portrait_full / fit_portrait / "
+                           "rotate_data, one call per sub-int at 64x512 and "
+                           "512x2048 (value: fit_portrait_full 64x512)",
+                           fit="single"),
+               calls=calls, roofline=None,
+               cpu_baseline=dict(value=calls[key]["cpu_oracle_ms_median"],
+                                 unit="ms", cores=1, kind="port",
+                                 sample="the oracle's fit_portrait_full of "
+                                        "the same 64x512 sub-int, median of "
+                                        "3 calls"))
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.fit == "single":
+        return bench_single(args)
     if args.fit == "align":
         return bench_align(args)
     if args.fit == "gettoas":

@@ -18,7 +18,13 @@
  *     gives the message.  Per-sub-integration numerical outcomes are reported
  *     in ppf_result.status, never by aborting the batch.
  *   - nbin must be a power of two in [32, 8192].
- *   - Contexts are thread-compatible, not thread-safe.
+ *   - Threads: ppf_fit_batch / ppf_fit2_batch must not run concurrently on
+ *     the same context (they share its profiling event ring and pinned
+ *     iteration counter); any other entry point may run on another host
+ *     thread beside them (GetTOAs builds templates with
+ *     ppf_gauss_portrait_batch while a worker thread fits).  The twiddle
+ *     cache and the error message are guarded; ppf_last_error returns the
+ *     message as last set by any thread, copied for the calling thread.
  */
 #ifndef PPFIT_H
 #define PPFIT_H
@@ -269,6 +275,22 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin,
                           const double *model, const int32_t *model_index,
                           const double *noise, int32_t Ns, double lo,
                           double hi, double *out, void *stream);
+
+/* Maximum-likelihood channel amplitudes at given parameters:
+ * pptoaslib.get_scales_full (pptoaslib.py:953-971), a_n = C_n / S_n with
+ * S_n = sum_k |B_nk|^2 |M_nk|^2 / e_n^2 (Sbp) and
+ * C_n = Re sum_k D_nk conj(M_nk) conj(B_nk) exp(2 pi i k phi_n) / e_n^2 (Cdbp),
+ * phi_n = phase_shifts(phi, DM, GM, nu_n, nu_DM, nu_GM, P), B the one-sided
+ * exponential scattering FT at tau_n = tau (nu_n / nu_tau)^alpha
+ * (10**tau with log10_tau).  D: [nsub][nchan][nharm] complex (re, im pairs);
+ * M: [nmodel][nchan][nharm] complex with model_index[nsub] (NULL -> 0);
+ * errs_FT: [nsub][nchan] or NULL; params: [nsub][5]; P: [nsub];
+ * freqs: [nsub][nchan]; nus: [nsub][3] = nu_DM, nu_GM, nu_tau;
+ * out: [nsub][nchan]. */
+int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, const double *D,
+                     const double *M, const int32_t *model_index, const double *errs_FT,
+                     const double *params, const double *P, const double *freqs, const double *nus,
+                     int32_t log10_tau, double *out, void *stream);
 
 /* Gaussian-component model portraits: pplib.gen_gaussian_portrait
  * (pplib.py:886-963, join_ichans = []) as called by pplib.read_model

@@ -20,7 +20,7 @@ __all__ = [
     "fit_portrait_full", "fit_portrait", "rotate_rows", "rotate_data",
     "fit_phase_shift", "nu_zeros", "get_toas_archive", "align_archives",
     "channel_red_chi2s", "select_zap_channels", "gaussian_profile",
-    "gen_gaussian_portrait",
+    "gen_gaussian_portrait", "get_scales_full",
 ]
 
 DCONST = 0.000241 ** -1          # pplib.py:64-67 (Dconst = Dconst_trad)
@@ -461,6 +461,24 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
                 snr=snr, channel_snrs=channel_snrs, duration=duration,
                 nfeval=res.nfev, return_code=res.status, Sd=Sd,
                 fun=res.fun, x_fit=res.x)
+
+
+def get_scales_full(params, Dft, Mft, errs_FT, P, freqs, nu_DM, nu_GM,
+                    nu_tau, log10_tau):
+    """pptoaslib.py:953-971: a_n = C_n / S_n (Cdbp / Sbp, pptoaslib.py:421-469)
+    at given parameters from given spectra."""
+    phi, DM, GM, tau, alpha = params
+    if log10_tau:
+        tau = 10 ** tau
+    nharm = Dft.shape[-1]
+    phis = (phi + DCONST * DM * (freqs ** -2 - nu_DM ** -2) / P +
+            DCONST ** 2 * GM * (freqs ** -4 - nu_GM ** -4) / P)
+    E = np.exp(2.0j * np.pi * np.outer(phis, np.arange(nharm)))
+    B = _scat_B(tau * (freqs / nu_tau) ** alpha, nharm)
+    S = np.sum(np.abs(B) ** 2 * np.abs(Mft) ** 2, axis=-1) / errs_FT ** 2
+    C = np.real(np.sum(Dft * np.conj(Mft) * np.conj(B) * E, axis=-1)) / \
+        errs_FT ** 2
+    return C / S
 
 
 def _schur_covariance(t, flags):

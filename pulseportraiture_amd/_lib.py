@@ -98,6 +98,9 @@ SIGNATURES = {
     "ppf_phase_shift_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp,
                                              _vp, _vp, _i32, ctypes.c_double,
                                              ctypes.c_double, _vp, _vp]),
+    "ppf_scales_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                        _vp]),
     "ppf_gauss_portrait_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32,
                                                 ctypes.c_char_p, _vp, _vp, _vp,
                                                 _vp, _vp, _vp]),

@@ -19,7 +19,8 @@
 
 struct ppf_ctx {
     int device;
-    std::string err;
+    std::string err;               // last error message, guarded by err_mu
+    mutable std::mutex err_mu;
     std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
     std::mutex tw_mu;              // guards tw (calls from several host threads)
     bool prof = false;
@@ -45,7 +46,10 @@ int fail(ppf_ctx *ctx, int code, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    if (ctx) ctx->err = buf;
+    if (ctx) {
+        std::lock_guard<std::mutex> lk(ctx->err_mu);
+        ctx->err = buf;
+    }
     return code;
 }
 
@@ -284,7 +288,15 @@ int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4) {
     return n == 1 ? PPF_OK : fail(ctx, PPF_EINVAL, "no profiled call yet");
 }
 
-const char *ppf_last_error(const ppf_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char *ppf_last_error(const ppf_ctx *ctx) {
+    if (!ctx) return "null context";
+    // a copy per calling thread: another thread's failure cannot rewrite the
+    // buffer this pointer refers to
+    thread_local std::string copy;
+    std::lock_guard<std::mutex> lk(ctx->err_mu);
+    copy = ctx->err;
+    return copy.c_str();
+}
 
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc) {
     if (!desc || desc->nsub < 1 || desc->nchan < 1 || !pow2_in_range(desc->nbin)) return 0;
@@ -628,6 +640,23 @@ int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
     if (rc) return rc;
     ppf::NoiseArgs a{nbin, ilog2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
     if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise");
+    return PPF_OK;
+}
+
+int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, const double *D,
+                     const double *M, const int32_t *model_index, const double *errs_FT,
+                     const double *params, const double *P, const double *freqs, const double *nus,
+                     int32_t log10_tau, double *out, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nsub < 0 || nchan < 1 || nharm < 1 ||
+        (nsub > 0 && (!D || !M || !params || !P || !freqs || !nus || !out)))
+        return fail(ctx, PPF_EINVAL, "bad scales arguments");
+    if (nsub == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    ppf::ScalesArgs a{nsub, nchan, nharm, log10_tau != 0, (const double2 *)D, (const double2 *)M,
+                      model_index, errs_FT, params, P, freqs, nus, out};
+    if ((e = ppf::launch_scales(a, (hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e, "k_scales");
     return PPF_OK;
 }
 

@@ -192,6 +192,21 @@ struct SynthArgs {
     void *out;
 };
 
+// pptoaslib.get_scales_full (pptoaslib.py:953-971) per (sub-int, channel) row
+struct ScalesArgs {
+    int nsub, nchan, nharm, log10_tau;
+    const double2 *D;            // [nsub][nchan][nharm] data spectra
+    const double2 *M;            // [nmodel][nchan][nharm] model spectra
+    const int32_t *model_index;  // [nsub] or null (model 0)
+    const double *errs_FT;       // [nsub][nchan] or null (no division)
+    const double *params;        // [nsub][5]
+    const double *P;             // [nsub]
+    const double *freqs;         // [nsub][nchan]
+    const double *nus;           // [nsub][3] nu_DM, nu_GM, nu_tau
+    double *out;                 // [nsub][nchan]
+};
+hipError_t launch_scales(const ScalesArgs &a, hipStream_t st);
+
 // pplib.gen_gaussian_portrait (pplib.py:886-963) per (portrait, channel) row
 struct GaussArgs {
     int nport, nchan, nbin, log2N, ngauss, npar;

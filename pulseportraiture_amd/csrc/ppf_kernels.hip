@@ -1318,4 +1318,64 @@ hipError_t launch_spline_port(const SplineArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// k_scales: pptoaslib.get_scales_full (pptoaslib.py:953-971) -- a_n = C_n/S_n
+// at given parameters from given spectra, one wave per (sub-int, channel):
+//   phi_n = phase_shifts(phi, DM, GM, nu_n, nu_DM, nu_GM, P)  (pptoaslib.py:195-228)
+//   tau_n = tau (nu_n / nu_tau)^alpha                         (pplib.py:4212-4216)
+//   B_k = 1 / (1 + 2 pi i k tau_n), 1 where tau_n == 0        (pplib.py:4219-4260)
+//   S_n = sum_k |B_k|^2 |M_k|^2 / e_n^2                        (Sbp, pptoaslib.py:421-428)
+//   C_n = Re sum_k D_k conj(M_k) conj(B_k) e^{2 pi i k phi_n} / e_n^2  (Cdbp, 458-469)
+// The phasor is taken with exact argument reduction (cexp2pi); the lanes'
+// partial sums are reduced in fixed order.
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_scales(ScalesArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (row >= (int64_t)a.nsub * a.nchan) return;
+    const int s = (int)(row / a.nchan), n = (int)(row % a.nchan);
+    const double *pr = a.params + (int64_t)s * 5;
+    const double P = a.P[s], nu = a.freqs[row];
+    const double nuDM = a.nus[s * 3 + 0], nuGM = a.nus[s * 3 + 1], nutau = a.nus[s * 3 + 2];
+    const double phi_n = pr[0] + kDconst * pr[1] * (pow(nu, -2.0) - pow(nuDM, -2.0)) / P +
+                         kDconst * kDconst * pr[2] * (pow(nu, -4.0) - pow(nuGM, -4.0)) / P;
+    const double tau = a.log10_tau ? pow(10.0, pr[3]) : pr[3];
+    const double tau_n = tau * pow(nu / nutau, pr[4]);
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const double2 *D = a.D + row * a.nharm;
+    const double2 *M = a.M + ((int64_t)mi * a.nchan + n) * a.nharm;
+    double C = 0.0, S = 0.0;
+    for (int k = lane; k < a.nharm; k += 64) {
+        const double2 m = M[k];
+        const double2 y = cmulc(D[k], m);
+        const double2 e = cexp2pi((double)k * phi_n);
+        double2 t = cmul(y, e);
+        double b2 = 1.0;
+        if (tau_n != 0.0) {
+            // conj(B) = 1 / (1 - i u), u = 2 pi k tau_n: (1 + i u) / (1 + u^2)
+            const double u = kTwoPi * (double)k * tau_n, den = 1.0 / (1.0 + u * u);
+            t = cmul(t, cmk(den, u * den));
+            b2 = den;
+        }
+        C += t.x;
+        S += b2 * cabs2(m);
+    }
+    C = wave_sum(C);
+    S = wave_sum(S);
+    if (lane == 0) {
+        if (a.errs_FT) {
+            const double e2 = a.errs_FT[row] * a.errs_FT[row];
+            C /= e2;
+            S /= e2;
+        }
+        a.out[row] = C / S;
+    }
+}
+
+hipError_t launch_scales(const ScalesArgs &a, hipStream_t st) {
+    const int64_t rows = (int64_t)a.nsub * a.nchan;
+    hipLaunchKernelGGL(k_scales, dim3((unsigned)((rows + kWaves - 1) / kWaves)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace ppf

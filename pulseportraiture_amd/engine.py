@@ -387,6 +387,51 @@ def noise_rows(rows, frac=4, dev=None):
     return out.reshape(shape[:-1])
 
 
+def scales_batch(D, M, params, P, freqs, nus, log10_tau, errs_FT=None,
+                 model_index=None, dev=None):
+    """get_scales_full (pptoaslib.py:953-971) per sub-int: D [nsub, nchan,
+    nharm] complex data spectra, M [nmodel, nchan, nharm] complex model
+    spectra (or [nchan, nharm]), params [nsub, 5], P [nsub], freqs
+    [nsub, nchan], nus [nsub, 3]; returns a_n [nsub, nchan] float64."""
+    dev = device(dev)
+    c128 = torch.complex128
+    D_t = to_dev(D, dev, c128)
+    if D_t.dim() == 2:
+        D_t = D_t.unsqueeze(0)
+    nsub, nchan, nharm = D_t.shape
+    M_t = to_dev(M, dev, c128)
+    if M_t.dim() == 2:
+        M_t = M_t.unsqueeze(0)
+    if M_t.shape[1:] != (nchan, nharm):
+        raise ValueError("model spectra %s != [*, %d, %d]" %
+                         (tuple(M_t.shape), nchan, nharm))
+    f64 = torch.float64
+    pr = to_dev(params, dev, f64).reshape(nsub, 5).contiguous()
+    P_t = to_dev(np.broadcast_to(np.asarray(P, dtype=float), (nsub,)).copy()
+                 if not isinstance(P, torch.Tensor) else P, dev, f64)
+    fr = to_dev(freqs, dev, f64).reshape(-1)
+    if fr.numel() == nchan:
+        fr = fr.repeat(nsub)
+    fr = fr.reshape(nsub, nchan).contiguous()
+    nu = to_dev(nus, dev, f64).reshape(-1)
+    if nu.numel() == 3:
+        nu = nu.repeat(nsub)
+    nu = nu.reshape(nsub, 3).contiguous()
+    e_t = None if errs_FT is None else \
+        to_dev(errs_FT, dev, f64).reshape(-1)
+    if e_t is not None and e_t.numel() == nchan:
+        e_t = e_t.repeat(nsub)
+    mi = None if model_index is None else \
+        to_dev(model_index, dev, torch.int32).reshape(nsub).contiguous()
+    out = torch.empty((nsub, nchan), dtype=f64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_scales_batch(
+        ctx, nsub, nchan, nharm, _p(D_t), _p(M_t), _p(mi), _p(e_t), _p(pr),
+        _p(P_t), _p(fr), _p(nu), int(bool(log10_tau)), _p(out), _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
 def phase_shift_batch(data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
                       model_index=None, dev=None):
     """Batched pplib.fit_phase_shift: data [nprof, nbin], model

@@ -12,6 +12,8 @@ import os
 import sys
 import time
 
+import pickle
+
 import numpy as np
 
 from . import _lib, engine
@@ -230,22 +232,48 @@ def gen_spline_portrait(mean_prof, freqs, eigvec, tck, nbin=None):
     return out[0].cpu().numpy()
 
 
+class _SplineUnpickler(pickle.Unpickler):
+    """The reference reads spline models with a plain pickle.load
+    (pplib.py:3083-3088), which runs whatever a crafted file names.  The
+    6-tuple of strings, numpy arrays and splprep's tck needs only numpy's
+    array reconstruction and a few builtins; any other global is refused."""
+    _ALLOWED = {
+        ("numpy.core.multiarray", "_reconstruct"),
+        ("numpy._core.multiarray", "_reconstruct"),
+        ("numpy.core.multiarray", "scalar"),
+        ("numpy._core.multiarray", "scalar"),
+        ("numpy", "ndarray"), ("numpy", "dtype"),
+        ("builtins", "list"), ("builtins", "tuple"), ("builtins", "int"),
+        ("builtins", "float"), ("builtins", "str"), ("builtins", "bytes"),
+        ("__builtin__", "list"), ("__builtin__", "tuple"),
+        ("_codecs", "encode"), ("copy_reg", "_reconstructor"),
+        ("copyreg", "_reconstructor"), ("__builtin__", "object"),
+        ("builtins", "object"),
+    }
+
+    def find_class(self, module, name):
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError("spline model file names %s.%s, which "
+                                     "a spline model never holds" %
+                                     (module, name))
+
+
 def read_spline_model(modelfile, freqs=None, nbin=None, quiet=False):
     """pplib.py:3060-3096: a make_spline_model(...) file -- the pickled
     (model name, source, datafile, mean profile, eigenvectors, tck) -- read
     as the reference reads it; with freqs, the portrait built on the device
     by gen_spline_portrait."""
-    import pickle
     if not quiet:
         print("Reading model from %s..." % modelfile)
     try:
         with open(modelfile, "rb") as fh:
             modelname, source, datafile, mean_prof, eigvec, tck = \
-                pickle.load(fh)
+                _SplineUnpickler(fh).load()
     except UnicodeDecodeError:       # python2 to python3 pickling issues
         with open(modelfile, "rb") as fh:
             modelname, source, datafile, mean_prof, eigvec, tck = \
-                pickle.load(fh, encoding="bytes")
+                _SplineUnpickler(fh, encoding="bytes").load()
     if freqs is None:
         return (modelname, source, datafile, mean_prof, eigvec, tck)
     return (modelname, gen_spline_portrait(mean_prof, freqs, eigvec, tck,

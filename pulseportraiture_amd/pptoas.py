@@ -152,6 +152,34 @@ class _Stager(object):
         self.bufs, self.events = [None, None], [None, None]
 
 
+class MJDValue(object):
+    """A picklable stand-in for a TOA epoch that cannot be pickled (a
+    PSRCHIVE MJD is a SWIG object): the integer and fractional day
+    write_TOAs prints (pplib.py:3612-3648), as the original object gave
+    them."""
+
+    def __init__(self, intday, fracday):
+        self._i, self._f = int(intday), float(fracday)
+
+    def intday(self):
+        return self._i
+
+    def fracday(self):
+        return self._f
+
+    def in_days(self):
+        return self._i + self._f
+
+
+def _picklable_toa(toa):
+    import pickle
+    try:
+        pickle.dumps(toa.MJD)
+    except Exception:
+        toa.MJD = MJDValue(toa.MJD.intday(), toa.MJD.fracday())
+    return toa
+
+
 def _table_width(nchan):
     return _lib.RESULT_DOUBLES + 3 * nchan + 25
 
@@ -339,8 +367,24 @@ class GetTOAs(object):
         self.tscrunch = tscrunch
         self.add_instrumental_response = add_instrumental_response
         self._ff = [None]   # fit_flags carried across sub-ints (pptoas.py:519-529)
+        # With several ranks and at least as many archives as ranks, each
+        # rank loads and fits only its own contiguous block of archives
+        # (pptoas.py:258) and the per-archive results are
+        # gathered at the end; a single archive (or fewer archives than
+        # ranks) is sharded by sub-int instead (_prep_archive).  So is a
+        # fit_DM + fit_GM run: its fit_flags list carries over from one
+        # archive to the next (the 2-channel rule, pptoas.py:523-525), which
+        # only a rank that has seen every earlier archive can reproduce.
+        rank, world = _rank_world()
+        by_archive = world > 1 and len(datafiles) >= world and \
+            not (self.fit_DM and self.fit_GM)
+        mine = range(len(datafiles))
+        if by_archive:
+            a0, na = _dist.shard(len(datafiles), rank, world)
+            mine = range(a0, a0 + na)
+            marks = {a: len(getattr(self, a)) for a in _ATTRS}
         ctx = dict(quiet=quiet, tscrunch=tscrunch, fit_scat=fit_scat,
-                   method=method, bounds=[bounds],
+                   method=method, bounds=[bounds], by_archive=by_archive,
                    nu_fit_tuple=nu_fit_tuple, nu_ref_tuple=nu_ref_tuple,
                    bary=bary, print_phase=print_phase, print_flux=print_flux,
                    print_parangle=print_parangle,
@@ -349,15 +393,14 @@ class GetTOAs(object):
         # archive i (a worker thread on its own HIP stream; ppf_fit_batch
         # releases the GIL), this thread loads archive i+1, builds its batch
         # and starts its upload from pinned memory on a copy stream; then it
-        # does archive i's bookkeeping.  With torch.distributed initialised
-        # (world > 1), every rank fits a contiguous share of each archive's
-        # sub-ints and the full result tables are all-gathered (dist.py).
+        # does archive i's bookkeeping.
         stager = _Stager()
         pool = ThreadPoolExecutor(max_workers=1)
         pending = None
+        err = None
         try:
-            for iarch, datafile in enumerate(datafiles):
-                job = self._prep_archive(iarch, datafile, ctx, stager)
+            for iarch in mine:
+                job = self._prep_archive(iarch, datafiles[iarch], ctx, stager)
                 if job is None:
                     continue
                 fut = pool.submit(self._fit_archive, job, ctx)
@@ -367,9 +410,49 @@ class GetTOAs(object):
                 pending = (job, fut)
             if pending is not None:
                 self._book_archive(pending[0], pending[1].result(), ctx, start)
+        except Exception as exc:            # every rank raises, below
+            if not by_archive:
+                raise
+            err = exc
         finally:
             pool.shutdown(wait=True)
             stager.close()
+        if by_archive:
+            # a failed rank must not leave the others in the gather
+            _dist.raise_if_any_failed(err)
+            self._gather_archives(marks)
+
+    def _gather_archives(self, marks):
+        """Archive-sharded get_TOAs: every rank's per-archive results (one
+        entry per archive in each per-archive attribute, the archive's TOAs)
+        are all-gathered as objects and re-assembled in archive order, so
+        every rank ends with the attributes and TOA list of a serial run."""
+        import torch.distributed as tdist
+        per = [a for a in _ATTRS if a not in ("ok_idatafiles", "TOA_list",
+                                              "channel_red_chi2s",
+                                              "zap_channels")]
+        mine = self.ok_idatafiles[marks["ok_idatafiles"]:]
+        recs = []
+        ntoa = [len(np.asarray(v)) for v in self.ok_isubs[marks["ok_isubs"]:]]
+        toas = self.TOA_list[marks["TOA_list"]:]
+        pos = 0
+        for j, iarch in enumerate(mine):
+            rec = {a: getattr(self, a)[marks[a] + j] for a in per}
+            rec["_toas"] = [_picklable_toa(t) for t in toas[pos:pos + ntoa[j]]]
+            rec["_iarch"] = iarch
+            pos += ntoa[j]
+            recs.append(rec)
+        allrecs = [None] * tdist.get_world_size()
+        tdist.all_gather_object(allrecs, recs)
+        merged = sorted((r for rr in allrecs for r in rr),
+                        key=lambda r: r["_iarch"])
+        for a in _ATTRS:
+            del getattr(self, a)[marks[a]:]
+        for r in merged:
+            self.ok_idatafiles.append(r["_iarch"])
+            for a in per:
+                getattr(self, a).append(r[a])
+            self.TOA_list.extend(r["_toas"])
 
     # ------------------------------------------------------------------
     def _prep_archive(self, iarch, datafile, ctx, stager):
@@ -525,7 +608,7 @@ class GetTOAs(object):
             else:
                 self._ff[0] = list(np.copy(self.fit_flags))
             flags_b[j] = self._ff[0]
-        rank, world = _rank_world()
+        rank, world = (0, 1) if ctx["by_archive"] else _rank_world()
         first, count = _dist.shard(nok, rank, world)
         sel = ok_isubs[first:first + count]
         if count and sel == list(range(sel[0], sel[0] + count)):

@@ -170,19 +170,13 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
 
 def get_scales_full(params, data_portrait_FT, model_portrait_FT, errs_FT, P,
                     freqs, nu_DM, nu_GM, nu_tau, log10_tau):
-    """pptoaslib.py:953-971: a_n = C_n / S_n at given params.  Takes
-    pre-computed spectra, so it is host arithmetic on small arrays (not on the
-    batched hot path, which returns scales from the device fit)."""
-    phi, DM, GM, tau, alpha = params
-    if log10_tau:
-        tau = 10 ** tau
-    nharm = data_portrait_FT.shape[-1]
-    phis = phase_shifts(phi, DM, GM, freqs, nu_DM, nu_GM, P, False)
-    E = np.exp(2.0j * np.pi * np.outer(phis, np.arange(nharm)))
-    B = scattering_portrait_FT(scattering_times(tau, alpha, freqs, nu_tau),
-                               2 * (nharm - 1))
-    S = np.sum(np.abs(B) ** 2 * np.abs(model_portrait_FT) ** 2, axis=-1) / \
-        errs_FT ** 2
-    C = np.real(np.sum(data_portrait_FT * np.conj(model_portrait_FT) *
-                       np.conj(B) * E, axis=-1)) / errs_FT ** 2
-    return C / S
+    """pptoaslib.py:953-971: a_n = C_n / S_n at given params, from the given
+    data and model spectra, on the GPU (ppf_scales_batch, k_scales: one wave
+    per channel, the phasor with exact argument reduction)."""
+    D = np.asarray(data_portrait_FT)
+    out = engine.scales_batch(
+        D, np.asarray(model_portrait_FT), np.asarray(params, dtype=float),
+        float(P), np.asarray(freqs, dtype=float),
+        [float(nu_DM), float(nu_GM), float(nu_tau)], log10_tau,
+        errs_FT=None if errs_FT is None else np.asarray(errs_FT, dtype=float))
+    return out[0].cpu().numpy()

@@ -178,3 +178,118 @@ def test_gettoas_table_gather_matches_serial():
     ref = {k: v.numpy() for k, v in _fake_results(0, n_total, nchan).items()}
     for k in ref:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+# ---------------------------------------------------------------------------
+# GetTOAs sharded by archive (pptoas.GetTOAs.get_TOAs with world > 1 and at
+# least as many archives as ranks): each rank runs only its own block of
+# archives; the per-archive attributes and TOAs are gathered in archive order
+# ---------------------------------------------------------------------------
+class _UnpicklableMJD(object):
+    """Stands in for a PSRCHIVE MJD (a SWIG object pickle refuses)."""
+
+    def __init__(self, days):
+        self.days = days
+
+    def intday(self):
+        return int(self.days)
+
+    def fracday(self):
+        return self.days - int(self.days)
+
+    def __reduce__(self):
+        raise TypeError("cannot pickle a SWIG object")
+
+
+def _fake_gettoas(nfile, skip=()):
+    """A GetTOAs whose device stages are replaced by deterministic per-archive
+    bookkeeping (values keyed by the archive index): exercises get_TOAs'
+    archive partition, its error path and _gather_archives."""
+    from pulseportraiture_amd import pptoas
+
+    class G(pptoas.GetTOAs):
+        def __init__(self):
+            for a in pptoas._ATTRS:
+                setattr(self, a, [])
+            self.datafiles = ["a%d.fits" % i for i in range(nfile)]
+            self.quiet = True
+            self.seen = []
+
+        def _prep_archive(self, iarch, datafile, ctx, stager):
+            self.seen.append(iarch)
+            if iarch in skip:                 # load_data failed: skipped
+                return None
+            self.ok_idatafiles.append(iarch)
+            return dict(iarch=iarch, datafile=datafile, nsub=2 + iarch % 3)
+
+        def _fit_archive(self, job, ctx):
+            return None
+
+        def _book_archive(self, job, r, ctx, start):
+            i, n = job["iarch"], job["nsub"]
+            for a in pptoas._ATTRS:
+                if a in ("ok_idatafiles", "TOA_list", "channel_red_chi2s",
+                         "zap_channels"):
+                    continue
+                getattr(self, a).append(np.arange(n) * 1.5 + 100 * i +
+                                        len(a))
+            self.ok_isubs[-1] = np.arange(n)
+            for s in range(n):
+                self.TOA_list.append(pptoas.TOA(
+                    job["datafile"], 1400.0 + s, _UnpicklableMJD(
+                        57000.0 + i + s / 7.0), 0.5, "GBT", "1", 34.5 + s,
+                    1e-3, {"subint": s}))
+    return G()
+
+
+def _summary(gt):
+    from pulseportraiture_amd import pptoas
+    out = {a: [np.asarray(v).tolist() for v in getattr(gt, a)]
+           for a in pptoas._ATTRS if a != "TOA_list"}
+    out["TOA_list"] = [(t.archive, t.frequency, t.MJD.intday(),
+                        t.MJD.fracday(), t.DM, dict(t.flags))
+                       for t in gt.TOA_list]
+    return out
+
+
+def _archive_worker(rank, world, port, nfile, skip, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    sys.path.insert(0, os.path.dirname(__file__))
+    import test_dist_gloo as T
+    pdist.init("gloo")
+    gt = T._fake_gettoas(nfile, skip)
+    gt.get_TOAs(quiet=True)
+    q.put((rank, gt.seen, T._summary(gt)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nfile,skip", [(5, ()), (4, (1,)), (2, ())])
+def test_gettoas_archive_sharding_equals_serial(nfile, skip):
+    """Every rank loads only its contiguous block of archives (none twice,
+    none missed) and ends with exactly the serial run's per-archive
+    attributes and TOA list (archive order; skipped archives absent; PSRCHIVE
+    MJDs that cannot be pickled travel as their printed int/frac day)."""
+    serial = _fake_gettoas(nfile, skip)
+    serial.get_TOAs(quiet=True)
+    ref = _summary(serial)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_archive_worker,
+                         args=(r, 2, port, nfile, skip, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (seen, summ)) for r, seen, summ in
+               (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(got[0][0] + got[1][0]) == list(range(nfile))
+    assert got[0][0] == list(range(len(got[0][0])))
+    for r in (0, 1):
+        assert got[r][1] == ref

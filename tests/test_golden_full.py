@@ -125,11 +125,11 @@ def test_oracle_matches_reference_align_duplicate_channels():
                                atol=1e-6 * np.abs(ref).max())
 
 
-def test_get_scales_full_matches_reference():
-    """pptoaslib.get_scales_full (pptoaslib.py:953-971) against the
+def test_oracle_get_scales_full_matches_reference():
+    """The oracle's get_scales_full (pptoaslib.py:953-971) against the
     reference's own output on a scattering case's spectra: log10 and linear
-    tau, tau = 0 (B = 1), fitted and arbitrary parameters."""
-    from pulseportraiture_amd import pptoaslib
+    tau, tau = 0 (B = 1), fitted and arbitrary parameters (the device path
+    is checked against the same vectors in test_gpu_fullshape.py)."""
     g = F.case("scales", "scales")
     c = G.full_case(str(g["case"]))
     data = c["data"].astype(np.float64)
@@ -142,10 +142,10 @@ def test_get_scales_full_matches_reference():
     errs_FT = c["errs"] * np.sqrt(nbin / 2.0)
     for i in range(4):
         nus = g["s%d_nus" % i]
-        got = pptoaslib.get_scales_full(list(g["s%d_params" % i]), dFT, mFT,
-                                        errs_FT, float(c["P"]), c["freqs"],
-                                        nus[0], nus[1], nus[2],
-                                        bool(g["s%d_log10_tau" % i]))
+        got = O.get_scales_full(list(g["s%d_params" % i]), dFT, mFT,
+                                errs_FT, float(c["P"]), c["freqs"],
+                                nus[0], nus[1], nus[2],
+                                bool(g["s%d_log10_tau" % i]))
         np.testing.assert_allclose(got, g["s%d_out" % i], rtol=1e-12,
                                    atol=1e-14 * np.abs(g["s%d_out" % i]).max())
 

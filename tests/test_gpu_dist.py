@@ -1,8 +1,11 @@
 """Multi-rank GetTOAs on the GPU: two ranks (one process each, both on the
-box's one GPU, collectives over gloo) shard every archive's sub-ints
-(pptoas.py:258, 384) and all-gather the full result tables (results,
-scales, scale_errs, channel_snrs, covariance); the sharded run's tables and
-.tim lines are bit-identical to the serial run's."""
+box's one GPU, collectives over gloo).  With at least as many archives as
+ranks (c1: 5 archives) each rank loads and fits only its own block of
+archives and the per-archive results are gathered (pptoas.py:258); a single
+archive (c2) is sharded by sub-int (pptoas.py:384) and the full result
+tables (results, scales, scale_errs, channel_snrs, covariance) are
+all-gathered.  Either way the sharded run's tables and .tim lines are
+bit-identical to the serial run's."""
 import io
 import os
 import socket
@@ -110,7 +113,7 @@ def _bench_rank(rank, world, port, args):
         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
 
 
-@pytest.mark.parametrize("fit", ["phase+DM", "align"])
+@pytest.mark.parametrize("fit", ["phase+DM", "align", "gettoas"])
 def test_bench_two_ranks_rehearsal(fit):
     """bench.py's N > 1 path (sharding, the result all-gather, max-over-ranks
     timing, rank-0 JSON) run as two processes on the box's one GPU over gloo,
@@ -120,6 +123,10 @@ def test_bench_two_ranks_rehearsal(fit):
     args = ["--gpus", "2", "--dist-backend", "gloo", "--nsub", "48",
             "--nchan", "64", "--nbin", "512", "--steps", "1", "--warmup",
             "1", "--passes", "1", "--cpu-sample", "0", "--fit", fit]
+    if fit == "gettoas":
+        # 6 archives of 8 sub-ints: archive-sharded GetTOAs (each rank
+        # loads only its own three; the loader asserts it)
+        args += ["--arch-nsub", "8"]
     procs = [_bench_rank(r, 2, port, args) for r in range(2)]
     outs = [p.communicate(timeout=240)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
@@ -130,3 +137,5 @@ def test_bench_two_ranks_rehearsal(fit):
     assert not any(ln.startswith("{") for ln in outs[1].splitlines())
     if fit == "phase+DM":
         assert d["fits_converged_frac"] == 1.0
+    if fit == "gettoas":
+        assert d["toas"] == 48 and d["config"]["sharding"] == "archives"

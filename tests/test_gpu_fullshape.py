@@ -328,6 +328,35 @@ def test_gettoas_raises_when_x_slots_are_short(monkeypatch, tmp_path):
     assert gt.TOA_list == []
 
 
+def test_get_scales_full_matches_reference():
+    """pptoaslib.get_scales_full (pptoaslib.py:953-971) on the GPU
+    (ppf_scales_batch) against the reference's own output on a scattering
+    case's spectra: log10 and linear tau, tau = 0 (B = 1), fitted and
+    arbitrary parameters.  The device takes the phasor with exact argument
+    reduction where NumPy rounds 2 pi k phi_n (|2 pi k phi| ~ 1e3 at 64 x 512:
+    ~1e-13 relative), hence rtol 1e-11."""
+    from pulseportraiture_amd import pptoaslib
+    g = F.case("scales", "scales")
+    c = G.full_case(str(g["case"]))
+    data = c["data"].astype(np.float64)
+    model = c["model"].astype(np.float64)
+    nbin = data.shape[1]
+    dFT = np.fft.rfft(data, axis=1)
+    dFT[:, 0] *= 0
+    mFT = np.fft.rfft(model, axis=1)
+    mFT[:, 0] *= 0
+    errs_FT = c["errs"] * np.sqrt(nbin / 2.0)
+    for i in range(4):
+        nus = g["s%d_nus" % i]
+        got = pptoaslib.get_scales_full(list(g["s%d_params" % i]), dFT, mFT,
+                                        errs_FT, float(c["P"]), c["freqs"],
+                                        nus[0], nus[1], nus[2],
+                                        bool(g["s%d_log10_tau" % i]))
+        ref = g["s%d_out" % i]
+        np.testing.assert_allclose(got, ref, rtol=1e-11,
+                                   atol=1e-13 * np.abs(ref).max())
+
+
 # ------------------------------------------------------------ ppalign (C4) ---
 @pytest.mark.parametrize("name", ["c4", "dup"])
 def test_fullshape_align_matches_reference(name, monkeypatch):

@@ -76,6 +76,10 @@ def parse():
                     help="sum every harmonic (PPF_OPT_NO_HCUT: no per-channel "
                     "cutoff of harmonics below 1e-28 of the template's peak "
                     "power)")
+    ap.add_argument("--solver", default="newton", choices=["newton", "scipy"],
+                    help="minimiser of the scattering fits (--fit full/scat): "
+                    "the Newton trust region (default) or scipy trust-ncg's "
+                    "own path (PPF_OPT_SCIPY_TR)")
     ap.add_argument("--cpu-sample", type=int, default=48,
                     help="sub-integrations for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -634,6 +638,7 @@ def main():
                     chan_mask=None if mask_t is None else mask_t[sl],
                     dev=dev, workspace=ws,
                     n_x=(c1 - c0) if n_x_all else 0, no_hcut=args.no_hcut,
+                    solver=args.solver,
                     max_workspace=1 << 62)
                 ws = res["workspace"]
                 outs.append(res["results"])
@@ -793,6 +798,7 @@ def main():
                            fits_per_step=total * args.passes,
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
                            harmonic_cutoff=not args.no_hcut,
+                           solver=args.solver,
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),

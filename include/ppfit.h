@@ -68,13 +68,23 @@ enum ppf_option {
     PPF_OPT_NO_HCUT = 1,     /* sum every harmonic: no per-channel cutoff of
                                 the harmonics whose template power is below
                                 1e-28 of the channel's peak */
-    PPF_OPT_NO_X = 2         /* the caller has checked that no sub-int
+    PPF_OPT_NO_X = 2,        /* the caller has checked that no sub-int
                                 streams the cross spectrum (no scattering
                                 flag, zero initial tau): on the fused
                                 phase+DM path no X slot is reserved and the
                                 cross-spectrum pass is not launched (a
                                 sub-int that would need X ends with
                                 PPF_ST_NOSPACE) */
+    PPF_OPT_SCIPY_TR = 4     /* scattering fits follow scipy's trust-ncg
+                                path step by step (pptoaslib.py:1055-1060:
+                                radius 1 in raw parameter units, CG-Steihaug
+                                subproblem).  Default: the Newton trust
+                                region (scaled coordinates, exact
+                                subproblem), which stops at the same
+                                stationary point in 3-4x fewer passes over
+                                the cross spectrum.  Fits
+                                without scattering and bounded (TNC) fits
+                                always take the scipy path. */
 };
 
 enum ppf_mode {
@@ -344,6 +354,13 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
  * root count or a negative value on failure.  The same code runs on the
  * device inside ppf_fit_batch; this export exists for CPU tests. */
 int ppf_poly_real_roots_host(const double *coeffs, int deg, double *out);
+
+/* Host-side (CPU) helper: the exact trust-region subproblem of the Newton
+ * solver, min g.p + p.H p / 2 over |p| <= R for a symmetric n x n H
+ * (row-major, n <= 5).  Writes p[n]; returns 1 if the step is on the
+ * boundary, 0 if interior, negative on a bad argument.  The same code runs
+ * on the device; this export exists for CPU tests. */
+int ppf_tr_subproblem_host(const double *H, const double *g, int n, double R, double *p);
 
 #ifdef __cplusplus
 }

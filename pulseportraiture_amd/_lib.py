@@ -22,6 +22,7 @@ ST_NO_ROOT, ST_SINGULAR, ST_NONFINITE, ST_NOFIT = 0x100, 0x200, 0x400, 0x800
 ST_NOSPACE = 0x1000
 OPT_NO_HCUT = 1           # ppf_fit_desc.options
 OPT_NO_X = 2
+OPT_SCIPY_TR = 4          # scattering fits follow scipy's trust-ncg path
 ABI_VERSION = 3
 
 # ppf_result: 32 doubles (include/ppfit.h)
@@ -112,6 +113,8 @@ SIGNATURES = {
                                        ctypes.c_double, ctypes.c_uint64,
                                        ctypes.c_int64, _i32, _vp, _vp]),
     "ppf_poly_real_roots_host": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+    "ppf_tr_subproblem_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int,
+                                              ctypes.c_double, _vp]),
 }
 
 _lib = None
@@ -176,3 +179,18 @@ def poly_real_roots(coeffs):
     if n < 0:
         raise RuntimeError("root finder failed")
     return out[:n]
+
+
+def tr_subproblem(H, g, R):
+    """Host (CPU) helper: the Newton solver's exact trust-region step
+    (p, hits_boundary) for a symmetric H [n, n], g [n], radius R."""
+    lib = load()
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    n = g.size
+    p = np.zeros(n)
+    rc = lib.ppf_tr_subproblem_host(H.ctypes.data, g.ctypes.data, n,
+                                    float(R), p.ctypes.data)
+    if rc < 0:
+        raise ValueError("bad trust-region subproblem arguments")
+    return p, bool(rc)

@@ -418,6 +418,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.bounds = d->bounds;
     sa.log10_tau = d->log10_tau; sa.option = d->option; sa.is_toa = d->is_toa; sa.mode = d->mode;
     sa.max_iter = d->max_iter; sa.guess = d->guess; sa.x0 = (double *)(ws + L.x0);
+    sa.newton = (d->options & PPF_OPT_SCIPY_TR) ? 0 : 1;
     sa.stats = (double *)(ws + L.stats); sa.results = d->results; sa.scales = d->scales;
     sa.scale_errs = d->scale_errs; sa.channel_snrs = d->channel_snrs; sa.covariance = d->covariance;
     sa.any_plain = 1;
@@ -785,6 +786,22 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, con
 int ppf_poly_real_roots_host(const double *coeffs, int deg, double *out) {
     if (!coeffs || !out || deg < 0 || deg > 8) return -2;
     return ppf::poly_real_roots(coeffs, deg, out);
+}
+
+int ppf_tr_subproblem_host(const double *H, const double *g, int n, double R, double *p) {
+    if (!H || !g || !p || n < 1 || n > 5 || !(R > 0.0)) return -1;
+    double A[5][5];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) A[i][j] = H[i * n + j];
+    bool hb = false;
+    switch (n) {
+        case 1: hb = ppf::tr_exact<1>(A, g, R, p); break;
+        case 2: hb = ppf::tr_exact<2>(A, g, R, p); break;
+        case 3: hb = ppf::tr_exact<3>(A, g, R, p); break;
+        case 4: hb = ppf::tr_exact<4>(A, g, R, p); break;
+        default: hb = ppf::tr_exact<5>(A, g, R, p); break;
+    }
+    return hb ? 1 : 0;
 }
 
 }  // extern "C"

@@ -425,6 +425,161 @@ __device__ bool cg_steihaug(const TRModel &m, double jac_mag, double R, double *
 }
 
 // ---------------------------------------------------------------------------
+// Exact trust-region subproblem for the Newton solver of the scattering fits
+// (PPF_TR_NEWTON): min_p g.p + p.H p / 2 subject to |p| <= R, H symmetric
+// N x N (N <= 5), by the eigendecomposition of H (cyclic Jacobi) and Newton
+// iterations on the secular equation 1/|p(l)| = 1/R, p(l) = -(H + l I)^-1 g
+// (More & Sorensen 1983; Nocedal & Wright, Numerical Optimization, alg. 4.3,
+// with the "hard case" of a g orthogonal to the lowest eigenvector).
+// Returns hits_boundary; p (length N) is the step.  __host__ as well so the
+// CPU tests check it against a NumPy restatement (ppf_tr_subproblem_host).
+// ---------------------------------------------------------------------------
+template <int N>
+__host__ __device__ inline void sym_eig_jacobi(double (&A)[5][5], double (&V)[5][5]) {
+    #pragma unroll
+    for (int i = 0; i < N; ++i)
+        #pragma unroll
+        for (int j = 0; j < N; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        double off = 0.0, dia = 0.0;
+        #pragma unroll
+        for (int p = 0; p < N; ++p) {
+            dia += A[p][p] * A[p][p];
+            #pragma unroll
+            for (int q = p + 1; q < N; ++q) off += A[p][q] * A[p][q];
+        }
+        if (!(off > 1e-34 * dia)) break;
+        #pragma unroll
+        for (int p = 0; p < N; ++p) {
+            #pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = A[p][q];
+                if (apq == 0.0) continue;
+                const double th = (A[q][q] - A[p][p]) / (2.0 * apq);
+                const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                #pragma unroll
+                for (int k = 0; k < N; ++k) {          // A J
+                    const double akp = A[k][p], akq = A[k][q];
+                    A[k][p] = c * akp - s * akq;
+                    A[k][q] = s * akp + c * akq;
+                }
+                #pragma unroll
+                for (int k = 0; k < N; ++k) {          // J^T (A J)
+                    const double apk = A[p][k], aqk = A[q][k];
+                    A[p][k] = c * apk - s * aqk;
+                    A[q][k] = s * apk + c * aqk;
+                }
+                A[p][q] = A[q][p] = 0.0;
+                #pragma unroll
+                for (int k = 0; k < N; ++k) {          // V J
+                    const double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = c * vkp - s * vkq;
+                    V[k][q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+}
+
+template <int N>
+__host__ __device__ inline bool tr_exact(const double (&H)[5][5], const double *g, double R, double *p) {
+    double A[5][5], V[5][5], lam[5], gp[5], q[5];
+    #pragma unroll
+    for (int i = 0; i < N; ++i)
+        #pragma unroll
+        for (int j = 0; j < N; ++j) A[i][j] = H[i][j];
+    sym_eig_jacobi<N>(A, V);
+    int imin = 0;
+    double gn2 = 0.0;
+    #pragma unroll
+    for (int i = 0; i < N; ++i) {
+        lam[i] = A[i][i];
+        if (lam[i] < lam[imin]) imin = i;
+        double s = 0.0;
+        #pragma unroll
+        for (int k = 0; k < N; ++k) s += V[k][i] * g[k];
+        gp[i] = s;
+        gn2 += s * s;
+    }
+    const double lmin = lam[imin];
+    bool hb = true;
+    if (lmin > 0.0) {
+        double n2 = 0.0;
+        #pragma unroll
+        for (int i = 0; i < N; ++i) { q[i] = gp[i] / lam[i]; n2 += q[i] * q[i]; }
+        if (n2 <= R * R) hb = false;      // interior Newton step
+    }
+    if (hb) {
+        const double lo = lmin > 0.0 ? 0.0 : -lmin;
+        // hard case: g (almost) orthogonal to the lowest eigenvector and the
+        // step at l = lo inside the region -> add that eigenvector
+        if (lmin <= 0.0 && fabs(gp[imin]) <= 1e-10 * sqrt(gn2)) {
+            double n2 = 0.0;
+            #pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const double d = lam[i] + lo;
+                q[i] = (i == imin || d <= 0.0) ? 0.0 : gp[i] / d;
+                n2 += q[i] * q[i];
+            }
+            if (n2 < R * R) {
+                q[imin] = -sqrt(R * R - n2);      // p = -V q below
+                #pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    double s = 0.0;
+                    #pragma unroll
+                    for (int i = 0; i < N; ++i) s += V[k][i] * q[i];
+                    p[k] = -s;
+                }
+                return true;
+            }
+        }
+        // iterate on the shift e = l - lo >= 0 with d_i = (lam_i + lo) + e
+        // (exactly e for the lowest eigenvalue when lo = -lam_min: no
+        // cancellation when lo is large).  Start where |p| >= R (|p| >=
+        // |gp_min| / e and |p| >= |g| / (e + lo + lam_max)): Newton on
+        // 1/|p| - 1/R from there increases e monotonically to the root
+        double sh[5], lmax = lam[0];
+        #pragma unroll
+        for (int i = 0; i < N; ++i) { sh[i] = (i == imin && lo > 0.0) ? 0.0 : lam[i] + lo; lmax = fmax(lmax, lam[i]); }
+        double e = fmax(fabs(gp[imin]) / R, sqrt(gn2) / R - lmax - lo);
+        if (!(e > 0.0)) e = 1e-300;
+        for (int it = 0; it < 100; ++it) {
+            double n2 = 0.0, w = 0.0;
+            #pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const double d = sh[i] + e;
+                q[i] = gp[i] / d;
+                n2 += q[i] * q[i];
+                w += q[i] * q[i] / d;
+            }
+            const double nq = sqrt(n2);
+            if (fabs(nq - R) <= 1e-13 * R || !(w > 0.0)) break;
+            double en = e + (n2 / w) * (nq - R) / R;
+            if (!(en > 0.0)) en = 0.5 * e;
+            if (en == e) break;
+            e = en;
+        }
+        double n2 = 0.0;
+        #pragma unroll
+        for (int i = 0; i < N; ++i) { q[i] = gp[i] / (sh[i] + e); n2 += q[i] * q[i]; }
+        if (n2 > R * R) {                 // round onto the sphere
+            const double sc = R / sqrt(n2);
+            #pragma unroll
+            for (int i = 0; i < N; ++i) q[i] *= sc;
+        }
+    }
+    #pragma unroll
+    for (int k = 0; k < N; ++k) {
+        double s = 0.0;
+        #pragma unroll
+        for (int i = 0; i < N; ++i) s += V[k][i] * q[i];
+        p[k] = -s;
+    }
+    return hb;
+}
+
+// ---------------------------------------------------------------------------
 // small dense inverse (Gauss-Jordan, partial pivoting); returns false if
 // singular.  n <= 5.
 // ---------------------------------------------------------------------------

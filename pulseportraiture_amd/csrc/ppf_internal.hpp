@@ -103,6 +103,7 @@ struct SolveArgs {
     const double *nu_fits, *nu_outs;
     const double *bounds;        // [nsub][5][2] (NaN: none) or null
     int log10_tau, option, is_toa, mode, max_iter, guess;
+    int newton;                  // 1: scattering fits use the Newton trust region (not PPF_OPT_SCIPY_TR)
     const double *x0;
     double *stats;               // [nsub][2][nchan][10]
     ppf_result *results;
@@ -262,6 +263,11 @@ hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st);
 hipError_t launch_moments(const SolveArgs &a, hipStream_t st);
 hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st);
 constexpr int kMoments = 32;     // Taylor moments per channel
+// Newton trust region of the scattering fits (ppf_solve.hip tr_update_newton):
+// initial radius in Jacobi-scaled units (~sigma), and the predicted reduction
+// of the objective (chi^2 units) below which the fit has converged
+constexpr double kNewtonR0 = 10.0;
+constexpr double kNewtonTol = 1e-12;
 hipError_t launch_postfit(const SolveArgs &a, hipStream_t st);
 size_t tr_state_bytes();
 int pass_blocks(int nchan);

@@ -25,6 +25,12 @@
 
 namespace ppf {
 
+// Newton trust region also for the moment-expansion fits (phase / DM / GM
+// without scattering); 0: those always follow scipy's trust-ncg path
+#ifndef PPF_NEWTON_MOM
+#define PPF_NEWTON_MOM 0
+#endif
+
 // ===========================================================================
 // per-channel likelihood terms (pptoaslib.py:195-561)
 // stats: 0 C, 1 C', 2 C'', 3 Q1, 4 Q1', 5 Q2, 6 S, 7 S1, 8 S2a, 9 S2b
@@ -240,7 +246,11 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         for (int i = 0; i < 5; ++i) { S.x[i] = x[i]; S.th[i] = x[i]; S.g[i] = 0.0; }
         S.f = 0.0;
         for (int i = 0; i < 15; ++i) S.H[i] = 0.0;
-        S.radius = 1.0;                 // scipy initial_trust_radius
+        // scattering fits without bounds take the Newton trust region
+        // (tr_update_newton) unless the caller asked for scipy's path
+        S.newton = (a.newton && (scat || PPF_NEWTON_MOM) && !bnd) ? 1 : 0;
+        S.radius = S.newton ? kNewtonR0 : 1.0;   // scipy initial_trust_radius = 1
+        S.pnorm = 0.0;
         S.pred = 0.0;
         for (int i = 0; i < 3; ++i) S.nu_fit[i] = nu_fit[i];
         S.nu_mean = nu_mean;
@@ -653,6 +663,117 @@ __device__ int tr_update_t(TRState &S, const double *o, int max_iter, const int 
     S.phase = done ? PH_DONE : PH_PROPOSAL;
     return cmd;
 }
+// ===========================================================================
+// Newton trust region (the default for scattering fits; PPF_OPT_SCIPY_TR
+// selects the scipy replica above).  It minimises the same objective
+// (pptoaslib.py:564-684) to the same stationary point, in fewer evaluations,
+// each of which is a pass over the cross spectrum:
+//   - the step is taken in Jacobi-scaled coordinates z_i = sqrt|H_ii| x_i,
+//     where a unit step moves the objective by O(1) (about 1 sigma) in every
+//     parameter: scipy's radius is in raw units (rotations, pc cm^-3, log10 s)
+//     and its CG-Steihaug solve stops at the loose tolerance
+//     min(0.5, sqrt|g|) |g|, so on these badly conditioned 5-parameter
+//     problems it alternates short boundary and inexact-Newton steps
+//     (27-52 evaluations against 7-22 here, tools/tr_probe.py);
+//   - the subproblem is solved exactly (tr_exact: eigendecomposition and the
+//     secular equation), so an interior step is the full Newton step;
+//   - radius: initial kNewtonR0, x4 on a boundary step with rho > 0.75,
+//     0.25 |p| when rho < 0.25, accept when rho > 0.15 (scipy's eta);
+//   - stop when the step's predicted reduction is <= kNewtonTol: the point is
+//     then within ~sqrt(kNewtonTol) sigma of the stationary point, where the
+//     reference's own trust-ncg ends at its rounding floor (~5e-5 sigma).
+// ===========================================================================
+template <int NF>
+__device__ int tr_update_newton(TRState &S, const double *o, int max_iter, const int (&idx)[5]) {
+    const int maxiter = max_iter > 0 ? max_iter : 200 * 5;
+    bool done = false;
+    int cmd = 0;
+    if (S.phase == PH_INIT) {
+        S.nfev = 1;
+        S.f = o[0];
+        for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+        for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+        if (!(o[0] == o[0])) { S.status = PPF_ST_NONFINITE; done = true; }
+        S.macc = S.meval;
+    } else {
+        S.nfev += 1;
+        const double fp = o[0];
+        const double rho = (S.f - fp) / S.pred;      // S.pred: predicted reduction
+        if (rho < 0.25) S.radius = 0.25 * S.pnorm;
+        else if (rho > 0.75 && S.hb) S.radius = fmin(4.0 * S.radius, 1e6);
+        if (rho > 0.15) {
+            for (int i = 0; i < 5; ++i) S.x[i] = S.th[i];
+            S.f = fp;
+            for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
+            for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
+            S.slot_cur = S.slot_eval;
+            S.macc = S.meval;
+        }
+        S.k += 1;
+        if (!(fp == fp)) { S.status = PPF_ST_NONFINITE; done = true; }
+        if (S.k >= maxiter) { S.status = PPF_ST_MAXITER; done = true; }
+    }
+    if (!done) {
+        double g[5], H[5][5], d[5], p[5];
+#pragma unroll
+        for (int q = 0; q < NF; ++q) d[q] = sqrt(fmax(fabs(S.H[uidx(idx[q], idx[q])]), 1e-300));
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            g[q] = S.g[idx[q]] / d[q];
+#pragma unroll
+            for (int r = 0; r < NF; ++r) {
+                const int i = min(idx[q], idx[r]), j = max(idx[q], idx[r]);
+                H[q][r] = S.H[uidx(i, j)] / (d[q] * d[r]);
+            }
+        }
+        const bool hb = tr_exact<NF>(H, g, S.radius, p);
+        double gp = 0.0, pHp = 0.0, pn = 0.0;
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            double s = 0.0;
+#pragma unroll
+            for (int r = 0; r < NF; ++r) s += H[q][r] * p[r];
+            gp += g[q] * p[q];
+            pHp += p[q] * s;
+            pn += p[q] * p[q];
+        }
+        const double pred = -(gp + 0.5 * pHp);
+        if (!(pred > kNewtonTol)) {
+            done = true;                 // converged (scipy's warnflag 2 status)
+        } else {
+            for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
+#pragma unroll
+            for (int q = 0; q < NF; ++q) S.th[idx[q]] = S.x[idx[q]] + p[q] / d[q];
+            S.pred = pred;
+            S.pnorm = sqrt(pn);
+            S.hb = hb ? 1 : 0;
+            S.slot_eval = S.slot_cur ^ 1;
+            cmd = 1;
+        }
+    }
+    S.phase = done ? PH_DONE : PH_PROPOSAL;
+    return cmd;
+}
+
+template <int MAXNF = 5>
+__device__ int tr_update_newton_n(TRState &S, const double *o, int max_iter) {
+    int idx[5] = {0, 0, 0, 0, 0}, nf = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        if (S.flagmask >> i & 1) idx[nf++] = i;
+    switch (nf) {
+        case 1: return tr_update_newton<1>(S, o, max_iter, idx);
+        case 2: return tr_update_newton<2>(S, o, max_iter, idx);
+        default:
+            if constexpr (MAXNF <= 3) return tr_update_newton<3>(S, o, max_iter, idx);
+            else {
+                if (nf == 3) return tr_update_newton<3>(S, o, max_iter, idx);
+                if (nf == 4) return tr_update_newton<4>(S, o, max_iter, idx);
+                return tr_update_newton<5>(S, o, max_iter, idx);
+            }
+    }
+}
+
 // MAXNF: the largest subspace the caller can meet (3 for the moment path,
 // which never fits tau/alpha; instantiating only those keeps its registers
 // down).  BOX: the instantiation also handles method='TNC' bounds.
@@ -706,7 +827,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     for (int i = 0; i < 21; ++i) o[i] = wave_sum(o[i]);
     int cmd = 0;
     if (lane == 0) {
-        cmd = tr_update<5, BOX>(S, o, a.max_iter);
+        cmd = S.newton ? tr_update_newton_n<5>(S, o, a.max_iter) : tr_update<5, BOX>(S, o, a.max_iter);
         for (int i = 0; i < 5; ++i) thb[wave][i] = S.th[i];
         thb[wave][5] = (double)cmd;
     }
@@ -1025,7 +1146,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
 #pragma unroll
             for (int e = 0; e < 6; ++e) o[6 + uidx(hi[e], hj[e])] = acc[4 + e];
             L.meval = qsel;
+#if PPF_NEWTON_MOM
+            cmdb = L.newton ? tr_update_newton_n<3>(L, o, a.max_iter) : tr_update<3>(L, o, a.max_iter);
+#else
             cmdb = tr_update<3>(L, o, a.max_iter);
+#endif
         }
         __syncthreads();
         if (!cmdb) break;

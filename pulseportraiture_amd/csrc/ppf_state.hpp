@@ -19,7 +19,7 @@ struct TRState {
     int k, status, nfev, phase;
     int slot_cur, slot_eval, flagmask, nchanx;
     int scat, hb, g_sum, g_tau;
-    int g_alpha, pad0, pad1, pad2;
+    int g_alpha, newton, pad1, pad2;   // newton: PPF_TR_NEWTON solver (see tr_update_newton)
     // moment mode (no scattering): two moment sets centred at mc[q]
     int mmode, need_mom, mtarget, macc;
     int mvalid[2], meval, nmom;
@@ -28,6 +28,7 @@ struct TRState {
     // bnd = 0: none on any fitted parameter (lo = -inf, hi = +inf)
     double lo[5], hi[5];
     int bnd, pad3;
+    double pnorm;         // Newton solver: |scaled step| of the pending proposal
 };
 
 __device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j

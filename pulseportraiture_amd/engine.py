@@ -7,6 +7,7 @@ returns device tensors; the drop-in modules (pplib / pptoaslib / pptoas)
 convert to the reference's numpy/DataBunch forms.
 """
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -82,13 +83,23 @@ def x_subints(fit_flags, init, log10_tau, nsub):
                                 (tau0 != 0.0)))
 
 
+SOLVER = os.environ.get("PPF_SOLVER", "newton")
+
+
+def _solver(name):
+    name = SOLVER if name is None else name
+    if name not in ("newton", "scipy"):
+        raise ValueError("solver must be 'newton' or 'scipy', not %r" % name)
+    return name
+
+
 def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               nu_outs=None, errs=None, chan_mask=None, model_index=None,
               log10_tau=False, option=0, is_toa=True, mode=_lib.PPF_MODE_FULL,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
               guess_Ns=100, guess_tau=None, dev=None, workspace=None,
               n_x=None, no_hcut=False, max_workspace=None, guess_ref=0,
-              bounds=None):
+              bounds=None, solver=None):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
@@ -99,6 +110,10 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     frequency then phase_transform to nu_fit, GetTOAs; 1: nu_fit, ppalign).
     bounds: method='TNC' box, [5, 2] or [nsub, 5, 2] (lower, upper; None or
     NaN = unbounded), or None for an unbounded fit.
+    solver: minimiser of the scattering fits, "newton" (scaled Newton trust
+    region with an exact subproblem: the same stationary point in 3-4x fewer
+    passes over the cross spectrum) or "scipy" (scipy trust-ncg's own path,
+    PPF_OPT_SCIPY_TR); None = SOLVER (env PPF_SOLVER, default "newton").
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
@@ -175,7 +190,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     xsel = None
     cfg = dict(model=model_t, log10_tau=log10_tau, option=option,
                is_toa=is_toa, mode=mode, max_iter=max_iter, guess=guess,
-               guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref)
+               guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref,
+               solver=_solver(solver))
     lib = _lib.load()
     need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
     if need <= (64 << 20) or nsub == 1:
@@ -240,7 +256,8 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.guess_tau = pp(per_sub["gtau"])
     d.x_subints = int(max(n_x, 1)) if n_x < (c1 - c0) else 0
     d.options = (_lib.OPT_NO_HCUT if cfg["no_hcut"] else 0) | \
-        (_lib.OPT_NO_X if n_x == 0 else 0)
+        (_lib.OPT_NO_X if n_x == 0 else 0) | \
+        (_lib.OPT_SCIPY_TR if cfg.get("solver") == "scipy" else 0)
     d.guess_ref = int(cfg["guess_ref"])
     d.bounds = pp(per_sub["bounds"])
     return d

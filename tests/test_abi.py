@@ -142,3 +142,54 @@ def test_box_bounds():
     b2 = _box([(-0.5, 0.5), (None, None), (0.0, 1.0)], 2)
     np.testing.assert_array_equal(b2[0], [-0.5, 0.5])
     assert np.isnan(b2[2]).all()
+
+
+def _tr_problem(rng, t):
+    """A random trust-region subproblem: PD, indefinite, badly scaled and
+    hard-case (g orthogonal to the lowest eigenvector) instances."""
+    n = int(rng.integers(1, 6))
+    A = rng.normal(size=(n, n))
+    H = A @ A.T
+    if t % 3 == 1:
+        H -= rng.uniform(0, 3) * np.eye(n)
+    if t % 7 == 0:
+        D = np.diag(10 ** rng.uniform(-4, 3, size=n))
+        H = D @ H @ D
+    if t % 11 == 0 and n > 1:
+        _, Q = np.linalg.eigh(H)
+        g = Q[:, 1:] @ rng.normal(size=n - 1)
+    else:
+        g = rng.normal(size=n) * 10 ** rng.uniform(-3, 3)
+    return H, g, 10 ** rng.uniform(-3, 2)
+
+
+def test_tr_subproblem_optimality():
+    """The Newton solver's exact trust-region step (ppf_device.hpp tr_exact,
+    host export) meets the More-Sorensen optimality conditions: |p| <= R,
+    (H + l I) p = -g with l >= 0, l (R - |p|) = 0 and H + l I positive
+    semi-definite; its model value is no worse than any point of a random
+    sample of the ball."""
+    rng = np.random.default_rng(0)
+    for t in range(3000):
+        H, g, R = _tr_problem(rng, t)
+        p, hb = _lib.tr_subproblem(H, g, R)
+        pn = np.linalg.norm(p)
+        assert pn <= R * (1 + 1e-12)
+        scale = np.abs(H).max() * max(pn, 1e-300) + np.linalg.norm(g)
+        if not hb:
+            assert np.linalg.eigvalsh(H)[0] > 0
+            assert np.linalg.norm(H @ p + g) <= 1e-8 * scale
+            continue
+        assert abs(pn - R) <= 1e-9 * R
+        lam = -(p @ (H @ p + g)) / (pn * pn)
+        assert lam >= -1e-9 * np.abs(H).max()
+        assert np.linalg.norm(H @ p + lam * p + g) <= 1e-7 * (scale + lam * pn)
+        assert np.linalg.eigvalsh(H + lam * np.eye(len(g)))[0] >= \
+            -1e-7 * (np.abs(H).max() + lam)
+        if t % 50 == 0:
+            v = rng.normal(size=(4000, len(g)))
+            v *= (R * rng.uniform(0, 1, size=(4000, 1)) ** (1 / len(g)) /
+                  np.linalg.norm(v, axis=1, keepdims=True))
+            mv = v @ g + 0.5 * np.einsum("ij,jk,ik->i", v, H, v)
+            mp = g @ p + 0.5 * p @ H @ p
+            assert mp <= mv.min() + 1e-9 * abs(mv.min())

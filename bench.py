@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--pinned", action="store_true",
                     help="--fit gettoas: archives held in page-locked host "
                     "memory (uploaded without the staging copy)")
+    ap.add_argument("--psrfits", action="store_true",
+                    help="--fit gettoas: archives written as fold-mode "
+                    "PSRFITS files (16-bit DATA + DAT_SCL/DAT_OFFS, one "
+                    "polarisation) and read through the PSRCHIVE-free fast "
+                    "path (raw bytes to the device, unpacked there)")
     ap.add_argument("--zap-frac", type=float, default=0.0,
                     help="fraction of channels masked (zapped) in every "
                     "sub-int, as GetTOAs passes its ok_ichans (default 0)")
@@ -350,6 +355,28 @@ def _host_rows(data, pinned):
     return out
 
 
+def _write_psrfits(path, b, f, per):
+    """One synthetic archive as a 16-bit fold-mode PSRFITS file (device
+    quantisation: per-profile offset = midrange, scale = half-range /
+    32767, as psrfits.quantize)."""
+    import torch
+    from pulseportraiture_amd import psrfits, synth
+    x = b["data"].double()
+    lo, hi = x.amin(dim=-1), x.amax(dim=-1)
+    offs = ((lo + hi) / 2).float()
+    scl = ((hi - lo) / 2 / 32767.0).clamp_min(1e-30).float()
+    q = torch.round((x - offs.double()[..., None]) / scl.double()[..., None])
+    q = q.clamp(-32768, 32767).to(torch.int16).cpu().numpy()
+    n, nchan, nbin = q.shape
+    psrfits.write_psrfits(
+        path, q[:, None], scl.cpu().numpy(), offs.cpu().numpy(),
+        np.tile(b["freqs"], (n, 1)), np.ones((n, nchan)), b["P"],
+        30.0 + 60.0 * np.arange(n), np.full(n, 60.0), stt_imjd=57000 + f,
+        npol=1, pol_type="AA+BB", telescope="GBT", frontend="fake_rx",
+        backend="fake_be", source="J1234-5678", dm=synth.DM0)
+    return path
+
+
 def bench_gettoas(args):
     """End-to-end GetTOAs.get_TOAs (pptoas.py:161-792) over in-memory
     archives (float32 amplitudes in host memory, as load_data hands them
@@ -373,12 +400,17 @@ def bench_gettoas(args):
     nfile = max(1, args.nsub // per)
     files = {}
     a0, na = dist.shard(nfile, rank, world) if nfile >= world else (0, nfile)
+    tmp = tempfile.mkdtemp()
     for f in range(nfile):
         name = "synthetic_%04d.fits" % f
         if not a0 <= f < a0 + na:
             files[name] = None          # another rank's archive: never loaded
             continue
         b = synth.make_batch(per, nchan, nbin, first=f * per, dev=dev)
+        if args.psrfits:
+            files[name] = _write_psrfits(os.path.join(tmp, name), b, f, per)
+            del b
+            continue
         noise = engine.noise_rows(b["data"]).cpu().numpy()
         snrs = (b["data"].amax(dim=-1).double().cpu().numpy() / noise * 3.0)
         files[name] = DataBunch(
@@ -405,13 +437,14 @@ def bench_gettoas(args):
             raise AssertionError("rank %d loaded another rank's archive %s"
                                  % (rank, fn))
         return files[fn]
-    pptoas.load_data = load
-    pptoas._MJD = _Epoch
-    tmp = tempfile.mkdtemp()
+    if not args.psrfits:
+        pptoas.load_data = load
+        pptoas._MJD = _Epoch
     gm = synth.write_gmodel(os.path.join(tmp, "example.gmodel"))
     meta = os.path.join(tmp, "meta.txt")
     with open(meta, "w") as fh:
-        fh.write("".join(n + "\n" for n in files))
+        fh.write("".join((files[n] if args.psrfits and files[n] else n) + "\n"
+                         for n in files))
 
     def step():
         gt = pptoas.GetTOAs(meta, gm, quiet=True)
@@ -437,8 +470,11 @@ def bench_gettoas(args):
                ms_per_step=round(dt / args.steps * 1e3, 3),
                higher_is_better=True, scaling="strong", vs_baseline=None,
                dtype="f64", data="synthetic (device-generated example.gmodel "
-               "archives held in %s host memory as float32)" % (
-                   "page-locked" if args.pinned else "pageable"),
+               "archives %s)" % (
+                   "written as 16-bit fold-mode PSRFITS files and read "
+                   "through the PSRFITS fast path" if args.psrfits else
+                   "held in %s host memory as float32" % (
+                       "page-locked" if args.pinned else "pageable")),
                config=dict(workload="configs[1]-shape archives: %d x %d "
                            "sub-ints x %dch x %dbin through GetTOAs.get_TOAs"
                            % (nfile, per, nchan, nbin), nfile=nfile,
@@ -447,10 +483,15 @@ def bench_gettoas(args):
                            fit="gettoas", parallelism="dp%d" % world,
                            sharding="archives" if nfile >= world and
                            world > 1 else "sub-ints" if world > 1 else None,
-                           load_data="in-memory dict lookup (no PSRCHIVE "
+                           load_data="PSRFITS fast path (psrfits.load_data:"
+                           " mmap, pinned copy of the DATA bytes, device "
+                           "unpack + baseline + noise; files in the page "
+                           "cache)" if args.psrfits else
+                           "in-memory dict lookup (no PSRCHIVE "
                            "read cost charged)"),
                toas=len(gt.TOA_list), host_gb=round(
-                   nfile * per * nchan * nbin * 4 / 1e9, 2),
+                   nfile * per * nchan * nbin * (2 if args.psrfits else 4)
+                   / 1e9, 2),
                roofline=None, cpu_baseline=None)
     if rank == 0:
         print(json.dumps(out), flush=True)

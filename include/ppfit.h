@@ -302,6 +302,31 @@ int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, c
                      const double *params, const double *P, const double *freqs, const double *nus,
                      int32_t log10_tau, double *out, void *stream);
 
+/* PSRCHIVE-free PSRFITS fast path (pulseportraiture_amd/psrfits.py; replaces
+ * the unpacking, baseline removal, pscrunch and per-profile statistics of
+ * pplib.load_data, pplib.py:2749-2915, for fold-mode PSRFITS): raw SUBINT
+ * DATA bytes as stored in the file (big-endian; elem 0 = int16, 1 = uint8,
+ * 2 = float32), one block of sub_stride bytes per sub-int holding
+ * [npol][nchan][nbin] samples (at least the pols used: 1, or 2 with
+ * pol_mode 1; scl / offs still index all npol), become float32 rows
+ *   out[s][n][b] = sum_p (DATA * DAT_SCL + DAT_OFFS)   (float32 arithmetic)
+ * over p = pol 0 (pol_mode 0: npol 1 or IQUV's I) or pols 0 + 1 (pol_mode 1:
+ * AA+BB / AABBCRCI).  The baseline window of each sub-int is the circular
+ * window of rint(0.15 nbin) bins with the smallest sum of the weighted
+ * total profile (PSRCHIVE's default BaselineWindow); with rm_baseline its
+ * mean is subtracted from every row.  scl, offs: float32 [nsub][npol*nchan];
+ * wts: float32 [nsub][nchan] or NULL; stats: [nsub][nchan][3] = off-pulse
+ * mean, off-pulse sigma, S/N (on-pulse sum / (sigma sqrt(n_on)));
+ * total: [nsub][nbin] weighted total profiles; wstart: int32 [nsub] window
+ * starts.  Any nbin >= 2.  workspace: ppf_unpack_workspace_bytes(). */
+size_t ppf_unpack_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin);
+int ppf_unpack_psrfits_batch(ppf_ctx *ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                             int32_t elem, const void *raw, int64_t sub_stride, const float *scl,
+                             const float *offs, const float *wts, int32_t pol_mode,
+                             int32_t rm_baseline, float *out, double *stats, double *total,
+                             int32_t *wstart, void *workspace, size_t workspace_bytes,
+                             void *stream);
+
 /* Gaussian-component model portraits: pplib.gen_gaussian_portrait
  * (pplib.py:886-963, join_ichans = []) as called by pplib.read_model
  * (pplib.py:2971-3057) for every sub-integration of GetTOAs.get_TOAs

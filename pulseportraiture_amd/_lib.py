@@ -112,6 +112,12 @@ SIGNATURES = {
                                        _vp, _vp, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_uint64,
                                        ctypes.c_int64, _i32, _vp, _vp]),
+    "ppf_unpack_workspace_bytes": (ctypes.c_size_t, [_i32, _i32, _i32]),
+    "ppf_unpack_psrfits_batch": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32,
+                                                _i32, _vp, ctypes.c_int64,
+                                                _vp, _vp, _vp, _i32, _i32,
+                                                _vp, _vp, _vp, _vp, _vp,
+                                                ctypes.c_size_t, _vp]),
     "ppf_poly_real_roots_host": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_tr_subproblem_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                               ctypes.c_double, _vp]),

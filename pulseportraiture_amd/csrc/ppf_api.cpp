@@ -2,6 +2,7 @@
 // carving, twiddle-table cache and kernel sequencing.  No compute here.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -658,6 +659,44 @@ int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, c
     ppf::ScalesArgs a{nsub, nchan, nharm, log10_tau != 0, (const double2 *)D, (const double2 *)M,
                       model_index, errs_FT, params, P, freqs, nus, out};
     if ((e = ppf::launch_scales(a, (hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e, "k_scales");
+    return PPF_OK;
+}
+
+size_t ppf_unpack_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin) {
+    if (nsub < 0 || nchan < 1 || nbin < 2) return 0;
+    return ppf::unpack_partials(nsub, nchan, nbin) * sizeof(double) + 256;
+}
+
+int ppf_unpack_psrfits_batch(ppf_ctx *ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                             int32_t elem, const void *raw, int64_t sub_stride, const float *scl,
+                             const float *offs, const float *wts, int32_t pol_mode,
+                             int32_t rm_baseline, float *out, double *stats, double *total,
+                             int32_t *wstart, void *workspace, size_t workspace_bytes,
+                             void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nsub < 0 || npol < 1 || nchan < 1 || nbin < 2 || elem < 0 || elem > 2 || pol_mode < 0 ||
+        pol_mode > 1 || (pol_mode == 1 && npol < 2))
+        return fail(ctx, PPF_EINVAL, "bad unpack arguments (npol=%d nchan=%d nbin=%d elem=%d "
+                    "pol_mode=%d)", npol, nchan, nbin, elem, pol_mode);
+    const int64_t esize = elem == 0 ? 2 : (elem == 1 ? 1 : 4);
+    if (sub_stride < (int64_t)(pol_mode == 1 ? 2 : 1) * nchan * nbin * esize)
+        return fail(ctx, PPF_EINVAL, "sub_stride %lld < one sub-int's DATA", (long long)sub_stride);
+    if (nsub == 0) return PPF_OK;
+    if (!raw || !scl || !offs || !out || !stats || !total || !wstart || !workspace)
+        return fail(ctx, PPF_EINVAL, "null unpack pointer");
+    if (workspace_bytes < ppf_unpack_workspace_bytes(nsub, nchan, nbin))
+        return fail(ctx, PPF_ENOMEM, "unpack workspace %zu < %zu", workspace_bytes,
+                    ppf_unpack_workspace_bytes(nsub, nchan, nbin));
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    ppf::UnpackArgs a{};
+    a.nsub = nsub; a.npol = npol; a.nchan = nchan; a.nbin = nbin; a.elem = elem;
+    a.pol_mode = pol_mode; a.rm_baseline = rm_baseline ? 1 : 0;
+    a.win = std::min(nbin - 1, std::max(1, (int)std::lrint(0.15 * nbin)));
+    a.raw = (const uint8_t *)raw; a.sub_stride = sub_stride;
+    a.scl = scl; a.offs = offs; a.wts = wts; a.out = out;
+    a.part = (double *)workspace; a.total = total; a.wstart = wstart; a.stats = stats;
+    if ((e = ppf::launch_unpack(a, (hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e, "k_unpack");
     return PPF_OK;
 }
 

@@ -208,6 +208,26 @@ struct ScalesArgs {
 };
 hipError_t launch_scales(const ScalesArgs &a, hipStream_t st);
 
+// PSRFITS fast path (ppf_psrfits.hip): raw SUBINT DATA bytes -> float32
+// total-intensity rows, baseline window, per-row statistics
+struct UnpackArgs {
+    int nsub, npol, nchan, nbin;
+    int elem;                    // 0 big-endian int16, 1 uint8, 2 big-endian float32
+    int pol_mode;                // 0: pol 0 (npol 1, IQUV); 1: AA + BB
+    int rm_baseline, win;        // subtract the off-pulse mean; window bins
+    const uint8_t *raw;          // [nsub] blocks of sub_stride bytes
+    int64_t sub_stride;
+    const float *scl, *offs;     // [nsub][npol * nchan]
+    const float *wts;            // [nsub][nchan] or null
+    float *out;                  // [nsub][nchan][nbin]
+    double *part;                // [nsub][nblk][nbin] workspace
+    double *total;               // [nsub][nbin]
+    int32_t *wstart;             // [nsub]
+    double *stats;               // [nsub][nchan][3]: off mean, off sigma, S/N
+};
+hipError_t launch_unpack(const UnpackArgs &a, hipStream_t st);
+size_t unpack_partials(int nsub, int nchan, int nbin);
+
 // pplib.gen_gaussian_portrait (pplib.py:886-963) per (portrait, channel) row
 struct GaussArgs {
     int nport, nchan, nbin, log2N, ngauss, npar;

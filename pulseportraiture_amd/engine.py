@@ -404,6 +404,38 @@ def noise_rows(rows, frac=4, dev=None):
     return out.reshape(shape[:-1])
 
 
+def unpack_psrfits(raw, elem, npol, nchan, nbin, scl, offs, wts=None,
+                   pol_mode=0, rm_baseline=True, dev=None):
+    """ppf_unpack_psrfits_batch: raw DATA bytes [nsub, >= npol nchan nbin
+    esize] (device uint8 tensor, one row per sub-int, as stored in the
+    file) -> dict(rows float32 [nsub, nchan, nbin], stats float64
+    [nsub, nchan, 3] (off-pulse mean, sigma, S/N), total float64
+    [nsub, nbin], wstart int32 [nsub]), all on the device."""
+    dev = device(dev)
+    nsub = raw.shape[0]
+    f32 = torch.float32
+    scl_t = to_dev(scl, dev, f32).reshape(nsub, npol * nchan).contiguous()
+    offs_t = to_dev(offs, dev, f32).reshape(nsub, npol * nchan).contiguous()
+    wts_t = None if wts is None else \
+        to_dev(wts, dev, f32).reshape(nsub, nchan).contiguous()
+    rows = torch.empty((nsub, nchan, nbin), dtype=f32, device=dev)
+    stats = torch.empty((nsub, nchan, 3), dtype=torch.float64, device=dev)
+    total = torch.empty((nsub, nbin), dtype=torch.float64, device=dev)
+    wstart = torch.empty(nsub, dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    wsb = int(lib.ppf_unpack_workspace_bytes(nsub, nchan, nbin))
+    ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = lib.ppf_unpack_psrfits_batch(
+        ctx, nsub, npol, nchan, nbin, int(elem), _p(raw), int(raw.stride(0)),
+        _p(scl_t), _p(offs_t), None if wts_t is None else _p(wts_t),
+        int(pol_mode), int(bool(rm_baseline)), _p(rows), _p(stats), _p(total),
+        _p(wstart), _p(ws), wsb, _stream(dev))
+    _lib.check(rc, ctx)
+    return dict(rows=rows, stats=stats, total=total, wstart=wstart,
+                _keep=(scl_t, offs_t, wts_t, ws, raw))
+
+
 def scales_batch(D, M, params, P, freqs, nus, log10_tau, errs_FT=None,
                  model_index=None, dev=None):
     """get_scales_full (pptoaslib.py:953-971) per sub-int: D [nsub, nchan,

@@ -50,6 +50,38 @@ class DataBunch(dict):
         self.__dict__ = self
 
 
+class MJD(object):
+    """A PSRCHIVE-free MJD (psrchive.MJD's interface as get_TOAs and
+    write_TOAs use it): integer day + fractional day, so a TOA keeps
+    sub-nanosecond resolution.  MJD(days) or MJD(intday, fracday)."""
+
+    def __init__(self, intday=0.0, fracday=None):
+        if fracday is None:
+            d = float(intday)
+            i = np.floor(d)
+            intday, fracday = int(i), d - i
+        i, f = int(intday), float(fracday)
+        k = int(np.floor(f))
+        self._i, self._f = i + k, f - k
+
+    def __add__(self, other):
+        if isinstance(other, MJD):
+            return MJD(self._i + other._i, self._f + other._f)
+        return MJD(self._i, self._f + float(other) / 86400.0)   # seconds
+
+    def intday(self):
+        return self._i
+
+    def fracday(self):
+        return self._f
+
+    def in_days(self):
+        return self._i + self._f
+
+    def __repr__(self):
+        return "MJD(%d, %.15f)" % (self._i, self._f)
+
+
 # ------------------------------------------------------------ host helpers --
 def get_bin_centers(nbin, lo=0.0, hi=1.0):
     """pplib.py:694-707."""
@@ -544,14 +576,19 @@ def write_TOAs(TOAs, inf_is_zero=True, SNR_cutoff=0.0, outfile=None,
 
 # ------------------------------------------------------------ archive I/O --
 def load_data(filename, **kwargs):
-    """pplib.py:2749-2915.  Archive I/O stays on PSRCHIVE (host); it is not
-    installed in this image, so this raises unless ``psrchive`` imports."""
+    """pplib.py:2749-2915.  Fold-mode PSRFITS files take the PSRCHIVE-free
+    fast path (psrfits.load_data: raw DATA bytes to the device, unpacked,
+    baseline-removed and pscrunched there); any other archive format needs
+    PSRCHIVE, which is not installed in this image."""
+    if file_is_type(filename, "FITS"):
+        from . import psrfits
+        return psrfits.load_data(filename, **kwargs)
     try:
         import psrchive  # noqa: F401
     except ImportError as exc:
-        raise ImportError("load_data needs the PSRCHIVE Python bindings "
-                          "(archive I/O is host-side and out of the "
-                          "accelerated path)") from exc
+        raise ImportError("load_data needs the PSRCHIVE Python bindings for "
+                          "non-PSRFITS archives (archive I/O is host-side "
+                          "and out of the accelerated path)") from exc
     raise NotImplementedError("PSRCHIVE-backed load_data is not provided in "
                               "this build; pass a DataBunch with the keys of "
                               "pplib.py:2904-2914")

@@ -37,7 +37,10 @@ def load_data(filename, **kwargs):
 
 
 def _MJD(days):
-    import psrchive as pr
+    try:
+        import psrchive as pr
+    except ImportError:
+        return _pplib.MJD(days)
     return pr.MJD(days)
 
 
@@ -77,6 +80,33 @@ class _Staged(object):
 
     def release(self):
         self.fut = None
+
+
+class _OnDevice(object):
+    """A staged batch that is already in HBM (the PSRFITS fast path's
+    unpacked rows): the selected sub-ints, ordered after the unpack."""
+
+    def __init__(self, rows, event, sel, nchan, nbin):
+        self.rows, self.event, self.sel = rows, event, list(sel)
+        self.nchan, self.nbin = nchan, nbin
+
+    def wait(self):
+        cur = torch.cuda.current_stream(self.rows.device)
+        if self.event is not None:
+            cur.wait_event(self.event)
+        sel = self.sel
+        if not sel:
+            return torch.zeros((0, self.nchan, self.nbin), dtype=torch.float32,
+                               device=self.rows.device)
+        if sel == list(range(sel[0], sel[0] + len(sel))):
+            t = self.rows[sel[0]:sel[0] + len(sel)]
+        else:
+            t = self.rows.index_select(0, torch.as_tensor(sel, device=self.rows.device))
+        self.rows.record_stream(cur)
+        return t
+
+    def release(self):
+        self.rows = None
 
 
 class _Stager(object):
@@ -611,7 +641,16 @@ class GetTOAs(object):
         rank, world = (0, 1) if ctx["by_archive"] else _rank_world()
         first, count = _dist.shard(nok, rank, world)
         sel = ok_isubs[first:first + count]
-        if count and sel == list(range(sel[0], sel[0] + count)):
+        dev_rows = getattr(d.subints, "device_rows", None)
+        if dev_rows is not None:
+            # PSRFITS fast path: the rows were unpacked on the device by
+            # load_data (psrfits.load_data); no host copy, no second upload
+            staged = _OnDevice(dev_rows, d.subints.event, sel, nchan, nbin)
+        else:
+            staged = None
+        if staged is not None:
+            rows = None
+        elif count and sel == list(range(sel[0], sel[0] + count)):
             # contiguous sub-ints (the usual case): a view, no gather copy
             rows = np.asarray(d.subints)[sel[0]:sel[0] + count, 0]
         elif count:
@@ -628,7 +667,8 @@ class GetTOAs(object):
                     flags_b=flags_b, nu_fit_b=nu_fit_b, nu_out_b=nu_out_b,
                     guess_tau=guess_tau, first=first, count=count,
                     bounds=ctx["bounds"][0],
-                    world=world, staged=stager.stage(rows),
+                    world=world,
+                    staged=staged if staged is not None else stager.stage(rows),
                     fit_duration=fit_duration)
 
     def _fit_archive(self, job, ctx):

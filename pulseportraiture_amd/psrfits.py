@@ -1,0 +1,566 @@
+"""PSRCHIVE-free fast path from fold-mode PSRFITS files to the device.
+
+SURVEY.md 8(f)3: the host must not starve the GPUs.  PSRCHIVE's load_data
+(pplib.py:2749-2915) unpacks every sample to float on the host, removes the
+baseline, pscrunches and computes noise and S/N per profile before anything
+reaches the device.  Here the file is memory-mapped, only its headers are
+parsed on the host, and the SUBINT table's raw DATA bytes (big-endian
+integers, 2 B per sample for the usual 16-bit archives) go straight into
+pinned staging buffers and over PCIe; the device then unpacks them
+(DATA * DAT_SCL + DAT_OFFS in float32 arithmetic, as PSRCHIVE's FITS loader
+does), sums the polarisations to total intensity, removes the baseline and
+measures noise and S/N per channel (ppf_unpack_psrfits_batch, then
+ppf_noise_batch).  The archive's rows stay in HBM for the fit.
+
+This module is the FITS side: a minimal reader of the primary header and the
+SUBINT / POLYCO binary tables (FITS 4.0 standard: 2880-byte blocks, 80-byte
+header cards, big-endian binary tables), and a writer of the same subset
+(tests, bench).  Fold-mode (OBS_MODE PSR/CAL) archives only; search-mode
+data, FITS templates and PSRCHIVE's other formats stay with PSRCHIVE.
+
+What is restated from PSRCHIVE's documented behaviour and NOT pinned to a
+PSRCHIVE run (PSRCHIVE is absent from this image and the reference holds no
+PSRFITS fixture):
+  * the epoch of sub-int i is the start time plus OFFS_SUB (STT_IMJD,
+    STT_SMJD, STT_OFFS, OFFS_SUB); PSRCHIVE's loader may further refer it to
+    the folding predictor;
+  * the folding period is the SUBINT PERIOD column when present, else the
+    POLYCO table evaluated at the epoch (TEMPO polyco formula);
+  * Doppler factors need an ephemeris: they are 1 (the TOAs are
+    topocentric, as get_TOAs(bary=False) leaves them);
+  * baseline removal: PSRCHIVE's default BaselineWindow (the minimum mean
+    over a window of 15 % of the turn on the total profile of the sub-int,
+    subtracted from every channel);
+  * S/N per channel: the baseline-subtracted profile's sum over the
+    on-pulse bins (outside the baseline window) / (sigma_off sqrt(n_on)).
+"""
+import mmap
+import os
+
+import numpy as np
+
+BLOCK = 2880
+_TFORM = {"L": (1, "u1"), "B": (1, "u1"), "I": (2, ">i2"), "J": (4, ">i4"),
+          "K": (8, ">i8"), "A": (1, "S1"), "E": (4, ">f4"), "D": (8, ">f8"),
+          "C": (8, ">c8"), "M": (16, ">c16")}
+
+
+def _parse_value(v):
+    v = v.strip()
+    if v.startswith("'"):
+        end = v.find("'", 1)
+        while end + 1 < len(v) and v[end + 1] == "'":      # '' escape
+            end = v.find("'", end + 2)
+        return v[1:end].replace("''", "'").rstrip()
+    if "/" in v:
+        v = v.split("/", 1)[0].strip()
+    if v in ("T", "F"):
+        return v == "T"
+    try:
+        return int(v)
+    except ValueError:
+        pass
+    try:
+        return float(v.replace("D", "E"))
+    except ValueError:
+        return v
+
+
+def _read_header(buf, off):
+    """(dict of cards, offset of the data) of the HDU header at off."""
+    hdr = {}
+    while True:
+        if off + BLOCK > len(buf):
+            raise ValueError("truncated FITS header")
+        block = bytes(buf[off:off + BLOCK]).decode("ascii", "replace")
+        off += BLOCK
+        for i in range(0, BLOCK, 80):
+            card = block[i:i + 80]
+            key = card[:8].strip()
+            if key == "END":
+                return hdr, off
+            if card[8:10] == "= " and key:
+                hdr[key] = _parse_value(card[10:])
+
+
+def _data_bytes(hdr):
+    naxis = int(hdr.get("NAXIS", 0))
+    if naxis == 0:
+        return 0
+    n = 1
+    for i in range(1, naxis + 1):
+        n *= int(hdr["NAXIS%d" % i])
+    n = abs(int(hdr.get("BITPIX", 8))) // 8 * int(hdr.get("GCOUNT", 1)) * \
+        (int(hdr.get("PCOUNT", 0)) + n)
+    return (n + BLOCK - 1) // BLOCK * BLOCK
+
+
+class Table(object):
+    """A binary-table HDU: header cards and column accessors (views into
+    the mapped file)."""
+
+    def __init__(self, hdr, buf, off):
+        self.header = hdr
+        self.nrows, self.rowbytes = int(hdr["NAXIS2"]), int(hdr["NAXIS1"])
+        self._buf, self._off = buf, off
+        self.columns = {}
+        pos = 0
+        for i in range(1, int(hdr["TFIELDS"]) + 1):
+            form = str(hdr["TFORM%d" % i]).strip()
+            j = 0
+            while j < len(form) and form[j].isdigit():
+                j += 1
+            rep = int(form[:j]) if j else 1
+            code = form[j]
+            size, dt = _TFORM[code]
+            name = str(hdr.get("TTYPE%d" % i, "COL%d" % i)).strip()
+            dim = hdr.get("TDIM%d" % i)
+            self.columns[name] = (pos, rep, dt, code, dim)
+            pos += rep * size
+        if pos != self.rowbytes:
+            raise ValueError("binary table row size mismatch")
+
+    def raw(self):
+        """The table as a [nrows, rowbytes] uint8 view of the mapped file."""
+        return np.frombuffer(self._buf, dtype=np.uint8,
+                             count=self.nrows * self.rowbytes,
+                             offset=self._off).reshape(self.nrows,
+                                                       self.rowbytes)
+
+    def has(self, name):
+        return name in self.columns
+
+    def column(self, name):
+        """[nrows, repeat] array of a column (a strided view, big-endian;
+        character columns as str)."""
+        pos, rep, dt, code, _ = self.columns[name]
+        raw = self.raw()
+        if code == "A":
+            return [bytes(r[pos:pos + rep]).decode("ascii", "replace").rstrip()
+                    for r in raw]
+        size = _TFORM[code][0]
+        v = raw[:, pos:pos + rep * size]
+        return np.ascontiguousarray(v).view(dt).reshape(self.nrows, rep)
+
+    def column_bytes(self, name):
+        """(strided uint8 view [nrows, nbytes], element dtype) of a column:
+        the DATA bytes as they sit in the file, for the device unpack."""
+        pos, rep, dt, code, _ = self.columns[name]
+        size = _TFORM[code][0]
+        return self.raw()[:, pos:pos + rep * size], np.dtype(dt)
+
+
+class PSRFITS(object):
+    """A memory-mapped fold-mode PSRFITS file: .primary (header dict),
+    .subint and .polyco (Table or None)."""
+
+    def __init__(self, filename):
+        self.filename = filename
+        self._fh = open(filename, "rb")
+        size = os.fstat(self._fh.fileno()).st_size
+        self._buf = mmap.mmap(self._fh.fileno(), size, access=mmap.ACCESS_READ)
+        off = 0
+        self.primary, off = _read_header(self._buf, off)
+        if not self.primary.get("SIMPLE", False):
+            raise ValueError("%s is not a FITS file" % filename)
+        off += _data_bytes(self.primary)
+        self.subint = self.polyco = None
+        while off < size:
+            hdr, doff = _read_header(self._buf, off)
+            name = str(hdr.get("EXTNAME", "")).strip()
+            if hdr.get("XTENSION", "").strip() == "BINTABLE":
+                if name == "SUBINT":
+                    self.subint = Table(hdr, self._buf, doff)
+                elif name == "POLYCO":
+                    self.polyco = Table(hdr, self._buf, doff)
+            off = doff + _data_bytes(hdr)
+        if self.subint is None:
+            raise ValueError("%s has no SUBINT table" % filename)
+        mode = str(self.primary.get("OBS_MODE", "PSR")).strip()
+        if mode not in ("PSR", "CAL", "LEVPSR", "LEVCAL"):
+            raise NotImplementedError("OBS_MODE %s: only fold-mode PSRFITS "
+                                      "has the fast path" % mode)
+        h = self.subint.header
+        self.nbin, self.nchan = int(h["NBIN"]), int(h["NCHAN"])
+        self.npol = int(h["NPOL"])
+        self.nsub = self.subint.nrows
+        self.pol_type = str(h.get("POL_TYPE", "AA+BB" if self.npol == 1
+                                  else "AABBCRCI")).strip()
+
+    def close(self):
+        try:
+            self._buf.close()
+        except (BufferError, ValueError):
+            pass                  # views still alive: the map closes with them
+        self._fh.close()
+
+    # -- per sub-int metadata ------------------------------------------------
+    def epochs(self):
+        """MJD (integer day, fractional day) of every sub-int: STT_IMJD +
+        (STT_SMJD + STT_OFFS + OFFS_SUB) / 86400."""
+        p = self.primary
+        imjd = int(p.get("STT_IMJD", 0))
+        sec = float(p.get("STT_SMJD", 0)) + float(p.get("STT_OFFS", 0.0))
+        offs = self.subint.column("OFFS_SUB")[:, 0].astype(float) \
+            if self.subint.has("OFFS_SUB") else np.zeros(self.nsub)
+        tot = sec + offs
+        days = np.floor(tot / 86400.0)
+        return imjd + days.astype(np.int64), (tot - days * 86400.0) / 86400.0
+
+    def periods(self):
+        """Folding period [s] per sub-int: the PERIOD column, else the
+        POLYCO table at the sub-int epoch."""
+        if self.subint.has("PERIOD"):
+            return self.subint.column("PERIOD")[:, 0].astype(float)
+        if self.polyco is None or self.polyco.nrows == 0:
+            raise ValueError("no PERIOD column and no POLYCO table")
+        imjd, frac = self.epochs()
+        return np.array([1.0 / polyco_freq(self.polyco, i, f)
+                         for i, f in zip(imjd, frac)])
+
+    def freqs(self):
+        if self.subint.has("DAT_FREQ"):
+            return self.subint.column("DAT_FREQ").astype(float)
+        p, h = self.primary, self.subint.header
+        bw = float(h.get("CHAN_BW", float(p["OBSBW"]) / self.nchan))
+        f0 = float(p["OBSFREQ"]) - (self.nchan - 1) / 2.0 * bw
+        return np.tile(f0 + bw * np.arange(self.nchan), (self.nsub, 1))
+
+    def weights(self):
+        if self.subint.has("DAT_WTS"):
+            return self.subint.column("DAT_WTS").astype(float)
+        return np.ones((self.nsub, self.nchan))
+
+    def scales_offsets(self):
+        """DAT_SCL, DAT_OFFS as float32 [nsub, npol * nchan] (pol-major)."""
+        n = self.npol * self.nchan
+        scl = self.subint.column("DAT_SCL").astype(np.float32) \
+            if self.subint.has("DAT_SCL") else np.ones((self.nsub, n), np.float32)
+        offs = self.subint.column("DAT_OFFS").astype(np.float32) \
+            if self.subint.has("DAT_OFFS") else np.zeros((self.nsub, n), np.float32)
+        if scl.shape[1] == self.nchan and self.npol > 1:       # per channel only
+            scl = np.tile(scl, (1, self.npol))
+            offs = np.tile(offs, (1, self.npol))
+        return np.ascontiguousarray(scl), np.ascontiguousarray(offs)
+
+    def data_bytes(self):
+        """(uint8 view [nsub, npol * nchan * nbin * size], element dtype) of
+        the DATA column as stored."""
+        return self.subint.column_bytes("DATA")
+
+
+def polyco_freq(tab, imjd, frac):
+    """Spin frequency [Hz] of the TEMPO polyco set nearest the epoch:
+    f = REF_F0 + (1/60) sum_i i c_i dt^(i-1), dt in minutes from REF_MJD."""
+    ref = tab.column("REF_MJD")[:, 0].astype(float)
+    t = imjd + frac
+    i = int(np.argmin(np.abs(ref - t)))
+    f0 = float(tab.column("REF_F0")[i, 0])
+    ncoef = int(tab.column("NCOEF")[i, 0]) if tab.has("NCOEF") else None
+    c = tab.column("COEFF")[i].astype(float)
+    if ncoef:
+        c = c[:ncoef]
+    dt = ((imjd - np.floor(ref[i])) + (frac - (ref[i] - np.floor(ref[i])))) \
+        * 1440.0
+    df = sum(k * c[k] * dt ** (k - 1) for k in range(1, len(c)))
+    return f0 + df / 60.0
+
+
+def unpack_host(raw, dtype, scl, offs, npol, nchan, nbin):
+    """NumPy restatement of the device unpack (tests): float32 value =
+    DATA * DAT_SCL + DAT_OFFS (two float32 roundings, no fused
+    multiply-add, as PSRCHIVE's loader computes it), then total intensity:
+    npol 1 -> itself, AABBCRCI / AA+BB -> AA + BB, IQUV -> I.
+    raw: [nsub, npol * nchan * nbin] file bytes; returns [nsub, nchan, nbin]."""
+    nsub = raw.shape[0]
+    x = np.ascontiguousarray(raw).view(dtype).reshape(nsub, npol, nchan, nbin)
+    x = x.astype(np.float32)
+    s = scl.reshape(nsub, npol, nchan, 1).astype(np.float32)
+    o = offs.reshape(nsub, npol, nchan, 1).astype(np.float32)
+    v = (x * s).astype(np.float32) + o
+    return v[:, 0] if npol == 1 else v[:, 0] + v[:, 1]
+
+
+# ------------------------------------------------------------------ writer --
+def _card(key, value, comment=""):
+    if isinstance(value, bool):
+        v = "%20s" % ("T" if value else "F")
+    elif isinstance(value, (int, np.integer)):
+        v = "%20d" % value
+    elif isinstance(value, (float, np.floating)):
+        v = "%20s" % repr(float(value)).upper()
+    else:
+        v = "'%-8s'" % str(value).replace("'", "''")
+    c = "%-8s= %s" % (key, v)
+    if comment:
+        c += " / " + comment
+    return c[:80].ljust(80)
+
+
+def _header(cards):
+    s = "".join(_card(*c) for c in cards) + "END".ljust(80)
+    s += " " * (-len(s) % BLOCK)
+    return s.encode("ascii")
+
+
+def write_psrfits(filename, data, scl, offs, freqs, weights, periods,
+                  offs_sub, tsubint, stt_imjd=56000, stt_smjd=0, stt_offs=0.0,
+                  npol=1, pol_type="AA+BB", telescope="GBT", frontend="Rcvr1_2",
+                  backend="GUPPI", source="J1234+5678", dm=0.0, be_delay=0.0,
+                  par_ang=None):
+    """Write a minimal fold-mode PSRFITS file (primary header + SUBINT
+    binary table).  data: int16 [nsub, npol, nchan, nbin]; scl, offs:
+    float32 [nsub, npol * nchan]; freqs, weights: [nsub, nchan]; periods,
+    offs_sub, tsubint: [nsub]."""
+    data = np.asarray(data, dtype=np.int16)
+    nsub, npol_, nchan, nbin = data.shape
+    assert npol_ == npol
+    cols = [("TSUBINT", "1D", None), ("OFFS_SUB", "1D", None),
+            ("PERIOD", "1D", None), ("PAR_ANG", "1E", None),
+            ("DAT_FREQ", "%dD" % nchan, None), ("DAT_WTS", "%dE" % nchan, None),
+            ("DAT_OFFS", "%dE" % (nchan * npol), None),
+            ("DAT_SCL", "%dE" % (nchan * npol), None),
+            ("DATA", "%dI" % (nbin * nchan * npol), "(%d,%d,%d)" % (nbin, nchan, npol))]
+    rowdt = np.dtype([("TSUBINT", ">f8"), ("OFFS_SUB", ">f8"), ("PERIOD", ">f8"),
+                      ("PAR_ANG", ">f4"), ("DAT_FREQ", ">f8", (nchan,)),
+                      ("DAT_WTS", ">f4", (nchan,)), ("DAT_OFFS", ">f4", (nchan * npol,)),
+                      ("DAT_SCL", ">f4", (nchan * npol,)),
+                      ("DATA", ">i2", (nbin * nchan * npol,))])
+    rows = np.zeros(nsub, dtype=rowdt)
+    rows["TSUBINT"] = tsubint
+    rows["OFFS_SUB"] = offs_sub
+    rows["PERIOD"] = periods
+    rows["PAR_ANG"] = 0.0 if par_ang is None else par_ang
+    rows["DAT_FREQ"] = freqs
+    rows["DAT_WTS"] = weights
+    rows["DAT_OFFS"] = offs
+    rows["DAT_SCL"] = scl
+    rows["DATA"] = data.reshape(nsub, -1)
+    obsbw = float(freqs[0, -1] - freqs[0, 0]) * nchan / max(nchan - 1, 1)
+    prim = [("SIMPLE", True), ("BITPIX", 8), ("NAXIS", 0), ("EXTEND", True),
+            ("HDRVER", "6.1"), ("FITSTYPE", "PSRFITS"), ("OBS_MODE", "PSR"),
+            ("TELESCOP", telescope), ("FRONTEND", frontend),
+            ("BACKEND", backend), ("SRC_NAME", source),
+            ("OBSFREQ", float(np.mean(freqs[0]))), ("OBSBW", obsbw),
+            ("OBSNCHAN", nchan), ("STT_IMJD", int(stt_imjd)),
+            ("STT_SMJD", int(stt_smjd)), ("STT_OFFS", float(stt_offs)),
+            ("BE_DELAY", float(be_delay)), ("CHAN_DM", float(dm))]
+    ext = [("XTENSION", "BINTABLE"), ("BITPIX", 8), ("NAXIS", 2),
+           ("NAXIS1", rowdt.itemsize), ("NAXIS2", nsub), ("PCOUNT", 0),
+           ("GCOUNT", 1), ("TFIELDS", len(cols))]
+    for i, (name, form, dim) in enumerate(cols, 1):
+        ext += [("TTYPE%d" % i, name), ("TFORM%d" % i, form)]
+        if dim:
+            ext.append(("TDIM%d" % i, dim))
+    ext += [("EXTNAME", "SUBINT"), ("INT_TYPE", "TIME"), ("INT_UNIT", "SEC"),
+            ("NPOL", npol), ("POL_TYPE", pol_type), ("NBIN", nbin),
+            ("NCHAN", nchan), ("CHAN_BW", float(obsbw / nchan)),
+            ("DM", float(dm)), ("NSBLK", 1)]
+    body = rows.tobytes()
+    with open(filename, "wb") as fh:
+        fh.write(_header(prim))
+        fh.write(_header(ext))
+        fh.write(body)
+        fh.write(b"\0" * (-len(body) % BLOCK))
+    return filename
+
+
+def quantize(rows, npol=1):
+    """int16 DATA + per-profile float32 DAT_SCL / DAT_OFFS of float rows
+    [nsub, npol, nchan, nbin], as a backend digitises them: offset = the
+    profile's midrange, scale = half-range / 32767."""
+    rows = np.asarray(rows, dtype=np.float64)
+    nsub, npol_, nchan, nbin = rows.shape
+    lo, hi = rows.min(axis=-1), rows.max(axis=-1)
+    offs = ((lo + hi) / 2).astype(np.float32)
+    scl = np.maximum((hi - lo) / 2 / 32767.0, 1e-30).astype(np.float32)
+    q = np.clip(np.rint((rows - offs[..., None]) / scl[..., None]), -32768,
+                32767).astype(np.int16)
+    return q, scl.reshape(nsub, npol_ * nchan), offs.reshape(nsub, npol_ * nchan)
+
+
+# ------------------------------------------------------------- load_data --
+def _telescope_code(telescope):
+    """pplib.py:2773-2777: the TEMPO2 short code of the telescope
+    ($TEMPO2/observatory/observatories.dat when present), else its name."""
+    path = os.path.join(os.environ.get("TEMPO2", ""), "observatory",
+                        "observatories.dat")
+    if os.environ.get("TEMPO2") and os.path.isfile(path):
+        with open(path) as fh:
+            for ln in fh:
+                w = ln.split()
+                if w and not ln.startswith("#") and w[-2].upper() == \
+                        telescope.upper():
+                    return w[-1]
+    return telescope
+
+
+def _window_snr(prof, frac=0.15):
+    """S/N of a profile with the baseline window of the device
+    (k_base_window / k_row_stats restated): (on-pulse sum) / (sigma_off
+    sqrt(n_on)), the window the circular rint(frac nbin)-bin window of
+    smallest sum."""
+    prof = np.asarray(prof, dtype=float)
+    nbin = prof.size
+    W = min(nbin - 1, max(1, int(np.rint(frac * nbin))))
+    ext = np.concatenate([prof, prof[:W]])
+    cs = np.concatenate([[0.0], np.cumsum(ext)])
+    b0 = int(np.argmin(cs[W:W + nbin] - cs[:nbin]))
+    win = prof[(b0 + np.arange(W)) % nbin]
+    mean, sig = win.mean(), win.std()
+    on = np.ones(nbin, bool)
+    on[(b0 + np.arange(W)) % nbin] = False
+    if sig == 0.0 or not on.any():
+        return 0.0, sig
+    return float((prof[on] - mean).sum() / (sig * np.sqrt(on.sum()))), sig
+
+
+class DeviceRows(object):
+    """load_data's `subints` on the fast path: the float32 rows live in HBM
+    ([nsub, nchan, nbin], `.device_rows`); host code that indexes it or
+    takes np.asarray gets [nsub, 1, nchan, nbin] (copied back once)."""
+
+    def __init__(self, rows, event):
+        self.device_rows, self.event = rows, event
+        self._host = None
+        n, c, b = rows.shape
+        self.shape = (n, 1, c, b)
+        self.dtype = np.float32
+        self.ndim = 4
+
+    def _get(self):
+        if self._host is None:
+            if self.event is not None:
+                self.event.synchronize()
+            self._host = self.device_rows.cpu().numpy()[:, None]
+        return self._host
+
+    def __array__(self, dtype=None, copy=None):
+        h = self._get()
+        return h if dtype is None else h.astype(dtype)
+
+    def __getitem__(self, idx):
+        return self._get()[idx]
+
+    def __len__(self):
+        return self.shape[0]
+
+
+_LOAD_STREAMS = {}
+_PINNED = {}
+
+
+def load_data(filename, state=None, dedisperse=False, dededisperse=False,
+              tscrunch=False, pscrunch=False, fscrunch=False, rm_baseline=True,
+              flux_prof=False, refresh_arch=True, return_arch=True, quiet=False,
+              dev=None):
+    """pplib.load_data (pplib.py:2749-2915) for fold-mode PSRFITS without
+    PSRCHIVE.  The DATA bytes are copied from the memory-mapped file into a
+    pinned buffer and uploaded; the device unpacks them, sums the
+    polarisations (total intensity: the only state get_TOAs asks for,
+    pscrunch=True), removes the baseline and measures every profile
+    (ppf_unpack_psrfits_batch), and get_noise_PS gives noise_stds (the
+    reference's use_get_noise = True, pplib.py:74, 2841-2848).  The rows stay
+    on the device (`subints.device_rows`); get_TOAs fits them without a
+    second upload.  Options that need PSRCHIVE's predictor or state machine
+    (dedisperse, tscrunch, fscrunch, other polarisation states) raise
+    NotImplementedError."""
+    import torch
+    from . import engine, pplib
+    if dedisperse or tscrunch or fscrunch:
+        raise NotImplementedError("load_data(dedisperse / tscrunch / fscrunch)"
+                                  " needs PSRCHIVE; the PSRFITS fast path "
+                                  "reads archives as stored")
+    if state not in (None, "Intensity"):
+        raise NotImplementedError("state=%r needs PSRCHIVE" % state)
+    f = PSRFITS(filename)
+    nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
+    if npol > 1 and not (pscrunch or state == "Intensity"):
+        raise NotImplementedError("the PSRFITS fast path returns total "
+                                  "intensity (pscrunch=True) only")
+    pt = f.pol_type.upper()
+    if npol == 1 or pt.startswith("IQUV") or pt == "INTEN":
+        pol_mode = 0
+    elif pt.startswith("AABB") or pt.startswith("AA+BB"):
+        pol_mode = 1
+    else:
+        raise NotImplementedError("POL_TYPE %s" % f.pol_type)
+    raw, edt = f.data_bytes()
+    elem = {np.dtype(">i2"): 0, np.dtype("u1"): 1, np.dtype(">f4"): 2}.get(edt)
+    if elem is None:
+        raise NotImplementedError("DATA element type %s" % edt)
+    # only the polarisations total intensity needs cross PCIe: DATA is
+    # [npol][nchan][nbin] per sub-int, so AA and BB are its first two
+    # npol blocks (2 B / sample / pol for 16-bit data)
+    nbytes = (2 if pol_mode == 1 else 1) * nchan * nbin * edt.itemsize
+    scl, offs = f.scales_offsets()
+    weights = f.weights()
+    dev = engine.device(dev)
+    with torch.cuda.device(dev):
+        st = _LOAD_STREAMS.get(dev.index)
+        if st is None:
+            st = _LOAD_STREAMS[dev.index] = torch.cuda.Stream(dev)
+        # one reusable page-locked buffer per device: load_data returns
+        # only after the upload it fed has completed
+        buf = _PINNED.get(dev.index)
+        if buf is None or buf.numel() < nsub * nbytes:
+            buf = _PINNED[dev.index] = torch.empty(
+                max(nsub * nbytes, 1), dtype=torch.uint8, pin_memory=True)
+        host = buf[:nsub * nbytes].view(nsub, nbytes)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)   # read-only mmap
+            host.copy_(torch.from_numpy(raw[:, :nbytes]))
+        with torch.cuda.stream(st):
+            raw_d = host.to(dev, non_blocking=True)
+            out = engine.unpack_psrfits(raw_d, elem, npol, nchan, nbin, scl,
+                                        offs, wts=weights.astype(np.float32),
+                                        pol_mode=pol_mode,
+                                        rm_baseline=rm_baseline, dev=dev)
+            noise = engine.noise_rows(out["rows"], dev=dev)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        ev.synchronize()
+        stats = out["stats"].cpu().numpy()
+        total = out["total"].cpu().numpy()
+        noise = noise.cpu().numpy()
+    del host, raw_d
+    p, h = f.primary, f.subint.header
+    imjd, frac = f.epochs()
+    epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(imjd, frac)]
+    Ps = f.periods()
+    freqs = f.freqs()
+    weights_norm = np.where(weights == 0.0, 0.0, 1.0)
+    ok_isubs = np.compress(weights_norm.mean(axis=1), list(range(nsub)))
+    ok_ichans = [np.compress(weights_norm[isub], list(range(nchan)))
+                 for isub in range(nsub)]
+    masks = np.einsum("ij,k", weights_norm, np.ones(nbin))[:, None]
+    prof = total.sum(axis=0)
+    prof_SNR, prof_noise = _window_snr(prof)
+    telescope = str(p.get("TELESCOP", "")).strip()
+    tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
+        if f.subint.has("TSUBINT") else np.zeros(nsub)
+    par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
+        if f.subint.has("PAR_ANG") else np.zeros(nsub)
+    DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
+    if not quiet:
+        print("\nReading data from %s on source %s (PSRFITS fast path)..." %
+              (filename, p.get("SRC_NAME", "")))
+    data = pplib.DataBunch(
+        arch=None, backend=str(p.get("BACKEND", "")).strip(),
+        backend_delay=float(p.get("BE_DELAY", 0.0)),
+        bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub), DM=DM,
+        dmc=0, epochs=epochs, filename=filename, flux_prof=np.array([]),
+        freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
+        integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
+        nchan=nchan, noise_stds=noise[:, None, :], npol=1, nsub=nsub,
+        nu0=float(p.get("OBSFREQ", freqs.mean())), ok_ichans=ok_ichans,
+        ok_isubs=ok_isubs, parallactic_angles=par,
+        phases=pplib.get_bin_centers(nbin), prof=prof / max(1.0, weights_norm.sum()),
+        prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=Ps,
+        SNRs=stats[:, None, :, 2].copy(), source=str(p.get("SRC_NAME", "")).strip(),
+        state="Intensity", subints=DeviceRows(out["rows"], ev),
+        subtimes=list(tsub), telescope=telescope,
+        telescope_code=_telescope_code(telescope), weights=weights)
+    f.close()
+    return data

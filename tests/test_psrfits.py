@@ -1,0 +1,187 @@
+"""PSRFITS fast path (pulseportraiture_amd/psrfits.py): the FITS reader and
+writer on the CPU, and on the GPU the device unpack against its NumPy
+restatement and GetTOAs on a PSRFITS file against GetTOAs on the same rows
+handed over as a host DataBunch.
+
+Parity note: no PSRFITS fixture and no PSRCHIVE exist here, so what PSRCHIVE
+itself would return for a file (epochs referred to the predictor, Doppler
+factors, its own S/N) is unpinned; these tests pin the fast path to its
+documented restatement and to the DataBunch path that the reference goldens
+pin."""
+import os
+
+import numpy as np
+import pytest
+
+from pulseportraiture_amd import psrfits as PF
+
+
+def _archive(tmp, nsub=4, npol=2, nchan=32, nbin=256, seed=1, elem="I"):
+    rng = np.random.default_rng(seed)
+    b = np.arange(nbin)
+    prof = np.exp(-0.5 * ((b - 0.3 * nbin) / (0.02 * nbin)) ** 2)
+    rows = 20.0 * prof[None, None, None] * rng.uniform(0.5, 1.5, (nsub, 1, nchan, 1)) \
+        + rng.normal(0, 1.0, (nsub, npol, nchan, nbin)) + 7.0
+    q, scl, offs = PF.quantize(rows)
+    fr = np.tile(np.linspace(1100.0, 1900.0, nchan), (nsub, 1))
+    wts = np.ones((nsub, nchan))
+    wts[1, 3] = 0.0
+    fn = os.path.join(str(tmp), "a.fits")
+    PF.write_psrfits(fn, q, scl, offs, fr, wts, np.full(nsub, 0.00289),
+                     5.0 + 10.0 * np.arange(nsub), np.full(nsub, 10.0),
+                     stt_imjd=57000, stt_smjd=3600, stt_offs=0.25, npol=npol,
+                     pol_type="AABBCRCI" if npol == 4 or npol == 2 else "AA+BB",
+                     dm=12.5, be_delay=1e-6)
+    return fn, q, scl, offs, fr, wts
+
+
+def test_fits_round_trip(tmp_path):
+    fn, q, scl, offs, fr, wts = _archive(tmp_path)
+    f = PF.PSRFITS(fn)
+    assert (f.nsub, f.npol, f.nchan, f.nbin) == q.shape
+    raw, dt = f.data_bytes()
+    got = np.ascontiguousarray(raw).view(dt).reshape(q.shape)
+    np.testing.assert_array_equal(got, q)
+    s, o = f.scales_offsets()
+    np.testing.assert_array_equal(s, scl)
+    np.testing.assert_array_equal(o, offs)
+    np.testing.assert_array_equal(f.freqs(), fr)
+    np.testing.assert_array_equal(f.weights(), wts)
+    np.testing.assert_array_equal(f.periods(), 0.00289)
+    imjd, frac = f.epochs()
+    np.testing.assert_array_equal(imjd, 57000)
+    np.testing.assert_allclose(frac, (3600.25 + 5.0 + 10.0 * np.arange(4)) / 86400.0,
+                               rtol=0, atol=1e-15)
+    assert f.primary["TELESCOP"] == "GBT" and f.subint.header["DM"] == 12.5
+    f.close()
+
+
+def test_unpack_host_restatement(tmp_path):
+    fn, q, scl, offs, fr, wts = _archive(tmp_path)
+    f = PF.PSRFITS(fn)
+    raw, dt = f.data_bytes()
+    u = PF.unpack_host(raw, dt, *f.scales_offsets(), f.npol, f.nchan, f.nbin)
+    s4 = scl.reshape(4, 2, 32, 1)
+    o4 = offs.reshape(4, 2, 32, 1)
+    want = (q.astype(np.float32) * s4).astype(np.float32) + o4
+    np.testing.assert_array_equal(u, want[:, 0] + want[:, 1])
+    f.close()
+
+
+def test_mjd_arithmetic():
+    from pulseportraiture_amd.pplib import MJD
+    m = MJD(57000, 0.999999) + MJD(0.5 / 86400.0 * 86400.0 / 86400.0)
+    assert m.intday() == 57001 and abs(m.fracday() - (0.999999 + 0.5 / 86400 - 1)) < 1e-15
+    t = MJD(57000, 0.25) + 3600.0                       # seconds
+    assert t.intday() == 57000 and abs(t.fracday() - (0.25 + 1 / 24.0)) < 1e-15
+
+
+def test_load_data_rejects_psrchive_only_options(tmp_path):
+    fn = _archive(tmp_path)[0]
+    for kw in (dict(tscrunch=True), dict(dedisperse=True), dict(fscrunch=True)):
+        with pytest.raises(NotImplementedError):
+            PF.load_data(fn, pscrunch=True, **kw)
+    with pytest.raises(NotImplementedError):
+        PF.load_data(fn, pscrunch=False)              # npol 2, not scrunched
+
+
+def _host_baseline(u, wts, frac=0.15):
+    """NumPy restatement of k_base_window + k_row_stats."""
+    nsub, nchan, nbin = u.shape
+    W = min(nbin - 1, max(1, int(np.rint(frac * nbin))))
+    out, stats, w0s, mins = np.empty_like(u), np.empty((nsub, nchan, 3)), [], []
+    for s in range(nsub):
+        tot = (wts[s][:, None] * u[s].astype(float)).sum(axis=0)
+        ext = np.concatenate([tot, tot[:W]])
+        cs = np.concatenate([[0.0], np.cumsum(ext)])
+        sums = cs[W:W + nbin] - cs[:nbin]
+        w0s.append(int(np.argmin(sums)))
+        mins.append((sums, tot))
+    return W, w0s, mins
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npol,elem", [(2, "I"), (1, "I")])
+def test_device_unpack_matches_restatement(tmp_path, npol, elem):
+    import torch
+    from pulseportraiture_amd import engine
+    fn, q, scl, offs, fr, wts = _archive(tmp_path, npol=npol)
+    f = PF.PSRFITS(fn)
+    raw, dt = f.data_bytes()
+    s, o = f.scales_offsets()
+    raw_d = torch.from_numpy(np.ascontiguousarray(raw)).cuda()
+    res = engine.unpack_psrfits(raw_d, 0, npol, f.nchan, f.nbin, s, o,
+                                wts=wts.astype(np.float32),
+                                pol_mode=1 if npol == 2 else 0, rm_baseline=True)
+    rows = res["rows"].cpu().numpy()
+    st = res["stats"].cpu().numpy()
+    w0 = res["wstart"].cpu().numpy()
+    u = PF.unpack_host(raw, dt, s, o, npol, f.nchan, f.nbin)
+    W, w0h, mins = _host_baseline(u, wts)
+    for k in range(f.nsub):
+        sums, tot = mins[k]
+        np.testing.assert_allclose(res["total"].cpu().numpy()[k], tot, rtol=1e-12,
+                                   atol=1e-9)
+        # the device window is a minimum of the window sums (ties aside)
+        assert sums[w0[k]] <= sums.min() + 1e-9 * abs(sums).max()
+        idx = (w0[k] + np.arange(W)) % f.nbin
+        mean = u[k][:, idx].astype(float).mean(axis=1)
+        want = (u[k].astype(float) - mean[:, None]).astype(np.float32)
+        np.testing.assert_allclose(rows[k], want, rtol=0,
+                                   atol=2 * np.spacing(np.abs(want).max()))
+        np.testing.assert_allclose(st[k, :, 0], mean, rtol=1e-12)
+        sig = u[k][:, idx].astype(float).std(axis=1)
+        np.testing.assert_allclose(st[k, :, 1], sig, rtol=1e-10)
+        on = np.ones(f.nbin, bool)
+        on[idx] = False
+        snr = (u[k][:, on].astype(float) - mean[:, None]).sum(axis=1) / \
+            (sig * np.sqrt(on.sum()))
+        np.testing.assert_allclose(st[k, :, 2], snr, rtol=1e-9)
+    f.close()
+
+
+@pytest.mark.gpu
+def test_gettoas_psrfits_equals_databunch_path(tmp_path, monkeypatch):
+    """get_TOAs on a PSRFITS file (rows unpacked on the device, fitted
+    without leaving HBM) == get_TOAs on the same rows and metadata as a
+    host DataBunch (staged through pinned memory), bitwise."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import synth_np as SN
+    from pulseportraiture_amd import pptoas, pplib
+    nsub, nchan, nbin = 6, 64, 512
+    model, freqs = SN.template(nchan, nbin)
+    rng = np.random.default_rng(5)
+    P = 0.0028929
+    phis = rng.uniform(-0.2, 0.2, nsub)
+    port = np.stack([SN.rotate(model, -(phis[i] + 4148.808 * 10.0 *
+                                        (freqs ** -2 - 1500.0 ** -2) / P))
+                     for i in range(nsub)])
+    rows = 40.0 * port[:, None] + rng.normal(0, 1.0, (nsub, 2, nchan, nbin))
+    q, scl, offs = PF.quantize(rows)
+    fn = str(tmp_path / "p.fits")
+    PF.write_psrfits(fn, q, scl, offs, np.tile(freqs, (nsub, 1)),
+                     np.ones((nsub, nchan)), np.full(nsub, P),
+                     5.0 + 10.0 * np.arange(nsub), np.full(nsub, 10.0),
+                     npol=2, pol_type="AABBCRCI", dm=10.0)
+    gm = str(tmp_path / "t.gmodel")
+    SN.write_gmodel(gm, *SN.read_gmodel())
+    meta = tmp_path / "meta.txt"
+    meta.write_text(fn + "\n")
+    fast = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    fast.get_TOAs(quiet=True, bary=False)
+    d = pplib.load_data(fn, pscrunch=True, quiet=True)
+    host = pplib.DataBunch(**{k: v for k, v in d.items()})
+    host["subints"] = np.asarray(d.subints).copy()
+    monkeypatch.setattr(pptoas, "load_data", lambda f_, **kw: host)
+    slow = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    slow.get_TOAs(quiet=True, bary=False)
+    for key in ("phis", "phi_errs", "DMs", "DM_errs", "red_chi2s", "snrs"):
+        np.testing.assert_array_equal(np.asarray(getattr(fast, key)[0]),
+                                      np.asarray(getattr(slow, key)[0]), err_msg=key)
+    a = [str(t.MJD.intday()) + repr(t.MJD.fracday()) for t in fast.TOA_list]
+    b = [str(t.MJD.intday()) + repr(t.MJD.fracday()) for t in slow.TOA_list]
+    assert a == b
+    # the fits converged on data of unit reduced chi^2
+    rc = np.asarray(fast.red_chi2s[0])
+    assert np.all((rc > 0.8) & (rc < 1.25)), rc

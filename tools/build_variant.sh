@@ -12,8 +12,9 @@ C=$root/pulseportraiture_amd/csrc
 $H -c $C/ppf_kernels.hip -o $od/k.o &
 $H -c $C/ppf_xspec.hip -o $od/x.o &
 $H -c $C/ppf_solve.hip -o $od/s.o &
+$H -c $C/ppf_psrfits.hip -o $od/p.o &
 $H -x hip -c $C/ppf_api.cpp -o $od/a.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/varlib/libppfit_$name.so $od/k.o $od/x.o $od/s.o $od/a.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $root/varlib/libppfit_$name.so $od/k.o $od/x.o $od/s.o $od/p.o $od/a.o
 rm -rf $od
 echo built varlib/libppfit_$name.so

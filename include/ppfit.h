@@ -75,16 +75,20 @@ enum ppf_option {
                                 cross-spectrum pass is not launched (a
                                 sub-int that would need X ends with
                                 PPF_ST_NOSPACE) */
-    PPF_OPT_SCIPY_TR = 4     /* scattering fits follow scipy's trust-ncg
-                                path step by step (pptoaslib.py:1055-1060:
-                                radius 1 in raw parameter units, CG-Steihaug
-                                subproblem).  Default: the Newton trust
-                                region (scaled coordinates, exact
-                                subproblem), which stops at the same
-                                stationary point in 3-4x fewer passes over
-                                the cross spectrum.  Fits
-                                without scattering and bounded (TNC) fits
-                                always take the scipy path. */
+    PPF_OPT_SCIPY_TR = 4     /* the fits follow scipy's trust-ncg path
+                                step by step (pptoaslib.py:1055-1060:
+                                radius 1 in raw parameter units,
+                                CG-Steihaug subproblem).  Default: the
+                                Newton trust region (Jacobi-scaled
+                                coordinates, exact subproblem), which stops
+                                at the same stationary point, closer (the
+                                reference's Newton decrement at its end
+                                point reaches 6e-6, this one's 1e-20), in
+                                fewer evaluations: scattering fits 3x fewer
+                                passes over the cross spectrum, ppalign
+                                fits half the data passes.
+                                Bounded (method='TNC') fits always take the
+                                scipy path with projected steps. */
 };
 
 enum ppf_mode {

@@ -26,9 +26,10 @@
 namespace ppf {
 
 // Newton trust region also for the moment-expansion fits (phase / DM / GM
-// without scattering); 0: those always follow scipy's trust-ncg path
+// without scattering; C4: 1.04 instead of 2.34 data passes per fit);
+// 0 builds them with scipy's trust-ncg path only
 #ifndef PPF_NEWTON_MOM
-#define PPF_NEWTON_MOM 0
+#define PPF_NEWTON_MOM 1
 #endif
 
 // ===========================================================================

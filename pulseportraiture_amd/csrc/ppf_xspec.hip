@@ -60,14 +60,6 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 #ifndef PPF_XM_CUT
 #define PPF_XM_CUT 0
 #endif
-// k_xspec_w: every wave stores its own row of X from registers (no
-// workgroup barrier per round) instead of staging 8 rows in LDS
-#ifndef PPF_XSPEC_DIRECT
-#define PPF_XSPEC_DIRECT 0
-#endif
-#ifndef PPF_XSPEC_MINW
-#define PPF_XSPEC_MINW 4
-#endif
 #if PPF_XM_CUT
 #define XM_CUT() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -109,7 +101,7 @@ template <int LOG2N>
 __host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + 2; }
 
 template <int LOG2N, int DT>
-__global__ __launch_bounds__(64 * kXW, (PPF_XSPEC_DIRECT && LOG2N <= 9) ? PPF_XSPEC_MINW : 1) void k_xspec_w(XspecArgs a) {
+__global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
@@ -209,30 +201,6 @@ __global__ __launch_bounds__(64 * kXW, (PPF_XSPEC_DIRECT && LOG2N <= 9) ? PPF_XS
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
 
-#if PPF_XSPEC_DIRECT
-            {
-                // each wave stores its own row: X[k][n] for k = lane + 64 i
-                // and N - k straight from registers (16 B per lane; the
-                // waves of the workgroup fill each harmonic's line
-                // together), no workgroup barrier and no LDS round trip
-                double2 w = w_seed;
-                double2 *Xn = Xs + n;
-#pragma unroll
-                for (int i = 0; i < NP; ++i) {
-                    const int klo = lane + 64 * i, khi = N - klo;
-                    double2 Dlo, Dhi;
-                    rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
-                    w = cmul(w, w_step);
-                    const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
-                    if (klo < kw) Xn[(int64_t)klo * a.nchan] =
-                        (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
-                    if (khi < kw) Xn[(int64_t)khi * a.nchan] = cscale(cmulc(Dhi, Mhi), inv_e2);
-                    SCHED_CUT();
-                }
-            }
-            if (lane == 0) {
-                if (N / 2 < kw) Xs[(int64_t)(N / 2) * a.nchan + n] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
-#else
             {
                 // in place: X_k -> pad(k), X_{N-k} -> pad(N-k); the pair
                 // (0, N) keeps X_N in pad(N/2) (read above as Dm)
@@ -256,7 +224,6 @@ __global__ __launch_bounds__(64 * kXW, (PPF_XSPEC_DIRECT && LOG2N <= 9) ? PPF_XS
             }
             if (lane == 0) {
                 buf[XNYQ] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
-#endif
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
@@ -264,14 +231,6 @@ __global__ __launch_bounds__(64 * kXW, (PPF_XSPEC_DIRECT && LOG2N <= 9) ? PPF_XS
                 chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
             }
         }
-#if PPF_XSPEC_DIRECT
-        if (n < cend && !live) {
-            // masked channel: zeros where k_pass would read
-            for (int k = lane; k < kw; k += 64) Xs[(int64_t)k * a.nchan + n] = cmk(0.0, 0.0);
-        }
-    }
-}
-#else
         __syncthreads();
         // write-out: thread t -> channel c = t % 8 of the round, harmonics
         // k = t / 8 + 64 j
@@ -291,7 +250,6 @@ __global__ __launch_bounds__(64 * kXW, (PPF_XSPEC_DIRECT && LOG2N <= 9) ? PPF_XS
         __syncthreads();
     }
 }
-#endif
 
 // ===========================================================================
 // k_xmom_g: fused moment pass (see the file header and below)
@@ -504,11 +462,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     };
 
     for (int i = tid; i < TWN; i += 512) tw[i] = a.T[i];
-#ifdef PPF_XM_PRIO
-    // static priority for the second-dispatched half of the workgroup
-    // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if (wave >= XW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     int n = cbase;
     mload(n);
     mstore();

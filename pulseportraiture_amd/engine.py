@@ -110,9 +110,10 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     frequency then phase_transform to nu_fit, GetTOAs; 1: nu_fit, ppalign).
     bounds: method='TNC' box, [5, 2] or [nsub, 5, 2] (lower, upper; None or
     NaN = unbounded), or None for an unbounded fit.
-    solver: minimiser of the scattering fits, "newton" (scaled Newton trust
-    region with an exact subproblem: the same stationary point in 3-4x fewer
-    passes over the cross spectrum) or "scipy" (scipy trust-ncg's own path,
+    solver: minimiser of the unbounded fits, "newton" (scaled Newton trust
+    region with an exact subproblem: the same stationary point, in 3x fewer
+    passes over the cross spectrum for scattering fits and half the data
+    passes for ppalign's) or "scipy" (scipy trust-ncg's own path,
     PPF_OPT_SCIPY_TR); None = SOLVER (env PPF_SOLVER, default "newton").
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in

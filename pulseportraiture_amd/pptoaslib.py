@@ -129,9 +129,11 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
                       quiet=True):
     """pptoaslib.py:974-1144 on the GPU (single sub-integration).
 
-    ``method`` 'trust-ncg' is the reference default and what the device
-    solver replicates; 'Newton-CG' runs the same solver (it converges to the
-    same stationary point).  'TNC' applies ``bounds`` as the reference does
+    ``method`` 'trust-ncg' is the reference default: the device minimises
+    the same objective to the same stationary point with a Newton trust
+    region (scaled coordinates, exact subproblem; scipy's own path with
+    engine.SOLVER = 'scipy'); 'Newton-CG' runs the same solver.  'TNC'
+    applies ``bounds`` as the reference does
     (pptoaslib.py:1041-1046: only for TNC): the device trust-region steps
     are projected onto the box, so the fit ends at the bounded stationary
     point TNC converges to."""

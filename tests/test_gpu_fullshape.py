@@ -276,13 +276,20 @@ def test_gettoas_branches_match_reference(name, monkeypatch, tmp_path,
                 np.asarray(getattr(gt, key[:-1] + "_errs")[f])[held], 0.0)
         np.testing.assert_allclose(gt.red_chi2s[f][conv],
                                    c["out_red_chi2s"][f][conv], rtol=RCHI2)
+        # phi_err and nu_0 at 1e-4 / 1e-5: the reference's own trust-ncg
+        # stops short of the stationary point along the flat GM / tau /
+        # alpha direction (scatgm sub-int 0: Newton decrement 5.9e-6, 3e-9
+        # above the minimum the device's Newton trust region reaches, whose
+        # decrement is 1e-20); the phase error at the hypersensitive nu_0
+        #  moves by 5.3e-5 and nu_0 by 1.6e-6 relative
+        # between the two end points (CPU restatement: tools/tr_probe.py)
         np.testing.assert_allclose(gt.phi_errs[f][conv],
-                                   c["out_phi_errs"][f][conv], rtol=1e-5)
+                                   c["out_phi_errs"][f][conv], rtol=1e-4)
         np.testing.assert_allclose(gt.snrs[f][conv], c["out_snrs"][f][conv],
                                    rtol=1e-6)
         np.testing.assert_allclose(
             np.array(gt.nu_refs[f], dtype=float)[conv],
-            c["out_nu_refs"][f][conv], rtol=1e-6)
+            c["out_nu_refs"][f][conv], rtol=1e-5)
         np.testing.assert_allclose(np.array(gt.nu_fits[f], dtype=float),
                                    c["out_nu_fits"][f], rtol=1e-12)
         cov, cref = np.asarray(gt.covariances[f])[conv], \
@@ -576,11 +583,14 @@ def test_no_x_option_and_x_slots():
         assert got == bad, (n_x, st)
 
 
-def test_recentring_passes_batch_independent_and_deterministic():
+@pytest.mark.parametrize("solver,min_rc", [("scipy", 8), ("newton", 2)])
+def test_recentring_passes_batch_independent_and_deterministic(solver, min_rc):
     """Re-centring launches take the sub-ints k_tr_mom listed through an
     atomic slot counter, packed eight to a workgroup on 8-channel blocks, so
     the packing differs from run to run and from batch to batch: a sub-int's
-    result must not (bitwise), in fits where most sub-ints re-centre."""
+    result must not (bitwise), in fits where many sub-ints re-centre (with
+    scipy's path most do; the Newton trust region's scaled steps leave the
+    expansion radius far less often, 3 of 48 here)."""
     from pulseportraiture_amd import _lib, engine, synth
     nsub, nchan, nbin = 48, 256, 1024
     b = synth.make_batch(nsub, nchan, nbin, first=777)
@@ -599,13 +609,13 @@ def test_recentring_passes_batch_independent_and_deterministic():
             nu_outs=np.full((n, 3), np.nan), guess=True,
             guess_weights=np.ones((n, nchan)),
             guess_DM=np.full(n, dm_start), guess_Ns=nbin, guess_ref=1,
-            errs=errs[sl]))
+            errs=errs[sl], solver=solver))
     I = _lib.RESULT_INDEX
     full = fit(slice(0, nsub))
     again = fit(slice(0, nsub))
     part = fit(slice(5, 21))
     npass = full["results"][:, I["npass"]]
-    assert (npass >= 2).sum() >= 8, npass
+    assert (npass >= 2).sum() >= min_rc, npass
     for k in ("results", "scales", "scale_errs", "channel_snrs", "covariance"):
         np.testing.assert_array_equal(full[k], again[k])
         np.testing.assert_array_equal(full[k][5:21], part[k])

@@ -75,6 +75,15 @@ FITS = [
          seed=105),
     dict(name="pdta_64x128", nchan=64, nbin=128, flags=[1, 1, 0, 1, 1],
          seed=106, tau=2e-3),
+    # low S/N (round 3): |C_n| far below sum_k |Y_k|, where
+    # the moment expansion's truncation bound (relative to sum |Y|) is
+    # loosest, and the initial DM several bins off at the band edges
+    dict(name="lowsnr_pd_512x2048", nchan=512, nbin=2048, flags=[1, 1, 0, 0, 0],
+         seed=107, noise=40.0, dm_off=4e-3),
+    dict(name="lowsnr_pd_64x512", nchan=64, nbin=512, flags=[1, 1, 0, 0, 0],
+         seed=108, noise=12.0, dm_off=1.5e-2),
+    dict(name="lowsnr_all_512x2048", nchan=512, nbin=2048,
+         flags=[1, 1, 1, 1, 1], seed=109, tau=2e-3, noise=12.0),
 ]
 
 
@@ -90,12 +99,13 @@ def fit_inputs(c):
     model, freqs = S.template(nchan, nbin, gmodel=NARROW_GMODEL if
                               c.get("narrow") else None)
     tau = c.get("tau", 0.0)
-    data = S.subint(c["seed"], model, freqs, phi, S.DM0 + dDM, P, tau=tau)
+    data = S.subint(c["seed"], model, freqs, phi, S.DM0 + dDM, P, tau=tau,
+                    noise=c.get("noise", 1.5))
     nu_fit = float(_guess_fit_freq(freqs))
     phi_g = _phase_transform(phi + phi_guess_off, S.DM0, 1500.0, nu_fit, P)
     scat = c["flags"][3] == 1
-    init = [phi_g, S.DM0, 0.0, np.log10(1.0 / nbin) if scat else 0.0,
-            -4.0 if scat else 0.0]
+    init = [phi_g, S.DM0 + c.get("dm_off", 0.0), 0.0,
+            np.log10(1.0 / nbin) if scat else 0.0, -4.0 if scat else 0.0]
     return data, model, freqs, P, np.array([phi, S.DM0 + dDM, 0.0, tau,
                                             -4.0]), init, nu_fit
 

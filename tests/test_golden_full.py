@@ -47,7 +47,8 @@ def _oracle_fit(c, data, model, freqs):
 
 
 @pytest.mark.parametrize("name", ["c3_pdta_512x2048", "narrow_pd_512x2048",
-                                  "pd_64x4096", "pdta_64x128"])
+                                  "pd_64x4096", "pdta_64x128",
+                                  "lowsnr_pd_512x2048", "lowsnr_pd_64x512"])
 def test_oracle_matches_reference_fullshape_fits(name):
     c, data, model, freqs = F.fit_case(name)
     r = _oracle_fit(c, data, model, freqs)

@@ -31,12 +31,18 @@ def _kept_harmonic_fraction(model):
 # ----------------------------------------------- fit_portrait_full (C3 ...) --
 @pytest.mark.parametrize("name", ["c3_all_512x2048_a", "c3_all_512x2048_b",
                                   "c3_pdta_512x2048", "narrow_pd_512x2048",
-                                  "pd_64x4096", "pdta_64x128"])
+                                  "pd_64x4096", "pdta_64x128",
+                                  "lowsnr_pd_512x2048", "lowsnr_pd_64x512",
+                                  "lowsnr_all_512x2048"])
 def test_fullshape_fit_matches_reference(name):
     """configs[2]'s fit (phi, DM, GM, tau, alpha) and phi+DM+tau+alpha at
     512 x 2048, a narrow-component template at 512 x 2048 (no harmonic
-    cutoff may apply: its power reaches Nyquist), and the block-FFT fallback
-    shapes nbin = 4096 and 128, through the drop-in fit_portrait_full."""
+    cutoff may apply: its power reaches Nyquist), the block-FFT fallback
+    shapes nbin = 4096 and 128, and three low-S/N fits (S/N 45 and 26 with
+    the initial DM several bins off at the band edges: the moment path's
+    truncation bound is relative to sum_k |Y_k|, loosest when |C_n| is
+    small; S/N 133 with all five parameters), through the drop-in
+    fit_portrait_full."""
     from pulseportraiture_amd import pptoaslib
     c, data, model, freqs = F.fit_case(name)
     if int(c["narrow"]):
@@ -168,13 +174,22 @@ def test_fullshape_gettoas_matches_reference(name, monkeypatch, tmp_path,
     _tim_tokens_match(lines, list(c["out_tim_lines"]))
 
 
-def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True):
+def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True,
+                      nu0_rtol=1e-8, tok_rtol=0.0):
+    """Every .tim token to its printed precision; nu_0 (token 1) within
+    1e-8 relative.  nu0_rtol > 1e-8: a line whose nu_0 moved by more than
+    1e-8 (but less than nu0_rtol) reports its TOA at that other frequency,
+    so token 2 is not comparable there (the phase at the reference's nu_0
+    is checked to 0.01 sigma by the caller); tok_rtol > 0: the other
+    numeric tokens may also differ by that relative amount beyond their
+    printed precision."""
     assert len(lines) == len(ref)
     for il, (a, b) in enumerate(zip(lines, ref)):
         if il in skip_lines:
             continue
         ta, tb = a.split(), b.split()
         assert len(ta) == len(tb), (a, b)
+        moved = abs(float(ta[1]) / float(tb[1]) - 1) >= 1e-8
         for i, (x, y) in enumerate(zip(ta, tb)):
             if x.endswith((".gmodel", ".spl")):   # -tmplt path differs
                 continue
@@ -182,7 +197,12 @@ def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True):
                 continue
             if i == 1:
                 # nu_0 (see test_fullshape_gettoas_matches_reference)
-                assert abs(float(x) / float(y) - 1) < 1e-8, (a, b)
+                assert abs(float(x) / float(y) - 1) < nu0_rtol, (a, b)
+                continue
+            if i == 2 and moved:
+                continue
+            if tok_rtol and not _same_printed_number(x, y):
+                assert abs(float(x) / float(y) - 1) < tok_rtol, (i, a, b)
                 continue
             assert _same_printed_number(x, y), (i, a, b)
 
@@ -310,8 +330,14 @@ def test_gettoas_branches_match_reference(name, monkeypatch, tmp_path,
     # TNC: the reference's loosely converged x leaves nu_0 (token 1) and
     # the TOA at it (token 2) off in their last printed digits; they are
     # checked above through nu_refs (1e-6) and the transformed phase
+    # scatgm (phi, DM, GM, tau, alpha; nu_0 from the approximate
+    # [1, 1, 0, 1, 1] case): where the reference's trust-ncg stopped short
+    # of the stationary point (see the nu_refs check above) nu_0 sits up to
+    # 1.6e-6 away from the device's and the printed DM 1e-6 (0.0014 sigma)
     _tim_tokens_match(lines, list(c["out_tim_lines"]), skip,
-                      nu0_tokens=not tnc)
+                      nu0_tokens=not tnc,
+                      nu0_rtol=1e-5 if name == "scatgm" else 1e-8,
+                      tok_rtol=1e-5 if name == "scatgm" else 0.0)
     if tnc and skip:
         print("reference TNC unconverged (MAXFUN) on lines", skip)
 

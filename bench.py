@@ -844,6 +844,11 @@ def main():
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),
                roofline=roof, fp64_roofline=fp64, stage_ms=stages, kernels=kernels,
+               # algorithmic HBM bytes of the priced kernels per fit (the
+               # guess pass, the spectrum / moment pass and, for scattering
+               # fits, every streaming evaluation)
+               bytes_per_fit=round(sum(float(v["bytes"]) for v in kern.values())
+                                   / max(steps_subints, 1)),
                mean_passes_per_fit=round(mean_passes, 3),
                mean_evals_per_fit=round(mean_nfev, 3),
                fits_converged_frac=round(float(np.mean(

@@ -288,6 +288,11 @@ constexpr int kMoments = 32;     // Taylor moments per channel
 // of the objective (chi^2 units) below which the fit has converged
 constexpr double kNewtonR0 = 10.0;
 constexpr double kNewtonTol = 1e-12;
+// its warm start on a channel subset (every sub-th group of 64 channels;
+// scattering fits with >= 256 channels): leave it for every channel once an
+// interior step predicts less than kSubsetSwitch (chi^2 units of the subset)
+constexpr double kSubsetSwitch = 1.0;
+constexpr int kSubsetMaxStride = 16;
 hipError_t launch_postfit(const SolveArgs &a, hipStream_t st);
 size_t tr_state_bytes();
 int pass_blocks(int nchan);

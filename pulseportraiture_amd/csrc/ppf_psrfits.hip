@@ -39,6 +39,9 @@ __device__ __forceinline__ float sample_f32(const uint8_t *p, int elem, int64_t 
 }
 
 __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a) {
+    // DATA * DAT_SCL + DAT_OFFS rounds twice, as PSRCHIVE's (and NumPy's)
+    // float32 arithmetic does: the product is pinned in a register before
+    // the add, so the compiler cannot fuse them (-ffp-contract=fast)
     const int nblk = (a.nchan + kUnpackChans - 1) / kUnpackChans;
     const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const uint8_t *raw = a.raw + (int64_t)s * a.sub_stride;
@@ -52,9 +55,10 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs a) {
             float v = 0.0f;
             for (int p = 0; p < npol_used; ++p) {
                 const int64_t i = ((int64_t)p * a.nchan + n) * a.nbin + b;
-                const float x = __fadd_rn(__fmul_rn(sample_f32(raw, a.elem, i), scl[p * a.nchan + n]),
-                                          off[p * a.nchan + n]);
-                v = p == 0 ? x : __fadd_rn(v, x);
+                float prod = sample_f32(raw, a.elem, i) * scl[p * a.nchan + n];
+                asm volatile("" : "+v"(prod));      // rounded product: no fma
+                const float x = prod + off[p * a.nchan + n];
+                v = p == 0 ? x : v + x;
             }
             a.out[((int64_t)s * a.nchan + n) * a.nbin + b] = v;
             const double w = a.wts ? (double)a.wts[(int64_t)s * a.nchan + n] : 1.0;

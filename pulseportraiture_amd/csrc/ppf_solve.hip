@@ -31,6 +31,11 @@ namespace ppf {
 #ifndef PPF_NEWTON_MOM
 #define PPF_NEWTON_MOM 1
 #endif
+// channel-subset warm start of the Newton scattering fits (0: every
+// evaluation on every channel)
+#ifndef PPF_NEWTON_SUBSET
+#define PPF_NEWTON_SUBSET 1
+#endif
 
 // ===========================================================================
 // per-channel likelihood terms (pptoaslib.py:195-561)
@@ -251,6 +256,16 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
         // (tr_update_newton) unless the caller asked for scipy's path
         S.newton = (a.newton && (scat || PPF_NEWTON_MOM) && !bnd) ? 1 : 0;
         S.radius = S.newton ? kNewtonR0 : 1.0;   // scipy initial_trust_radius = 1
+        // channel-subset warm start of the scattering fits (every sub-th
+        // group of 64 channels, at least two groups; PPF_NEWTON_SUBSET)
+        int sub = 1;
+        if (PPF_NEWTON_SUBSET && S.newton && scat) {
+            const int ng = (a.nchan + 63) / 64;
+            while (sub * 2 <= kSubsetMaxStride && sub * 2 <= ng / 2) sub *= 2;
+        }
+        S.sub = sub;
+        S.sub0 = sub;
+        S.nsubev = 0;
         S.pnorm = 0.0;
         S.pred = 0.0;
         for (int i = 0; i < 3; ++i) S.nu_fit[i] = nu_fit[i];
@@ -375,7 +390,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 #pragma unroll
     for (int i = 0; i < 21; ++i) acc[i] = 0.0;
     const int n = blk * kPassChans + threadIdx.x;
-    const bool use_n = n < a.nchan && (!mask || mask[n]);
+    // Newton warm start: only every S.sub-th group of 64 channels (a wave)
+    const bool in_sub = S.sub <= 1 || ((n >> 6) % S.sub) == 0;
+    const bool use_n = in_sub && n < a.nchan && (!mask || mask[n]);
     // harmonics the wave sums: up to the largest cutoff of its channels
     // (k_model_cut; wave-uniform so the loads stay coalesced)
     const int kend = (int)wave_max(use_n ? (double)a.KC[(int64_t)mi * a.nchan + n] : 1.0);
@@ -689,12 +706,15 @@ __device__ int tr_update_newton(TRState &S, const double *o, int max_iter, const
     const int maxiter = max_iter > 0 ? max_iter : 200 * 5;
     bool done = false;
     int cmd = 0;
-    if (S.phase == PH_INIT) {
-        S.nfev = 1;
+    if (S.sub > 1) S.nsubev += 1;        // o is a channel-subset evaluation
+    if (S.phase == PH_INIT || S.phase == PH_RESTART) {
+        // first evaluation, or the point x evaluated again on every channel
+        S.nfev = S.phase == PH_INIT ? 1 : S.nfev + 1;
         S.f = o[0];
         for (int i = 0; i < 5; ++i) S.g[i] = o[1 + i];
         for (int i = 0; i < 15; ++i) S.H[i] = o[6 + i];
         if (!(o[0] == o[0])) { S.status = PPF_ST_NONFINITE; done = true; }
+        S.slot_cur = S.slot_eval;
         S.macc = S.meval;
     } else {
         S.nfev += 1;
@@ -739,7 +759,9 @@ __device__ int tr_update_newton(TRState &S, const double *o, int max_iter, const
             pn += p[q] * p[q];
         }
         const double pred = -(gp + 0.5 * pHp);
-        if (!(pred > kNewtonTol)) {
+        if (S.sub > 1 && !hb && pred < kSubsetSwitch) {
+            done = true;                 // the subset's basin is found: switch below
+        } else if (!(pred > kNewtonTol)) {
             done = true;                 // converged (scipy's warnflag 2 status)
         } else {
             for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
@@ -751,6 +773,16 @@ __device__ int tr_update_newton(TRState &S, const double *o, int max_iter, const
             S.slot_eval = S.slot_cur ^ 1;
             cmd = 1;
         }
+    }
+    if (done && S.sub > 1 && S.status != PPF_ST_NONFINITE) {
+        // leave the channel subset: evaluate x on every channel and go on
+        // from there (a fit never ends on a subset evaluation, so k_postfit
+        // always reads complete per-channel terms)
+        S.sub = 1;
+        for (int i = 0; i < 5; ++i) S.th[i] = S.x[i];
+        S.slot_eval = S.slot_cur ^ 1;
+        S.phase = PH_RESTART;
+        return 1;
     }
     S.phase = done ? PH_DONE : PH_PROPOSAL;
     return cmd;
@@ -1595,7 +1627,14 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
         res->x_fit_tau = x[3];
         // full passes over X: one per evaluation (k_pass) or one per moment
         // (re)centre (k_moments)
-        res->npass = S.mmode ? (double)S.nmom + 1.0 : (double)nfev;
+        // passes over X: subset evaluations count their fraction of the
+        // channel groups
+        double npass = S.mmode ? (double)S.nmom + 1.0 : (double)nfev;
+        if (!S.mmode && S.nsubev > 0) {
+            const int ng = (a.nchan + 63) / 64, nsel = (ng + S.sub0 - 1) / S.sub0;
+            npass -= (double)S.nsubev * (1.0 - (double)nsel / (double)ng);
+        }
+        res->npass = npass;
         res->reserved[0] = res->reserved[1] = 0.0;
     }
 }

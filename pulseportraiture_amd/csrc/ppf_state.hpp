@@ -8,7 +8,9 @@ namespace ppf {
 // ===========================================================================
 // per-sub-integration solver state (workspace)
 // ===========================================================================
-enum { PH_INIT = 0, PH_PROPOSAL = 1, PH_DONE = 2 };
+// PH_RESTART: the Newton solver's switch from the channel subset to every
+// channel: the pending evaluation is at the accepted point x (not a proposal)
+enum { PH_INIT = 0, PH_PROPOSAL = 1, PH_DONE = 2, PH_RESTART = 3 };
 
 struct TRState {
     double x[5];          // accepted point
@@ -19,7 +21,8 @@ struct TRState {
     int k, status, nfev, phase;
     int slot_cur, slot_eval, flagmask, nchanx;
     int scat, hb, g_sum, g_tau;
-    int g_alpha, newton, pad1, pad2;   // newton: PPF_TR_NEWTON solver (see tr_update_newton)
+    int g_alpha, newton, sub, pad2;    // newton: Newton trust region; sub: channel-group stride of
+                                       // its warm start (1: every channel; tr_update_newton)
     // moment mode (no scattering): two moment sets centred at mc[q]
     int mmode, need_mom, mtarget, macc;
     int mvalid[2], meval, nmom;
@@ -29,6 +32,7 @@ struct TRState {
     double lo[5], hi[5];
     int bnd, pad3;
     double pnorm;         // Newton solver: |scaled step| of the pending proposal
+    int nsubev, sub0;     // evaluations on the channel subset; its initial stride
 };
 
 __device__ __forceinline__ int uidx(int i, int j) {     // upper-tri index, i <= j

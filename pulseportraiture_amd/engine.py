@@ -8,6 +8,7 @@ convert to the reference's numpy/DataBunch forms.
 """
 import ctypes
 import os
+import threading
 import warnings
 
 import numpy as np
@@ -46,6 +47,50 @@ def to_dev(x, dev, dtype):
             warnings.simplefilter("ignore", UserWarning)
             return torch.as_tensor(a, dtype=dtype).to(dev)
     return torch.as_tensor(a, dtype=dtype).to(dev)
+
+
+_PIN = {}
+_PIN_LOCK = threading.Lock()
+
+
+def _pinned(tag, nbytes):
+    """A page-locked staging buffer of at least nbytes, one per (thread,
+    tag), grown on demand and reused: the single-call APIs copy their host
+    arrays through it instead of torch's pageable path (whose per-call
+    staging made a 512 x 2048 rotate_data take 1.6-25 ms)."""
+    key = (threading.get_ident(), tag)
+    with _PIN_LOCK:
+        buf = _PIN.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8,
+                              pin_memory=True)
+            _PIN[key] = buf
+    return buf
+
+
+def host_to_dev(x, dev, dtype):
+    """to_dev through the caller's pinned staging buffer (the copy is
+    ordered on the current stream; the buffer is reused only by the same
+    thread's next call, which comes after this call's own synchronising
+    read-back)."""
+    a = np.ascontiguousarray(x)
+    t = torch.as_tensor(a) if a.flags.writeable else torch.from_numpy(a.copy())
+    t = t.to(dtype)
+    buf = _pinned("in", t.numel() * t.element_size())
+    h = buf[:t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+    h.copy_(t)
+    return h.to(dev, non_blocking=True)
+
+
+def dev_to_host(t):
+    """A NumPy copy of device tensor t, read back through the caller's
+    pinned staging buffer (synchronises the current stream)."""
+    n = t.numel() * t.element_size()
+    buf = _pinned("out", n)
+    h = buf[:n].view(t.dtype).view(t.shape)
+    h.copy_(t, non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return h.numpy().copy()
 
 
 def _p(t):
@@ -306,7 +351,8 @@ def rotate_rows(rows, phases, dev=None):
     """irfft(rfft(row) * exp(2 pi i k phase)) for each row of rows [..., nbin]
     (float64 output, same leading shape)."""
     dev = device(dev)
-    r = to_dev(rows, dev, _data_dtype(rows))
+    r = to_dev(rows, dev, _data_dtype(rows)) if isinstance(rows, torch.Tensor) \
+        else host_to_dev(rows, dev, _data_dtype(rows))
     shape = r.shape
     nbin = shape[-1]
     r2 = r.reshape(-1, nbin).contiguous()

@@ -363,10 +363,10 @@ def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
         nrows = int(np.prod(shape[:-1])) if ndim > 1 else 1
         out = engine.rotate_rows(data.reshape(nrows, nbin),
                                  np.full(nrows, float(phase)))
-        return out.cpu().numpy().reshape(shape)
-    d4 = np.copy(data)
+        return engine.dev_to_host(out).reshape(shape)
+    d4 = data                       # only read: the result is a new array
     while d4.ndim != 4:
-        d4 = np.array([d4])
+        d4 = d4[None]
     nsub, npol, nchan = d4.shape[:3]
     D = Dconst * DM / (np.ones(nsub) * Ps)
     if len(D) != nsub:
@@ -398,7 +398,7 @@ def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
     ph = phase + D[:, None] * fterm
     ph = np.broadcast_to(ph[:, None, :], (nsub, npol, nchan))
     out = engine.rotate_rows(d4.reshape(-1, nbin), ph.reshape(-1))
-    out = out.cpu().numpy().reshape(d4.shape)
+    out = engine.dev_to_host(out).reshape(d4.shape)
     if ndim == 1:
         return out[0, 0, 0]
     if ndim == 2:

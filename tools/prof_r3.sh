@@ -18,4 +18,13 @@ for m in c2 c3; do
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $out/fetch_$m -o fetch --output-format csv -- python3 bench.py $args > $out/fetch_$m.log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $out/write_$m -o write --output-format csv -- python3 bench.py $args > $out/write_$m.log 2>&1
 done
-echo prof_done
+
+# SQ counters of the C3 command (k_xspec_w / k_pass issue and wait split)
+p1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
+p2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"
+i=0
+for p in "$p1" "$p2"; do
+  i=$((i+1))
+  timeout -s KILL 300 rocprofv3 --pmc $p -d $out/sq${i}_c3 -o sq$i --output-format csv -- python3 bench.py $c3 > $out/sq${i}_c3.log 2>&1
+done
+echo sq_done

@@ -42,7 +42,11 @@
 
 namespace ppf {
 
-constexpr int kXW = 8;                 // waves per k_xspec_w workgroup
+constexpr int kXW = 8;                 // waves per k_align_part_w workgroup
+#ifndef PPF_XSPEC_WAVES
+#define PPF_XSPEC_WAVES 8
+#endif
+constexpr int kXSW = PPF_XSPEC_WAVES;  // waves (= channel rows per round) per k_xspec_w workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 // row elements as native vectors: arrays of HIP_vector_type structs carried
 // across the row loop are not promoted to VGPRs
@@ -101,7 +105,7 @@ template <int LOG2N>
 __host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + 2; }
 
 template <int LOG2N, int DT>
-__global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
+__global__ __launch_bounds__(64 * kXSW) void k_xspec_w(XspecArgs a) {
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
@@ -115,9 +119,9 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     int s, cb;
     block_map(a.xcd_swizzle, a.nblk, s, cb);
     if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
-    // rounds: in round r wave w takes channel cb*CB + r*kXW + w
+    // rounds: in round r wave w takes channel cb*CB + r*kXSW + w
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
-    const int nround = (a.cb + kXW - 1) / kXW;
+    const int nround = (a.cb + kXSW - 1) / kXSW;
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double sqrtN = sqrt((double)N);
@@ -152,11 +156,11 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
     };
     int n = cbase + wave;
     if (usable(n)) fetch(n);
-    for (int r = 0; r < nround; ++r, n += kXW) {
+    for (int r = 0; r < nround; ++r, n += kXSW) {
         const bool live = usable(n);
         if (n < cend && !live) {
             if (lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
-            if (usable(n + kXW)) fetch(n + kXW);
+            if (usable(n + kXSW)) fetch(n + kXSW);
         }
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
@@ -164,8 +168,8 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
 #pragma unroll
             for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
             const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-            const bool nxt = usable(n + kXW);
-            if (nxt) fetch(n + kXW);                   // next row in flight during this FFT
+            const bool nxt = usable(n + kXSW);
+            if (nxt) fetch(n + kXSW);                   // next row in flight during this FFT
             wfft::fft_row<LOG2N>(x, buf, a.T, lane);
 
             // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
@@ -235,12 +239,12 @@ __global__ __launch_bounds__(64 * kXW) void k_xspec_w(XspecArgs a) {
         // write-out: thread t -> channel c = t % 8 of the round, harmonics
         // k = t / 8 + 64 j
         {
-            const int c = threadIdx.x & 7, n0 = cbase + r * kXW;
+            const int c = threadIdx.x % kXSW, n0 = cbase + r * kXSW;
             const int nc = n0 + c;
             if (nc < cend) {
                 const bool ok = !mask || mask[nc];
                 const double2 *b = lds + c * SL;
-                for (int k = threadIdx.x >> 3; k < kw; k += 64 * kXW / 8) {
+                for (int k = threadIdx.x / kXSW; k < kw; k += 64) {
                     const int slot = k == N ? wfft::pad<LOG2N>(N / 2)
                                             : (k == N / 2 ? XNYQ : wfft::pad<LOG2N>(k));
                     Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);
@@ -688,13 +692,13 @@ __global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan
 // ===========================================================================
 template <int L2, int DT>
 static void launch_w(const XspecArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)kXW * xspec_slw<L2>() * sizeof(double2);
-    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kXW);
+    const size_t lds = (size_t)kXSW * xspec_slw<L2>() * sizeof(double2);
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kXSW);
     hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
 }
 
 bool xspec_wave_supported(int log2N, int cb) {
-    return log2N >= 7 && log2N <= 10 && cb % kXW == 0;
+    return log2N >= 7 && log2N <= 10 && cb % kXSW == 0 && cb % kXW == 0;
 }
 
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {

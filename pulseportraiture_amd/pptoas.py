@@ -431,11 +431,31 @@ class GetTOAs(object):
         # does archive i's bookkeeping.
         stager = _Stager()
         pool = ThreadPoolExecutor(max_workers=1)
+        # load_data of archive i+1 runs on its own thread while archive i is
+        # prepared (a PSRFITS archive's read, upload and device unpack:
+        # psrfits.load_data); the reference's first load_data call, made
+        # ahead of time, with the same arguments
+        loader = ThreadPoolExecutor(max_workers=1)
+        mine = list(mine)
+        loads = {}
+
+        def _load(f):
+            return load_data(f, dedisperse=False, dededisperse=False,
+                             tscrunch=tscrunch, pscrunch=True, fscrunch=False,
+                             rm_baseline=rm_baseline, flux_prof=False,
+                             refresh_arch=False, return_arch=False,
+                             quiet=quiet)
         pending = None
         err = None
         try:
-            for iarch in mine:
-                job = self._prep_archive(iarch, datafiles[iarch], ctx, stager)
+            for pos, iarch in enumerate(mine):
+                if iarch not in loads:
+                    loads[iarch] = loader.submit(_load, datafiles[iarch])
+                if pos + 1 < len(mine):
+                    nxt = mine[pos + 1]
+                    loads[nxt] = loader.submit(_load, datafiles[nxt])
+                job = self._prep_archive(iarch, datafiles[iarch], ctx, stager,
+                                         loads.pop(iarch))
                 if job is None:
                     continue
                 fut = pool.submit(self._fit_archive, job, ctx)
@@ -451,6 +471,9 @@ class GetTOAs(object):
             err = exc
         finally:
             pool.shutdown(wait=True)
+            for fu in loads.values():
+                fu.cancel()
+            loader.shutdown(wait=True)
             stager.close()
         if by_archive:
             # a failed rank must not leave the others in the gather
@@ -490,21 +513,25 @@ class GetTOAs(object):
             self.TOA_list.extend(r["_toas"])
 
     # ------------------------------------------------------------------
-    def _prep_archive(self, iarch, datafile, ctx, stager):
+    def _prep_archive(self, iarch, datafile, ctx, stager, loaded=None):
         """Load one archive and build its batch (pptoas.py:258-529); None if
-        the archive is skipped."""
+        the archive is skipped.  loaded: the future of load_data(datafile)
+        already started ahead (get_TOAs' loader thread)."""
         quiet, tscrunch, fit_scat = ctx["quiet"], ctx["tscrunch"], \
             ctx["fit_scat"]
         nu_fit_tuple, nu_ref_tuple, bary = ctx["nu_fit_tuple"], \
             ctx["nu_ref_tuple"], ctx["bary"]
         fit_duration = 0.0
         try:
-            data = load_data(datafile, dedisperse=False,
-                             dededisperse=False, tscrunch=tscrunch,
-                             pscrunch=True, fscrunch=False,
-                             rm_baseline=rm_baseline, flux_prof=False,
-                             refresh_arch=False, return_arch=False,
-                             quiet=quiet)
+            if loaded is not None:
+                data = loaded.result()
+            else:
+                data = load_data(datafile, dedisperse=False,
+                                 dededisperse=False, tscrunch=tscrunch,
+                                 pscrunch=True, fscrunch=False,
+                                 rm_baseline=rm_baseline, flux_prof=False,
+                                 refresh_arch=False, return_arch=False,
+                                 quiet=quiet)
             if data.dmc:
                 if not quiet:
                     print("%s is dedispersed (dmc = 1).  Reloading it." %

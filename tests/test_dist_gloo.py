@@ -215,8 +215,10 @@ def _fake_gettoas(nfile, skip=()):
             self.quiet = True
             self.seen = []
 
-        def _prep_archive(self, iarch, datafile, ctx, stager):
+        def _prep_archive(self, iarch, datafile, ctx, stager, loaded=None):
             self.seen.append(iarch)
+            # get_TOAs' loader thread already ran load_data on this archive
+            assert loaded is not None and loaded.result() == datafile
             if iarch in skip:                 # load_data failed: skipped
                 return None
             self.ok_idatafiles.append(iarch)
@@ -242,6 +244,13 @@ def _fake_gettoas(nfile, skip=()):
     return G()
 
 
+def _recording_loader(log):
+    def load(filename, **kw):
+        log.append(filename)
+        return filename
+    return load
+
+
 def _summary(gt):
     from pulseportraiture_amd import pptoas
     out = {a: [np.asarray(v).tolist() for v in getattr(gt, a)]
@@ -261,8 +270,13 @@ def _archive_worker(rank, world, port, nfile, skip, q):
     sys.path.insert(0, os.path.dirname(__file__))
     import test_dist_gloo as T
     pdist.init("gloo")
+    from pulseportraiture_amd import pptoas
+    loaded = []
+    pptoas.load_data = T._recording_loader(loaded)
     gt = T._fake_gettoas(nfile, skip)
     gt.get_TOAs(quiet=True)
+    # each rank's loader read exactly its own archives, once each
+    assert sorted(loaded) == sorted(gt.datafiles[i] for i in gt.seen), loaded
     q.put((rank, gt.seen, T._summary(gt)))
     dist.barrier()
     dist.destroy_process_group()
@@ -274,8 +288,15 @@ def test_gettoas_archive_sharding_equals_serial(nfile, skip):
     none missed) and ends with exactly the serial run's per-archive
     attributes and TOA list (archive order; skipped archives absent; PSRCHIVE
     MJDs that cannot be pickled travel as their printed int/frac day)."""
-    serial = _fake_gettoas(nfile, skip)
-    serial.get_TOAs(quiet=True)
+    from pulseportraiture_amd import pptoas
+    loaded, real = [], pptoas.load_data
+    pptoas.load_data = _recording_loader(loaded)
+    try:
+        serial = _fake_gettoas(nfile, skip)
+        serial.get_TOAs(quiet=True)
+    finally:
+        pptoas.load_data = real
+    assert sorted(loaded) == sorted(serial.datafiles)
     ref = _summary(serial)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -13,8 +13,8 @@ c5="--fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 1 --warmup 1 --cpu-s
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $out/ks_c2 -o ks --output-format csv -- python3 bench.py $c2 > $out/ks_c2.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/ks_c3 -o ks --output-format csv -- python3 bench.py $c3 > $out/ks_c3.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/ks_c5 -o ks --output-format csv -- python3 bench.py $c5 > $out/ks_c5.log 2>&1
-for m in c2 c3; do
-  args=$c2; [ $m = c3 ] && args=$c3
+for m in c2 c3 c5; do
+  args=$c2; [ $m = c3 ] && args=$c3; [ $m = c5 ] && args=$c5
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $out/fetch_$m -o fetch --output-format csv -- python3 bench.py $args > $out/fetch_$m.log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $out/write_$m -o write --output-format csv -- python3 bench.py $args > $out/write_$m.log 2>&1
 done

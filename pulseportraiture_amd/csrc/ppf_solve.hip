@@ -1017,6 +1017,18 @@ __device__ __forceinline__ void taylor_seg(const double2 (&mu)[M1 - M0], double 
 #ifndef PPF_TRMOM_WPE
 #define PPF_TRMOM_WPE 2
 #endif
+#ifdef PPF_TM_PROF
+// section cycle counters of k_tr_mom, thread 0 of each workgroup (profiling
+// builds only: tools/tprof.py)
+__device__ unsigned long long g_tprof[8];
+#define TP_INIT() unsigned long long tp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long tp_t = __builtin_amdgcn_s_memtime()
+#define TP(i) do { const unsigned long long tp_n = __builtin_amdgcn_s_memtime(); tp_acc[i] += tp_n - tp_t; tp_t = tp_n; } while (0)
+#define TP_DONE() do { if (tid == 0) for (int ti = 0; ti < 8; ++ti) atomicAdd(&g_tprof[ti], tp_acc[ti]); } while (0)
+#else
+#define TP_INIT()
+#define TP(i)
+#define TP_DONE()
+#endif
 // k_tr_mom: one workgroup per moment-mode sub-integration; runs trust-region
 // iterations back to back, every evaluation from the moments, until the fit
 // stops or a point leaves the expansion radius of both moment sets (then it
@@ -1033,6 +1045,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
     if (s >= a.nsub) return;
     TRState &G = a.state[s];
     if (!G.mmode || G.phase == PH_DONE) return;          // uniform per workgroup
+    TP_INIT();
     static_assert(sizeof(TRState) % 8 == 0, "TRState copy");
     constexpr int NW = (int)(sizeof(TRState) / 8);
     for (int i = tid; i < NW; i += kBlock)
@@ -1055,6 +1068,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
     __syncthreads();
     if (tid == 0) L.need_mom = 0;
     const int cap = (a.max_iter > 0 ? a.max_iter : 1000) + 4;
+    TP(0);
     for (int it = 0; it < cap; ++it) {
         __syncthreads();
         const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
@@ -1086,6 +1100,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                 xsel = kTwoPi * h * xm[0];
             }
         }
+        TP(1);
         if (qsel < 0) {
             if (tid == 0) {
                 const int tgt = L.mvalid[L.macc] ? 1 - L.macc : L.macc;
@@ -1168,7 +1183,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                 if ((flagmask >> hi[e] & 1) && (flagmask >> hj[e] & 1))
                     acc[4 + e] += hn * dph[hi[e]] * dph[hj[e]];
         }
+        TP(2);
         block_sum<10>(acc, red);
+        TP(3);
         if (tid == 0) {
             double o[21];
 #pragma unroll
@@ -1185,12 +1202,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
             cmdb = tr_update<3>(L, o, a.max_iter);
 #endif
         }
+        TP(4);
         __syncthreads();
+        TP(5);
         if (!cmdb) break;
     }
     __syncthreads();
     for (int i = tid; i < NW; i += kBlock)
         reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&L)[i];
+    TP(6);
+    TP_DONE();
 }
 
 // nu_zero-case accumulation slots
@@ -1697,3 +1718,15 @@ size_t tr_state_bytes() { return sizeof(TRState); }
 int pass_blocks(int nchan) { return (nchan + kPassChans - 1) / kPassChans; }
 
 }  // namespace ppf
+
+#ifdef PPF_TM_PROF
+extern "C" int ppf_debug_tprof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ppf::g_tprof), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ppf::g_tprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

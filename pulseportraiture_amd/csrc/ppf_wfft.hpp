@@ -5,11 +5,10 @@
 // every Stockham stage is a radix-R (last stage: the remaining radix) DFT
 // done entirely in registers, and the data is exchanged between stages
 // through the wave's own LDS buffer.  The buffer is padded by one slot per
-// 2^S (pad(idx) = idx + (idx >> S), S = max(3, log2 R)) so the stride-R
-// stores of the first stage and the strided reads of the later stages are
-// bank-conflict free for ds_*_b128, and every access is a lane-dependent base
-// plus a compile-time offset (folded into the ds_* immediate: no per-element
-// address registers held across the row loop).
+// 2^S (pad(idx) = idx + (idx >> S), S = max(3, log2 R)), so the stride-R
+// stores of the first stage are conflict-free and every access is a
+// lane-dependent base plus a compile-time offset (folded into the ds_*
+// immediate: no per-element address registers held across the row loop).
 // Stage twiddles: one read of w = T[k N/(radix L)] (global table, L1/L2
 // resident) per butterfly, the other powers by recurrence.
 //
@@ -127,18 +126,60 @@ struct Plan {
     static constexpr int toff(int s) { return L(s) - L2; }
 };
 
+// Element idx -> LDS slot.  Default: the padding above.  PPF_LDS_XOR=1: slot
+// = idx ^ ((idx >> SH) & MK), a permutation inside aligned blocks, no padding.
+// Priced with MI355X_MICROARCH.md's LDS lane groups (tools/lds_conflicts.py),
+// the XOR map cuts the extra bank-conflict cycles of a 1024-point row from
+// 2.25 to 0.75 per ds_*_b128 (the padding moves lanes 16-31 of a
+// ds_read_b128 group one slot onto lanes 0-15's banks) and makes the
+// eight-channel write-out of k_xspec_w conflict-free.  Measured on MI355X
+// (89 GPU tests green with it): C2 and C3 unchanged (k_xmom_g, k_xspec_w are
+// f64-issue bound, not LDS bound), C5 7% slower (k_xspec_w<9> needs 136
+// VGPRs instead of 124: three waves per SIMD instead of four).  Kept off.
+#ifndef PPF_LDS_XOR
+#define PPF_LDS_XOR 0
+#endif
+template <int LOG2N>
+struct Swz {
+    static constexpr int SH = LOG2N == 7 ? 2 : (LOG2N == 10 ? 4 : 3);
+    static constexpr int MK = LOG2N == 7 ? 3 : 7;
+    // offsets that are multiples of FREE commute with the map
+    static constexpr int FREE = PPF_LDS_XOR ? (MK + 1) << SH : 1 << Plan<LOG2N>::S;
+};
 template <int LOG2N>
 __device__ __forceinline__ constexpr int pad(int idx) {
+#if PPF_LDS_XOR
+    return idx ^ ((idx >> Swz<LOG2N>::SH) & Swz<LOG2N>::MK);
+#else
     return idx + (idx >> Plan<LOG2N>::S);
+#endif
+}
+// pad(a + C) given pad(a), for a compile-time C that is a multiple of FREE
+template <int LOG2N, int C>
+__device__ __forceinline__ int pad_add(int pa) {
+    static_assert(C % Swz<LOG2N>::FREE == 0, "offset must commute with the slot map");
+#if PPF_LDS_XOR
+    return pa + C;
+#else
+    return pa + C + (C >> Plan<LOG2N>::S);
+#endif
 }
 // LDS slots of one wave buffer
 template <int LOG2N>
-__host__ __device__ constexpr int buf_slots() { return Plan<LOG2N>::N + (Plan<LOG2N>::N >> Plan<LOG2N>::S); }
-
-// slot of element lane + C (C a compile-time multiple of 64): base + const
+__host__ __device__ constexpr int buf_slots() {
+#if PPF_LDS_XOR
+    return Plan<LOG2N>::N;
+#else
+    return Plan<LOG2N>::N + (Plan<LOG2N>::N >> Plan<LOG2N>::S);
+#endif
+}
+// slot of element lane + C, C a compile-time multiple of 64: one of two
+// lane bases (lb[0] = pad(lane), lb[1] = pad(lane + 64) - 64) plus a constant
 template <int LOG2N, int C>
-__device__ __forceinline__ int slot_lane(int lane_base /* pad(lane) */) {
-    return lane_base + C + (C >> Plan<LOG2N>::S);
+__device__ __forceinline__ int lane_slot(const int (&lb)[2]) {
+    constexpr int F = Swz<LOG2N>::FREE;
+    if constexpr (F <= 64) return pad_add<LOG2N, C>(lb[0]);
+    else return pad_add<LOG2N, C - C % F>(lb[(C % F) / 64]) + C % F;
 }
 
 __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
@@ -146,13 +187,21 @@ __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 // One Stockham stage ST >= 1: read from buf, twiddle, DFT, write to buf.
 // Reads j + q NB (j = lane + 64 b): pad(lane) + const.  Writes o + q L with
 // o = (j - k) rad + k: pad(o) + const when 2^S divides L, else computed.
+template <int LOG2N, int ST, int B, int Q>
+__device__ __forceinline__ void stage_read_q(double2 *buf, const int (&lb)[2], double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int rad = P::radix(ST), NB = P::N / rad;
+    if constexpr (Q < rad) {
+        v[B][Q] = buf[lane_slot<LOG2N, 64 * B + Q * NB>(lb)];
+        stage_read_q<LOG2N, ST, B, Q + 1>(buf, lb, v);
+    }
+}
 template <int LOG2N, int ST, int B>
-__device__ __forceinline__ void stage_read(double2 *buf, int lb, double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+__device__ __forceinline__ void stage_read(double2 *buf, const int (&lb)[2], double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
     using P = Plan<LOG2N>;
     constexpr int rad = P::radix(ST), NB = P::N / rad, BPL = NB / 64;
     if constexpr (B < BPL) {
-#pragma unroll
-        for (int q = 0; q < rad; ++q) v[B][q] = buf[lb + (64 * B + q * NB) + ((64 * B + q * NB) >> P::S)];
+        stage_read_q<LOG2N, ST, B, 0>(buf, lb, v);
         stage_read<LOG2N, ST, B + 1>(buf, lb, v);
     }
 }
@@ -160,8 +209,8 @@ template <int LOG2N, int ST>
 __device__ __forceinline__ void stage(double2 *buf, const double2 *__restrict__ T, int lane) {
     using P = Plan<LOG2N>;
     constexpr int N = P::N, rad = P::radix(ST), L = P::L(ST);
-    constexpr int NB = N / rad, BPL = NB / 64, S = P::S, TS = N / (rad * L);
-    const int lb = pad<LOG2N>(lane);
+    constexpr int NB = N / rad, BPL = NB / 64, TS = N / (rad * L);
+    const int lb[2] = {pad<LOG2N>(lane), pad<LOG2N>(lane + 64) - 64};
     double2 v[BPL][rad];
     stage_read<LOG2N, ST, 0>(buf, lb, v);
 #pragma unroll
@@ -184,10 +233,10 @@ __device__ __forceinline__ void stage(double2 *buf, const double2 *__restrict__ 
     for (int b = 0; b < BPL; ++b) {
         const int j = lane + 64 * b, k = j & (L - 1);
         const int o = (j - k) * rad + k;
-        if constexpr ((L >> S) << S == L) {
+        if constexpr (L % Swz<LOG2N>::FREE == 0) {
             const int ob = pad<LOG2N>(o);
 #pragma unroll
-            for (int q = 0; q < rad; ++q) buf[ob + q * L + ((q * L) >> S)] = v[b][q];
+            for (int q = 0; q < rad; ++q) buf[ob + q * L + (PPF_LDS_XOR ? 0 : (q * L) >> P::S)] = v[b][q];
         } else {
 #pragma unroll
             for (int q = 0; q < rad; ++q) buf[pad<LOG2N>(o + q * L)] = v[b][q];
@@ -212,11 +261,18 @@ __device__ __forceinline__ void fft_row(double2 (&x)[Plan<LOG2N>::R], double2 *b
     constexpr int R = P::R;
     dft<R>(x);
     wave_sync();
-    // stage 0 output: o = lane R + q (L = 1, k = 0); pad(lane R + q) =
-    // pad(lane R) + q since q < R <= 2^S and 2^S is a multiple of R
+    // stage 0 output: o = lane R + q (L = 1, k = 0).  Padding: pad(lane R +
+    // q) = pad(lane R) + q (q < R <= 2^S).  XOR map: the lane's R outputs are
+    // permuted inside their block, slot = lane R + (q ^ f_lane) when R <=
+    // 2^SH, else computed per element
+#if PPF_LDS_XOR
+#pragma unroll
+    for (int q = 0; q < R; ++q) buf[pad<LOG2N>(lane * R + q)] = x[q];
+#else
     const int ob = pad<LOG2N>(lane * R);
 #pragma unroll
     for (int q = 0; q < R; ++q) buf[ob + q] = x[q];
+#endif
     wave_sync();
     stages_from<LOG2N, 1>(buf, T, lane);
 }

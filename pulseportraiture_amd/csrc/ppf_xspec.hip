@@ -43,10 +43,18 @@
 namespace ppf {
 
 constexpr int kXW = 8;                 // waves per k_align_part_w workgroup
-#ifndef PPF_XSPEC_WAVES
-#define PPF_XSPEC_WAVES 8
+// waves (= channel rows per round) per k_xspec_w workgroup: 4 at 1024-point
+// rows (two 70 KB workgroups per CU instead of one of 139 KB: a round's
+// write-out barrier holds 4 waves, not 8; C3 k_xspec_w 27.7 vs 29.2 ms),
+// 8 below (C5, 512-point rows: 29.8 vs 37.0 ms)
+template <int LOG2N>
+__host__ __device__ constexpr int xsw() {
+#ifdef PPF_XSPEC_WAVES
+    return PPF_XSPEC_WAVES;
+#else
+    return LOG2N == 10 ? 4 : 8;
 #endif
-constexpr int kXSW = PPF_XSPEC_WAVES;  // waves (= channel rows per round) per k_xspec_w workgroup
+}
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 // row elements as native vectors: arrays of HIP_vector_type structs carried
 // across the row loop are not promoted to VGPRs
@@ -101,11 +109,15 @@ __device__ __forceinline__ void rfft_pair(const double2 *buf, int k, double2 w, 
 // ===========================================================================
 // k_xspec_w: cross spectrum X of the sub-ints that stream it
 // ===========================================================================
+// wave buffer + 2 side slots; with the XOR slot map the buffers start 4
+// slots apart mod 16, which makes the eight-channel write-out of k_xspec_w
+// conflict-free (tools/lds_conflicts.py)
 template <int LOG2N>
-__host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + 2; }
+__host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + (PPF_LDS_XOR ? 4 : 2); }
 
 template <int LOG2N, int DT>
-__global__ __launch_bounds__(64 * kXSW) void k_xspec_w(XspecArgs a) {
+__global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
+    constexpr int kXSW = xsw<LOG2N>();
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
@@ -692,13 +704,13 @@ __global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan
 // ===========================================================================
 template <int L2, int DT>
 static void launch_w(const XspecArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)kXSW * xspec_slw<L2>() * sizeof(double2);
-    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kXSW);
+    const size_t lds = (size_t)xsw<L2>() * xspec_slw<L2>() * sizeof(double2);
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * xsw<L2>());
     hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
 }
 
 bool xspec_wave_supported(int log2N, int cb) {
-    return log2N >= 7 && log2N <= 10 && cb % kXSW == 0 && cb % kXW == 0;
+    return log2N >= 7 && log2N <= 10 && cb % xsw<7>() == 0 && cb % xsw<10>() == 0 && cb % kXW == 0;
 }
 
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {

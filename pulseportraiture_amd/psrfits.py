@@ -248,11 +248,13 @@ class PSRFITS(object):
         the DATA column as stored."""
         return self.subint.column_bytes("DATA")
 
-    def read_data_into(self, nbytes, dst):
+    def read_data_into(self, nbytes, dst, on_chunk=None):
         """The first nbytes of every sub-int's DATA cell, read straight from
         the file into dst (a writable uint8 array [nsub, nbytes], e.g. a
         pinned buffer) by parallel positioned reads (os.preadv releases the
-        GIL): no page faults on a memory map and no second host copy."""
+        GIL): no page faults on a memory map and no second host copy.
+        on_chunk(r0, r1) is called in row order as each chunk of rows lands
+        (load_data starts that chunk's upload while the rest is read)."""
         t = self.subint
         pos = t.columns["DATA"][0]
         fd = self._fh.fileno()
@@ -272,8 +274,10 @@ class PSRFITS(object):
         cuts = [self.nsub * i // nw for i in range(nw + 1)]
         futs = [_reader_pool().submit(rows, cuts[i], cuts[i + 1])
                 for i in range(nw)]
-        for fu in futs:
+        for i, fu in enumerate(futs):
             fu.result()
+            if on_chunk is not None and cuts[i + 1] > cuts[i]:
+                on_chunk(cuts[i], cuts[i + 1])
 
 
 _POOL = []
@@ -557,32 +561,56 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     scl, offs = f.scales_offsets()
     weights = f.weights()
     dev = engine.device(dev)
+    # the scales, offsets and weights travel with the DATA bytes: one
+    # page-locked buffer per device holds [DATA rows | DAT_SCL | DAT_OFFS |
+    # weights] (float32, 256-B aligned), so the small columns cost no
+    # separate pageable copies; load_data returns only after the uploads it
+    # fed have completed
+    nraw = -(-nsub * nbytes // 256) * 256
+    nsc = nsub * npol * nchan
+    naux = 4 * (2 * nsc + nsub * nchan)
     with torch.cuda.device(dev):
         st = _LOAD_STREAMS.get(dev.index)
         if st is None:
             st = _LOAD_STREAMS[dev.index] = torch.cuda.Stream(dev)
-        # one reusable page-locked buffer per device: load_data returns
-        # only after the upload it fed has completed
         buf = _PINNED.get(dev.index)
-        if buf is None or buf.numel() < nsub * nbytes:
+        if buf is None or buf.numel() < nraw + naux:
             buf = _PINNED[dev.index] = torch.empty(
-                max(nsub * nbytes, 1), dtype=torch.uint8, pin_memory=True)
+                max(nraw + naux, 1), dtype=torch.uint8, pin_memory=True)
         host = buf[:nsub * nbytes].view(nsub, nbytes)
-        f.read_data_into(nbytes, host.numpy())
+        aux = buf[nraw:nraw + naux].view(torch.float32)
+        a = aux.numpy()
+        a[:nsc] = scl.reshape(-1)
+        a[nsc:2 * nsc] = offs.reshape(-1)
+        a[2 * nsc:] = weights.reshape(-1)
+        dbuf = torch.empty(nraw + naux, dtype=torch.uint8, device=dev)
+        raw_d = dbuf[:nsub * nbytes].view(nsub, nbytes)
+        aux_d = dbuf[nraw:nraw + naux].view(torch.float32)
         with torch.cuda.stream(st):
-            raw_d = host.to(dev, non_blocking=True)
-            out = engine.unpack_psrfits(raw_d, elem, npol, nchan, nbin, scl,
-                                        offs, wts=weights.astype(np.float32),
-                                        pol_mode=pol_mode,
-                                        rm_baseline=rm_baseline, dev=dev)
+            aux_d.copy_(aux, non_blocking=True)
+
+            def upload(r0, r1):          # chunk r0:r1 landed: start its copy
+                with torch.cuda.stream(st):
+                    raw_d[r0:r1].copy_(host[r0:r1], non_blocking=True)
+            f.read_data_into(nbytes, host.numpy(), on_chunk=upload)
+            out = engine.unpack_psrfits(
+                raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
+                aux_d[nsc:2 * nsc], wts=aux_d[2 * nsc:], pol_mode=pol_mode,
+                rm_baseline=rm_baseline, dev=dev)
             noise = engine.noise_rows(out["rows"], dev=dev)
+            # one download: stats [nsub, nchan, 3], total [nsub, nbin],
+            # noise [nsub, nchan] (all float64)
+            packed = torch.cat([out["stats"].reshape(-1),
+                                out["total"].reshape(-1), noise.reshape(-1)])
             ev = torch.cuda.Event()
             ev.record(st)
         ev.synchronize()
-        stats = out["stats"].cpu().numpy()
-        total = out["total"].cpu().numpy()
-        noise = noise.cpu().numpy()
-    del host, raw_d
+        packed = packed.cpu().numpy()
+    n1, n2 = nsub * nchan * 3, nsub * nbin
+    stats = packed[:n1].reshape(nsub, nchan, 3)
+    total = packed[n1:n1 + n2].reshape(nsub, nbin)
+    noise = packed[n1 + n2:].reshape(nsub, nchan)
+    del host, raw_d, aux_d
     p, h = f.primary, f.subint.header
     imjd, frac = f.epochs()
     epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(imjd, frac)]

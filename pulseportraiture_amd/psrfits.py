@@ -248,13 +248,11 @@ class PSRFITS(object):
         the DATA column as stored."""
         return self.subint.column_bytes("DATA")
 
-    def read_data_into(self, nbytes, dst, on_chunk=None):
+    def read_data_into(self, nbytes, dst):
         """The first nbytes of every sub-int's DATA cell, read straight from
         the file into dst (a writable uint8 array [nsub, nbytes], e.g. a
         pinned buffer) by parallel positioned reads (os.preadv releases the
-        GIL): no page faults on a memory map and no second host copy.
-        on_chunk(r0, r1) is called in row order as each chunk of rows lands
-        (load_data starts that chunk's upload while the rest is read)."""
+        GIL): no page faults on a memory map and no second host copy."""
         t = self.subint
         pos = t.columns["DATA"][0]
         fd = self._fh.fileno()
@@ -274,10 +272,8 @@ class PSRFITS(object):
         cuts = [self.nsub * i // nw for i in range(nw + 1)]
         futs = [_reader_pool().submit(rows, cuts[i], cuts[i + 1])
                 for i in range(nw)]
-        for i, fu in enumerate(futs):
+        for fu in futs:
             fu.result()
-            if on_chunk is not None and cuts[i + 1] > cuts[i]:
-                on_chunk(cuts[i], cuts[i + 1])
 
 
 _POOL = []
@@ -589,10 +585,11 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
         with torch.cuda.stream(st):
             aux_d.copy_(aux, non_blocking=True)
 
-            def upload(r0, r1):          # chunk r0:r1 landed: start its copy
-                with torch.cuda.stream(st):
-                    raw_d[r0:r1].copy_(host[r0:r1], non_blocking=True)
-            f.read_data_into(nbytes, host.numpy(), on_chunk=upload)
+            # (starting each chunk's upload as soon as it lands, beside the
+            # reads of the rest, was measured slower end to end: 6.2-6.8k
+            # vs 7.7k TOAs/s in one call)
+            f.read_data_into(nbytes, host.numpy())
+            raw_d.copy_(host, non_blocking=True)
             out = engine.unpack_psrfits(
                 raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
                 aux_d[nsc:2 * nsc], wts=aux_d[2 * nsc:], pol_mode=pol_mode,

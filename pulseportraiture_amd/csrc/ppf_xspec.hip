@@ -39,7 +39,6 @@
 #include "ppf_internal.hpp"
 #include "ppf_state.hpp"
 #include "ppf_wfft.hpp"
-#include "ppf_wfft2.hpp"
 
 namespace ppf {
 
@@ -286,168 +285,6 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
             }
         }
         __syncthreads();
-    }
-}
-
-// ===========================================================================
-// k_xspec_p: k_xspec_w for 1024-point rows with two waves per row
-// ===========================================================================
-// A k_xspec_w wave holds a whole 1024-point row (16 KB of LDS), so at most
-// two waves per SIMD are resident and the f64 FFT's latencies show.  Here a
-// workgroup of 16 waves takes 8 channel rows per round, two waves (128 lanes,
-// ppf_wfft2.hpp) per row: 148 KB of LDS per CU, four waves per SIMD.  The
-// arithmetic per row is k_xspec_w's (noise and Sd sums reduced per wave,
-// then the two waves' partials added in wave order); the round's 8 rows are
-// written out together as before (8 channels x 16 B per harmonic).
-#ifndef PPF_XSPEC_PAIR
-#define PPF_XSPEC_PAIR 0
-#endif
-constexpr int kXPR = 8;                                  // rows per round (pairs per workgroup)
-__host__ __device__ constexpr int xspec_psl() { return wfft2::buf_slots() + 4; }
-
-__device__ __forceinline__ void rfft_pair2(const double2 *buf, int k, double2 w, double2 &Dlo,
-                                           double2 &Dhi) {
-    constexpr int N = wfft2::N;
-    const double2 zk = buf[wfft2::pad(k)];
-    const double2 zn = buf[k == 0 ? 0 : wfft2::pad(N - k)];
-    const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
-    const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
-    const double2 wo = cmul(w, o);
-    Dlo = cmk(e.x + wo.y, e.y - wo.x);
-    Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
-}
-
-template <int DT>
-__global__ __launch_bounds__(128 * kXPR) void k_xspec_p(XspecArgs a) {
-    constexpr int N = wfft2::N, NH = N + 1, R0 = wfft2::R0, P = wfft2::P;
-    constexpr int NPP = N / (2 * P);                 // (k, N-k) pairs per lane
-    constexpr int SL = xspec_psl();
-    constexpr int XNYQ = SL - 4, PSUM = SL - 3;      // X_{N/2}; the two waves' (noise, Sd) sums
-    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int pr = wave >> 1, half = wave & 1, L = tid & (P - 1);
-    double2 *buf = lds + pr * SL;
-
-    int s, cb;
-    block_map(a.xcd_swizzle, a.nblk, s, cb);
-    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
-#if PPF_TW_LDS
-    double2 *twl = lds + kXPR * SL;
-    for (int i = tid; i < N / 2; i += 128 * kXPR) twl[i] = a.T[i];
-    __syncthreads();
-    const double2 *tw = twl;
-#else
-    const double2 *tw = a.T;
-#endif
-    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
-    const int nround = (a.cb + kXPR - 1) / kXPR;
-    const int mi = a.model_index ? a.model_index[s] : 0;
-    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double sqrtN = sqrt((double)N);
-    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
-    const double2 w_seed = a.T2[L], w_step = a.T2[P];
-    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
-    int kw = NH;
-    if (a.KC) {
-        const int nn = (cbase & ~63) + lane;
-        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
-    }
-    const int mlane = (cbase + lane < cend && (!mask || mask[cbase + lane])) ? 1 : 0;
-    auto usable = [&](int n) {
-        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
-    };
-    RowT zr[R0];
-    auto fetch = [&](int n) {
-        const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
-#pragma unroll
-        for (int q = 0; q < R0; ++q) zr[q] = src[L + P * q];
-    };
-    int n = cbase + pr;
-    if (usable(n)) fetch(n);
-    for (int r = 0; r < nround; ++r, n += kXPR) {
-        const bool live = usable(n);
-        // converted unconditionally (a dead pair's values are never stored):
-        // no phi of stale registers across the round loop
-        double2 x[R0];
-#pragma unroll
-        for (int q = 0; q < R0; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-        if (!live && n < cend && half == 0 && lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
-        if (usable(n + kXPR)) fetch(n + kXPR);           // next row in flight during this FFT
-        wfft2::fft_row(x, buf, tw, L, live);
-
-        // pass 1: power sums (noise, Sd); the pair's two partials through LDS
-        double2 Dm = cmk(0.0, 0.0);
-        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + (live ? n : cbase)) * NH;
-        if (live) {
-            double pn = 0.0, pd = 0.0;
-            double2 w = w_seed;
-#pragma unroll
-            for (int i = 0; i < NPP; ++i) {
-                const int klo = L + P * i, khi = N - klo;
-                double2 Dlo, Dhi;
-                rfft_pair2(buf, klo, w, Dlo, Dhi);
-                w = cmul(w, w_step);
-                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
-                if (klo >= a.kc) pn += p0;
-                if (khi >= a.kc) pn += p1;
-                if (klo >= 1) pd += p0;
-                pd += p1;
-            }
-            if (L == 0) {
-                const double2 zm = buf[wfft2::pad(N / 2)];
-                Dm = cmk(zm.x, -zm.y);
-                const double p = cabs2(Dm);
-                if (N / 2 >= a.kc) pn += p;
-                pd += p;
-            }
-            pn = wave_sum(pn);
-            pd = wave_sum(pd);
-            if (lane == 0) buf[PSUM + half] = cmk(pn, pd);
-        }
-        __syncthreads();
-        if (live) {
-            const double2 q0 = buf[PSUM], q1 = buf[PSUM + 1];
-            const double pn = q0.x + q1.x, pd = q0.y + q1.y;
-            const int64_t crow = (int64_t)s * a.nchan + n;
-            double errs_FT;
-            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
-            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
-            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-            double2 w = w_seed;
-#pragma unroll
-            for (int i = 0; i < NPP; ++i) {
-                const int klo = L + P * i, khi = N - klo;
-                double2 Dlo, Dhi;
-                rfft_pair2(buf, klo, w, Dlo, Dhi);
-                w = cmul(w, w_step);
-                const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
-                buf[wfft2::pad(klo)] = (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
-                buf[klo == 0 ? wfft2::pad(N / 2) : wfft2::pad(khi)] = cscale(cmulc(Dhi, Mhi), inv_e2);
-            }
-            if (L == 0) {
-                buf[XNYQ] = cscale(cmulc(Dm, Mrow[N / 2]), inv_e2);
-                double *chan = a.chan + crow * 4;
-                chan[0] = errs_FT;
-                chan[1] = inv_e2;
-                chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
-            }
-        }
-        __syncthreads();
-        // write-out: thread t -> channel c = t % 8 of the round, harmonics
-        // k = t / 8 + 128 j (the next round's FFT starts with a barrier)
-        {
-            const int c = tid % kXPR, nc = cbase + r * kXPR + c;
-            if (nc < cend) {
-                const bool ok = !mask || mask[nc];
-                const double2 *b = lds + c * SL;
-                for (int k = tid / kXPR; k < kw; k += 128 * kXPR / kXPR) {   // 128 harmonics per sweep
-                    const int slot = k == N ? wfft2::pad(N / 2) : (k == N / 2 ? XNYQ : wfft2::pad(k));
-                    Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);
-                }
-            }
-        }
     }
 }
 
@@ -771,6 +608,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         XP(2);
         __syncthreads();
         XP(3);
+        mstore();                         // this round no longer reads mrow
 
         f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0;
         // folded pairs (k, N - k) with k >= KC_n hold only harmonics whose
@@ -800,12 +638,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(abase[2 * so], bv, d1, 0, 0, 0);
         }
 #endif
-        // the next round's model row into LDS (this round's post-pass was the
-        // last reader of mrow; the MFMA phase reads only the wave buffers).
-        // Here rather than before the MFMA phase: its wait for the model-row
-        // loads also waits (vmcnt counts in order) for the data row issued
-        // after them, which then stays in flight through the MFMA phase too
-        mstore();
         XP(4);
         // output element tid: this wave's sub-int, moment om = 2 j + set,
         // Re/Im ori
@@ -898,13 +730,6 @@ static void launch_w(const XspecArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
 }
 
-template <int DT>
-static void launch_p(const XspecArgs &a, hipStream_t st) {
-    const size_t lds = ((size_t)kXPR * xspec_psl() + (PPF_TW_LDS ? wfft2::N / 2 : 0)) * sizeof(double2);
-    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(128 * kXPR);
-    hipLaunchKernelGGL((k_xspec_p<DT>), g, b, lds, st, a);
-}
-
 bool xspec_wave_supported(int log2N, int cb) {
     return log2N >= 7 && log2N <= 10 && cb % xsw<7>() == 0 && cb % xsw<10>() == 0 && cb % kXW == 0;
 }
@@ -917,13 +742,8 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {
         case 17: launch_w<8, 1>(a, st); break;
         case 18: launch_w<9, 0>(a, st); break;
         case 19: launch_w<9, 1>(a, st); break;
-#if PPF_XSPEC_PAIR
-        case 20: launch_p<0>(a, st); break;
-        case 21: launch_p<1>(a, st); break;
-#else
         case 20: launch_w<10, 0>(a, st); break;
         case 21: launch_w<10, 1>(a, st); break;
-#endif
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

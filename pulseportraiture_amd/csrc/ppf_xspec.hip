@@ -136,6 +136,17 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
     constexpr int SL = xspec_slw<LOG2N>();           // padded wave buffer + 2 side slots
     constexpr int XNYQ = SL - 2;                      // X_{N/2} of the row
+    // model pairs loaded ahead in pass 2: at 1024 points the 4-wave
+    // workgroups leave VGPRs to spare (LDS caps them at two waves per SIMD);
+    // at 512 points k_xspec_w runs four waves per SIMD at <= 128 VGPRs
+#ifndef PPF_XS_MPRE9
+#define PPF_XS_MPRE9 0
+#endif
+#ifdef PPF_XS_MPRE
+    constexpr int MD = PPF_XS_MPRE;
+#else
+    constexpr int MD = LOG2N == 10 ? 4 : (LOG2N == 9 ? PPF_XS_MPRE9 : 0);
+#endif
     using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -205,6 +216,15 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
             if (nxt) fetch(n + kXSW);                   // next row in flight during this FFT
             wfft::fft_row<LOG2N>(x, buf, tw, lane);
 
+            // the model pairs of pass 2's first MD iterations, loaded now (the
+            // FFT is done, so their wait no longer holds up anything): each
+            // pass-2 iteration otherwise waited for its own two L2 loads
+            double2 Mq[MD > 0 ? MD : 1][2];
+#pragma unroll
+            for (int i = 0; i < MD; ++i) {
+                Mq[i][0] = Mrow[lane + 64 * i];
+                Mq[i][1] = Mrow[N - lane - 64 * i];
+            }
             // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
             double pn = 0.0, pd = 0.0;
             {
@@ -251,7 +271,18 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
                     // (loading these before the next row's prefetch, so their
                     // in-order wait skips it, was measured: the extra
                     // registers cost occupancy, C5 29.7 -> 33.2 ms)
-                    const double2 Mlo = Mrow[klo], Mhi = Mrow[khi];
+                    double2 Mlo, Mhi;
+                    if constexpr (MD > 0) {
+                        Mlo = Mq[i % MD][0];
+                        Mhi = Mq[i % MD][1];
+                        if (i + MD < NP) {
+                            Mq[i % MD][0] = Mrow[klo + 64 * MD];
+                            Mq[i % MD][1] = Mrow[khi - 64 * MD];
+                        }
+                    } else {
+                        Mlo = Mrow[klo];
+                        Mhi = Mrow[khi];
+                    }
                     buf[wfft::pad<LOG2N>(klo)] =
                         (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
                     buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =

@@ -36,6 +36,7 @@ PSRFITS fixture):
 """
 import mmap
 import os
+import threading
 
 import numpy as np
 
@@ -507,8 +508,9 @@ class _Masks(object):
         return self._full()[idx]
 
 
-_LOAD_STREAMS = {}
-_PINNED = {}
+# per loading thread and device: a copy stream and a reusable page-locked
+# buffer (get_TOAs runs two load_data calls at once on its loader threads)
+_TLS = threading.local()
 
 
 def load_data(filename, state=None, dedisperse=False, dededisperse=False,
@@ -565,13 +567,15 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     nraw = -(-nsub * nbytes // 256) * 256
     nsc = nsub * npol * nchan
     naux = 4 * (2 * nsc + nsub * nchan)
+    if not hasattr(_TLS, "streams"):
+        _TLS.streams, _TLS.pinned = {}, {}
     with torch.cuda.device(dev):
-        st = _LOAD_STREAMS.get(dev.index)
+        st = _TLS.streams.get(dev.index)
         if st is None:
-            st = _LOAD_STREAMS[dev.index] = torch.cuda.Stream(dev)
-        buf = _PINNED.get(dev.index)
+            st = _TLS.streams[dev.index] = torch.cuda.Stream(dev)
+        buf = _TLS.pinned.get(dev.index)
         if buf is None or buf.numel() < nraw + naux:
-            buf = _PINNED[dev.index] = torch.empty(
+            buf = _TLS.pinned[dev.index] = torch.empty(
                 max(nraw + naux, 1), dtype=torch.uint8, pin_memory=True)
         host = buf[:nsub * nbytes].view(nsub, nbytes)
         aux = buf[nraw:nraw + naux].view(torch.float32)

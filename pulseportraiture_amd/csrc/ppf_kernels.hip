@@ -404,12 +404,30 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
     }
     const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
     const VecT *rows = reinterpret_cast<const VecT *>(a.data) + (int64_t)s * a.nchan * (NB / VW);
+    // the block's channel scalars in lane registers (channel c0 + lane + 64 k,
+    // cbd <= 128), broadcast by readlane: a global load of the weight or the
+    // frequency after the next row's prefetch would wait for that prefetch
+    // (vmcnt counts in order), i.e. only one row would be in flight
+    double t_w[2], t_f[2];
+    int t_m[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int ch = c0 + lane + 64 * k;
+        const bool in = ch < c1;
+        t_w[k] = in ? gwt[ch] : 0.0;
+        t_f[k] = in ? fr[ch] : 1.0;
+        t_m[k] = (in && (!mask || mask[ch])) ? 1 : 0;
+    }
+    auto usable = [&](int n) {
+        const int r = n - c0;
+        return n < c1 && __builtin_amdgcn_readlane(r < 64 ? t_m[0] : t_m[1], r & 63) != 0;
+    };
     double acc[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = 0.0;
     double wsum = 0.0, wcnt = 0.0;
     int n = c0 + wave;
-    while (n < c1 && mask && !mask[n]) n += kWaves;
+    while (n < c1 && !usable(n)) n += kWaves;
     VecT pre[NL];
     {
         const VecT *src = rows + (int64_t)min(n, c1 - 1) * (NB / VW);
@@ -421,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
 #pragma unroll
         for (int i = 0; i < NL; ++i) reinterpret_cast<VecT *>(xs)[lane + 64 * i] = pre[i];
         int nn = n + kWaves;
-        while (nn < c1 && mask && !mask[nn]) nn += kWaves;
+        while (nn < c1 && !usable(nn)) nn += kWaves;
         {
             // next row in flight during this one (unconditional load: keeps
             // pre[] in VGPRs)
@@ -429,7 +447,9 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
 #pragma unroll
             for (int i = 0; i < NL; ++i) pre[i] = src[lane + 64 * i];
         }
-        const double w = gwt[n], f0 = fr[n];
+        const int r = n - c0;
+        const double w = readlane_d(r < 64 ? t_w[0] : t_w[1], r & 63),
+                     f0 = readlane_d(r < 64 ? t_f[0] : t_f[1], r & 63);
         const double tau = Dg * (1.0 / (f0 * f0) - nu_mean_m2);
         const double fl = floor(tau), f = tau - fl;
         const int i0 = (int)(fl - (double)NB * floor(fl / (double)NB));   // mod nbin

@@ -137,10 +137,12 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
     constexpr int SL = xspec_slw<LOG2N>();           // padded wave buffer + 2 side slots
     constexpr int XNYQ = SL - 2;                      // X_{N/2} of the row
     // model pairs loaded ahead in pass 2: at 1024 points the 4-wave
-    // workgroups leave VGPRs to spare (LDS caps them at two waves per SIMD);
-    // at 512 points k_xspec_w runs four waves per SIMD at <= 128 VGPRs
+    // workgroups leave VGPRs to spare (LDS caps them at two waves per SIMD:
+    // 4 ahead, C3 27.1 -> 25.5 ms); at 512 points k_xspec_w runs four waves
+    // per SIMD at <= 128 VGPRs, which one pair ahead keeps (126; C5 29.2 ->
+    // 28.6 ms), two would not (132)
 #ifndef PPF_XS_MPRE9
-#define PPF_XS_MPRE9 0
+#define PPF_XS_MPRE9 1
 #endif
 #ifdef PPF_XS_MPRE
     constexpr int MD = PPF_XS_MPRE;
@@ -372,18 +374,6 @@ __device__ unsigned long long g_xprof[8];
 #endif
 __device__ __forceinline__ double bin_centre(double phc, int nbin) {
     return rint(phc * (double)nbin);
-}
-__device__ __forceinline__ double readfirst_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)b);
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 template <int LOG2N>
 __host__ __device__ constexpr size_t xmom_g_lds() {

@@ -355,7 +355,15 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ppf::XspecArgs xa{};
     xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = ilog2(d->nbin / 2);
     xa.kc = kc; xa.nblk = L.nblk; xa.cb = L.cb; xa.dtype = d->data_dtype;
-    xa.xcd_swizzle = (L.nblk % 8 == 0) ? 1 : 0;
+    // k_xspec_w: channel-block-major (mode 2) when the model spectra
+    // outgrow the L2s, sub-int-major otherwise; k_xmom_g stages its model
+    // row in LDS per workgroup and keeps mode 1
+#ifndef PPF_XSPEC_ORDER2_BYTES
+#define PPF_XSPEC_ORDER2_BYTES (32ll << 20)
+#endif
+    const long long model_bytes = (long long)d->nchan * (d->nbin / 2 + 1) * 16;
+    const int xcd1 = (L.nblk % 8 == 0) ? 1 : 0;
+    xa.xcd_swizzle = (xcd1 && model_bytes > PPF_XSPEC_ORDER2_BYTES) ? 2 : xcd1;
     xa.data = d->data; xa.Mft = Mft; xa.model_index = d->model_index; xa.mask = d->chan_mask;
     xa.errs = d->errs; xa.freqs = d->freqs; xa.P = d->P; xa.T = T; xa.T2 = T2;
     xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);
@@ -452,7 +460,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     const bool any_mom = ctx->host_active[1] != 0, any_pass = ctx->host_active[2] != 0;
     ppf::XmomArgs ma{};
     ma.nsub = d->nsub; ma.nchan = d->nchan; ma.nbin = d->nbin; ma.log2N = xa.log2N;
-    ma.nblk = L.nblk; ma.cb = L.cb; ma.dtype = d->data_dtype; ma.xcd_swizzle = xa.xcd_swizzle;
+    ma.nblk = L.nblk; ma.cb = L.cb; ma.dtype = d->data_dtype; ma.xcd_swizzle = xcd1;
     ma.data = d->data; ma.Mft = Mft; ma.model_index = d->model_index; ma.mask = d->chan_mask;
     ma.chan = xa.chan; ma.dphi = sa.dphi; ma.T = T; ma.T2 = T2; ma.state = sa.state;
     ma.mom = (double *)sa.mom;

@@ -79,9 +79,17 @@ typedef float vf4 __attribute__((ext_vector_type(4)));
 #endif
 
 // XCD-aware block -> (sub-int, channel block): blocks b and b+8 share an
-// XCD, so each XCD keeps only its channel blocks' model rows in its L2
-__device__ __forceinline__ void block_map(int xcd_swizzle, int nblk, int &s, int &cb) {
-    if (xcd_swizzle) {
+// XCD, so each XCD keeps only its channel blocks' model rows in its L2.
+// Mode 1 walks an XCD's channel blocks sub-int by sub-int (a model larger
+// than the L2s is then re-read for every sub-int: 134 MB per C5 sub-int);
+// mode 2 walks every sub-int (of nsub) for one channel block before the next,
+// so the workgroups resident on an XCD share one block of model rows.
+__device__ __forceinline__ void block_map(int xcd_swizzle, int nblk, int &s, int &cb, int nsub = 0) {
+    if (xcd_swizzle == 2) {
+        const int per = nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
+        cb = x * per + r / nsub;
+        s = r % nsub;
+    } else if (xcd_swizzle) {
         const int per = nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
         cb = x * per + r % per;
         s = r / per;
@@ -155,7 +163,7 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
     double2 *buf = lds + wave * SL;
 
     int s, cb;
-    block_map(a.xcd_swizzle, a.nblk, s, cb);
+    block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
     if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
 #if PPF_TW_LDS
     double2 *twl = lds + kXSW * SL;

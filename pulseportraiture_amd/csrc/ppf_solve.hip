@@ -841,12 +841,21 @@ __device__ int tr_update(TRState &S, const double *o, int max_iter) {
 template <bool BOX>
 __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     __shared__ double thb[kWaves][8];
+    // the trust-region update runs on lane 0 against an LDS copy of the
+    // sub-int's state: on the global TRState every one of its serial field
+    // accesses was a dependent L2 round trip (~170 us per launch at C5)
+    __shared__ TRState Ls[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int s = blockIdx.x * kWaves + wave;
     if (s >= a.nsub) return;
-    TRState &S = a.state[s];
-    const int phase = S.phase;
-    if (phase == PH_DONE || S.mmode) return;
+    TRState &G = a.state[s];
+    const int phase = G.phase;
+    if (phase == PH_DONE || G.mmode) return;
+    static_assert(sizeof(TRState) % 8 == 0, "TRState copy");
+    constexpr int NW = (int)(sizeof(TRState) / 8);
+    TRState &S = Ls[wave];
+    for (int i = lane; i < NW; i += 64)
+        reinterpret_cast<double *>(&S)[i] = reinterpret_cast<const double *>(&G)[i];
     const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
     double o[21];
 #pragma unroll
@@ -858,6 +867,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 21; ++i) o[i] = wave_sum(o[i]);
+    wave_lds_sync();                                   // every lane's copy of the state has landed
     int cmd = 0;
     if (lane == 0) {
         cmd = S.newton ? tr_update_newton_n<5>(S, o, a.max_iter) : tr_update<5, BOX>(S, o, a.max_iter);
@@ -865,19 +875,22 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
         thb[wave][5] = (double)cmd;
     }
     cmd = __shfl(cmd, 0, 64);
-    if (!cmd) return;
-    if (lane == 0) atomicAdd(a.active, 1u);
-    if (S.scat) {
-        // reference gates at the proposal (taus.sum(), dtau.sum(), dalpha.sum())
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const double t3 = __shfl(lane == 0 ? S.th[3] : 0.0, 0, 64);
-        const double t4 = __shfl(lane == 0 ? S.th[4] : 0.0, 0, 64);
-        const double tl = a.log10_tau ? pow(10.0, t3) : t3;
-        int gs, gt, ga;
-        wave_gates(a.dphi + (int64_t)s * a.nchan * 2, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
-                   a.nchan, tl, t4, a.log10_tau, gs, gt, ga);
-        if (lane == 0) { S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga; }
+    if (cmd) {
+        if (lane == 0) atomicAdd(a.active, 1u);
+        if (S.scat) {
+            // reference gates at the proposal (taus.sum(), dtau.sum(), dalpha.sum())
+            const double t3 = __shfl(lane == 0 ? S.th[3] : 0.0, 0, 64);
+            const double t4 = __shfl(lane == 0 ? S.th[4] : 0.0, 0, 64);
+            const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+            int gs, gt, ga;
+            wave_gates(a.dphi + (int64_t)s * a.nchan * 2, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
+                       a.nchan, tl, t4, a.log10_tau, gs, gt, ga);
+            if (lane == 0) { S.g_sum = gs; S.g_tau = gt; S.g_alpha = ga; }
+        }
     }
+    wave_lds_sync();                                   // lane 0's updates are visible to the wave
+    for (int i = lane; i < NW; i += 64)
+        reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&S)[i];
 }
 
 // ===========================================================================

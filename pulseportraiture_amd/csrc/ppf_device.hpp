@@ -2,10 +2,12 @@
 //
 // Complex fp64 helpers, wave64/workgroup reductions, an LDS-resident Stockham
 // radix-4/2 FFT shared by every FFT-using kernel, the real<->half-length
-// complex FFT packing, the scipy trust-ncg replica used by the solver and a
+// complex FFT packing, the scipy trust-ncg replica and the exact trust-region
+// subproblem (Jacobi eigendecomposition and the secular equation) of the
+// Newton solver, and a
 // companion-matrix polynomial root finder (np.roots replacement for the
-// zero-covariance GM cases).  Everything is fp64: nothing on this path is a
-// dense contraction, so there is no MFMA.
+// zero-covariance GM cases).  Everything is fp64; the one dense contraction
+// on the path (the Taylor moments of k_xmom_g, ppf_xspec.hip) is f64 MFMA.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -107,9 +109,6 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 #endif
 
-// wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
-// operations are processed in issue order; this keeps the compiler from
-// moving them across the exchange point)
 // wave-uniform copies of a double held by the first / a given lane
 __device__ __forceinline__ double readfirst_d(double v) {
     const long long b = __double_as_longlong(v);
@@ -124,6 +123,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// wave-scope ordering of LDS traffic (no hardware barrier: a wave's LDS
+// operations are processed in issue order; this keeps the compiler from
+// moving them across the exchange point)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -342,7 +342,10 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
 constexpr int kPassChans = kBlock;             // channels per workgroup
 
 #ifndef PPF_PASS_WPE
-#define PPF_PASS_WPE 2
+#define PPF_PASS_WPE 3
+#endif
+#ifndef PPF_PASS_SPLIT
+#define PPF_PASS_SPLIT 1
 #endif
 template <bool SCAT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS_WPE))) void k_pass(SolveArgs a) {
@@ -389,28 +392,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
     double acc[21];
 #pragma unroll
     for (int i = 0; i < 21; ++i) acc[i] = 0.0;
-    const int n = blk * kPassChans + threadIdx.x;
-    // Newton warm start: only every S.sub-th group of 64 channels (a wave)
+    // Newton warm start: only every S.sub-th group of 64 channels (a wave).
+    // With a stride of four groups or more a workgroup holds at most one such
+    // group, its first; then all four waves take that group's 64 channels and
+    // split its harmonics (split: workgroup-uniform), so a subset pass is not
+    // one wave's serial harmonic loop per 256 channels while the other three
+    // idle (C5: 16 of 256 groups per sub-int)
+    const bool split = PPF_PASS_SPLIT && S.sub >= kWaves;
+    const int n = blk * kPassChans + (split ? lane : (int)threadIdx.x);
     const bool in_sub = S.sub <= 1 || ((n >> 6) % S.sub) == 0;
     const bool use_n = in_sub && n < a.nchan && (!mask || mask[n]);
     // harmonics the wave sums: up to the largest cutoff of its channels
-    // (k_model_cut; wave-uniform so the loads stay coalesced)
+    // (k_model_cut; wave-uniform so the loads stay coalesced); split: the
+    // wave's quarter of them, in whole 64-harmonic phasor-seed spans
     const int kend = (int)wave_max(use_n ? (double)a.KC[(int64_t)mi * a.nchan + n] : 1.0);
+    int kb0 = 0, kb1 = kend;
+    if (split) {
+        const int Q = ((kend + 64 * kWaves - 1) / (64 * kWaves)) * 64;
+        kb0 = min(kend, wave * Q);
+        kb1 = min(kend, kb0 + Q);
+    }
+    double nu = 0.0, aa = 0.0, inv_e2 = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    double q1 = 0.0, q1p = 0.0, q2 = 0.0, s0 = 0.0, t1 = 0.0, t2 = 0.0;
     if (use_n) {
-        const double nu = fr[n];
+        nu = fr[n];
         const double phin = th[0] + kDconst * th[1] * (pow(nu, -2.0) - nuDM2) / g.P +
                             kDconst * kDconst * th[2] * (pow(nu, -4.0) - nuGM4) / g.P;
         const double2 W = cexp2pi(phin);
         const double2 *Xc = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * nharm * a.nchan + n;
         const double *Pc = a.MP + (int64_t)mi * nharm * a.nchan + n;
         const int64_t xs = a.nchan;
-        double aa = 0.0, inv_e2 = 0.0;
         if (SCAT) {
             aa = kTwoPi * tau_lin * pow(nu / g.nu_tau, alpha);
             inv_e2 = chan[n * 4 + 1];
         }
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-        double q1 = 0.0, q1p = 0.0, q2 = 0.0, s0 = 0.0, t1 = 0.0, t2 = 0.0;
         // Scattering terms in closed form (pptoaslib.py:344-455 restated):
         // with u = 2 pi k tau_n, d = 1 / (1 + u^2), w = conj(B) = d (1 + iu),
         //   B - 1 = -iu B, so dB ~ B (B - 1) = -iu B^2, d2B ~ -u^2 B^3 and
@@ -449,7 +465,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
                 const double kk = (double)(kb + u);
-                const bool in = kb + u < kend;
+                const bool in = kb + u < kb1;
                 const double2 y = in ? cmul(xv[u], E) : cmk(0.0, 0.0);
                 if (!SCAT) {
                     a0 += y.x;
@@ -482,15 +498,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
                 E = cmul(E, W);
             }
         };
-        ldg(0, xa, pa);
+        ldg(kb0, xa, pa);
         // (no early exit: a trailing group may sum zeros, which keeps one
         // straight-line body and its load/wait schedule)
-        for (int kb = 0; kb < kend; kb += 2 * KB) {
+        for (int kb = kb0; kb < kb1; kb += 2 * KB) {
             ldg(kb + KB, xb, pb);
             sum_group(kb, xa, pa);
             ldg(kb + 2 * KB, xa, pa);
             sum_group(kb + KB, xb, pb);
         }
+    }
+    if (split) {
+        // the four waves' partial sums of the same 64 channels, added in wave
+        // order (fixed: bitwise reproducible)
+        __shared__ double sp[kWaves - 1][9][64];
+        if (wave > 0) {
+            double *o = &sp[wave - 1][0][lane];
+            o[0] = a0; o[64] = a1; o[128] = a2; o[192] = q1; o[256] = q1p;
+            o[320] = q2; o[384] = s0; o[448] = t1; o[512] = t2;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            for (int w = 0; w < kWaves - 1; ++w) {
+                const double *o = &sp[w][0][lane];
+                a0 += o[0]; a1 += o[64]; a2 += o[128]; q1 += o[192]; q1p += o[256];
+                q2 += o[320]; s0 += o[384]; t1 += o[448]; t2 += o[512];
+            }
+        }
+    }
+    if (use_n && (!split || wave == 0)) {
         double my[10];
         my[0] = a0; my[1] = -kTwoPi * a1; my[2] = -kTwoPi * kTwoPi * a2;
         if (SCAT) {

@@ -133,45 +133,38 @@ struct Plan {
 // 2.25 to 0.75 per ds_*_b128 (the padding moves lanes 16-31 of a
 // ds_read_b128 group one slot onto lanes 0-15's banks) and makes the
 // eight-channel write-out of k_xspec_w conflict-free.  Measured on MI355X
-// (89 GPU tests green with it): C2 and C3 unchanged (k_xmom_g, k_xspec_w are
-// f64-issue bound, not LDS bound), C5 7% slower (k_xspec_w<9> needs 136
+// (89 GPU tests green with it): C3 unchanged, k_xmom_g 3% slower (31.8 vs
+// 30.8 ms; the kernels are f64-issue bound, not LDS bound), C5 7% slower (k_xspec_w<9> needs 136
 // VGPRs instead of 124: three waves per SIMD instead of four).  Kept off.
 #ifndef PPF_LDS_XOR
 #define PPF_LDS_XOR 0
 #endif
 template <int LOG2N>
+__host__ __device__ constexpr bool use_xor() { return PPF_LDS_XOR != 0; }
+template <int LOG2N>
 struct Swz {
     static constexpr int SH = LOG2N == 7 ? 2 : (LOG2N == 10 ? 4 : 3);
     static constexpr int MK = LOG2N == 7 ? 3 : 7;
     // offsets that are multiples of FREE commute with the map
-    static constexpr int FREE = PPF_LDS_XOR ? (MK + 1) << SH : 1 << Plan<LOG2N>::S;
+    static constexpr int FREE = use_xor<LOG2N>() ? (MK + 1) << SH : 1 << Plan<LOG2N>::S;
 };
 template <int LOG2N>
 __device__ __forceinline__ constexpr int pad(int idx) {
-#if PPF_LDS_XOR
-    return idx ^ ((idx >> Swz<LOG2N>::SH) & Swz<LOG2N>::MK);
-#else
-    return idx + (idx >> Plan<LOG2N>::S);
-#endif
+    if constexpr (use_xor<LOG2N>()) return idx ^ ((idx >> Swz<LOG2N>::SH) & Swz<LOG2N>::MK);
+    else return idx + (idx >> Plan<LOG2N>::S);
 }
 // pad(a + C) given pad(a), for a compile-time C that is a multiple of FREE
 template <int LOG2N, int C>
 __device__ __forceinline__ int pad_add(int pa) {
     static_assert(C % Swz<LOG2N>::FREE == 0, "offset must commute with the slot map");
-#if PPF_LDS_XOR
-    return pa + C;
-#else
-    return pa + C + (C >> Plan<LOG2N>::S);
-#endif
+    if constexpr (use_xor<LOG2N>()) return pa + C;
+    else return pa + C + (C >> Plan<LOG2N>::S);
 }
 // LDS slots of one wave buffer
 template <int LOG2N>
 __host__ __device__ constexpr int buf_slots() {
-#if PPF_LDS_XOR
-    return Plan<LOG2N>::N;
-#else
-    return Plan<LOG2N>::N + (Plan<LOG2N>::N >> Plan<LOG2N>::S);
-#endif
+    if constexpr (use_xor<LOG2N>()) return Plan<LOG2N>::N;
+    else return Plan<LOG2N>::N + (Plan<LOG2N>::N >> Plan<LOG2N>::S);
 }
 // slot of element lane + C, C a compile-time multiple of 64: one of two
 // lane bases (lb[0] = pad(lane), lb[1] = pad(lane + 64) - 64) plus a constant
@@ -217,7 +210,9 @@ __device__ __forceinline__ void stage(double2 *buf, const double2 *__restrict__ 
     for (int b = 0; b < BPL; ++b) {
         const int j = lane + 64 * b, k = j & (L - 1);
         // twiddles w^q, w = exp(-2 pi i k / (rad L)) = T[k N / (rad L)], by
-        // recurrence from one table read (no rad-1 twiddles live at once)
+        // recurrence from one table read (no rad-1 twiddles live at once;
+        // every power read from a table instead, k_xmom_g at 1024 points:
+        // 34.6 vs 30.8 ms)
         const double2 w1 = T[k * TS];
         double2 wq = w1;
         v[b][1] = cmul(v[b][1], w1);
@@ -236,7 +231,7 @@ __device__ __forceinline__ void stage(double2 *buf, const double2 *__restrict__ 
         if constexpr (L % Swz<LOG2N>::FREE == 0) {
             const int ob = pad<LOG2N>(o);
 #pragma unroll
-            for (int q = 0; q < rad; ++q) buf[ob + q * L + (PPF_LDS_XOR ? 0 : (q * L) >> P::S)] = v[b][q];
+            for (int q = 0; q < rad; ++q) buf[ob + q * L + (use_xor<LOG2N>() ? 0 : (q * L) >> P::S)] = v[b][q];
         } else {
 #pragma unroll
             for (int q = 0; q < rad; ++q) buf[pad<LOG2N>(o + q * L)] = v[b][q];
@@ -265,14 +260,14 @@ __device__ __forceinline__ void fft_row(double2 (&x)[Plan<LOG2N>::R], double2 *b
     // q) = pad(lane R) + q (q < R <= 2^S).  XOR map: the lane's R outputs are
     // permuted inside their block, slot = lane R + (q ^ f_lane) when R <=
     // 2^SH, else computed per element
-#if PPF_LDS_XOR
+    if constexpr (use_xor<LOG2N>()) {
 #pragma unroll
-    for (int q = 0; q < R; ++q) buf[pad<LOG2N>(lane * R + q)] = x[q];
-#else
-    const int ob = pad<LOG2N>(lane * R);
+        for (int q = 0; q < R; ++q) buf[pad<LOG2N>(lane * R + q)] = x[q];
+    } else {
+        const int ob = pad<LOG2N>(lane * R);
 #pragma unroll
-    for (int q = 0; q < R; ++q) buf[ob + q] = x[q];
-#endif
+        for (int q = 0; q < R; ++q) buf[ob + q] = x[q];
+    }
     wave_sync();
     stages_from<LOG2N, 1>(buf, T, lane);
 }

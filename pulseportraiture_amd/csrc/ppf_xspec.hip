@@ -134,7 +134,7 @@ __host__ __device__ constexpr int tw_slots() {
 #define PPF_TW_LDS 1
 #endif
 template <int LOG2N>
-__host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + (PPF_LDS_XOR ? 4 : 2); }
+__host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + (wfft::use_xor<LOG2N>() ? 4 : 2); }
 
 template <int LOG2N, int DT>
 __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {

@@ -275,8 +275,7 @@ def bench_align(args):
         engine.align_accum(R.data[:, 0], ph, w, out, wsum, dev=dev)
         if comm:
             dist.allreduce_sum_(out, wsum)
-        good = wsum > 0
-        out[good] /= wsum[good][:, None]
+        out /= torch.where(wsum > 0, wsum, torch.ones_like(wsum))[:, None]   # as ppalign
         return out                      # the next template stays in HBM
 
     m = model0

@@ -270,12 +270,18 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     phi = r[:, I["params"]][:, 0]
     DM = r[:, I["params"]][:, 1]
     nu_ref = r[:, I["nu_out"]][:, 0]
-    ok = dc["mask"] != 0
+    # the iteration-invariant factors once per batch of rows (each torch op
+    # is a launch and a Python round trip in every ppalign iteration)
+    if "ok" not in dc:
+        dc["ok"] = dc["mask"] != 0
+        dc["f2"] = dc["freqs"] ** -2.0
+        dc["e2"] = dc["errs"] ** 2
+        dc["zero"] = torch.zeros((), dtype=torch.float64, device=dev)
+    ok, zero = dc["ok"], dc["zero"]
     ph = phi[:, None] + (Dconst * DM / dc["P"])[:, None] * (
-        dc["freqs"] ** -2.0 - (nu_ref ** -2.0)[:, None])
-    zero = torch.zeros((), dtype=torch.float64, device=dev)
+        dc["f2"] - (nu_ref ** -2.0)[:, None])
     ph = torch.where(ok, ph, zero)
-    wt = torch.where(ok, res["scales"] / dc["errs"] ** 2, zero)
+    wt = torch.where(ok, res["scales"] / dc["e2"], zero)
     return ph, wt
 
 
@@ -424,8 +430,10 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
             # all-reduce: agree on success first
             _dist.raise_if_any_failed(err, dev)
             _dist.allreduce_sum_(out, wsum)
-        good = wsum > 0
-        out[:, good] /= wsum[good][None, :, None]
+        # channels with weight: divided by it; the rest (all zero) by 1 --
+        # the same values as out[:, good] /= wsum[good], without the boolean
+        # indexing's device-to-host round trip in every iteration
+        out /= torch.where(wsum > 0, wsum, torch.ones_like(wsum))[None, :, None]
         model_port = out[0]             # the next template stays in HBM
         niter -= 1
         count += 1

@@ -273,6 +273,7 @@ def bench_align(args):
         wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
         ph, w = ppalign._fit_and_weights(R, model_port, True, nbin, dev)
         engine.align_accum(R.data[:, 0], ph, w, out, wsum, dev=dev)
+        ppalign.raise_pending(R)
         if comm:
             dist.allreduce_sum_(out, wsum)
         out /= torch.where(wsum > 0, wsum, torch.ones_like(wsum))[:, None]   # as ppalign

@@ -252,21 +252,23 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     """One batched ppf_fit_batch of `rows` (guess + phase[/DM] fit), the
     reference's exceptions raised for failed sub-ints."""
     flags = [1, int(bool(fit_dm)), 0, 0, 0]
+    # no scattering and a zero initial tau (init holds only the DM): no
+    # sub-int streams the cross spectrum -- known on the host, so fit_batch
+    # need not read the device-resident init back to count them
     res = engine.fit_batch(
         rows, model, dc["freqs"], dc["P"], dc["init"], flags,
         nu_fits=dc["nu_fits"], nu_outs=dc["nu_outs"], errs=dc["errs"],
         chan_mask=dc["mask"], model_index=mi, log10_tau=False, is_toa=True,
         guess=True, guess_weights=dc["gw"], guess_DM=dc["DM"],
-        guess_Ns=nbin, dev=dev, guess_ref=1)   # ppalign.py:214-219: at nu_fit
+        guess_Ns=nbin, dev=dev, guess_ref=1,   # ppalign.py:214-219: at nu_fit
+        n_x=0)
     I = _lib.RESULT_INDEX
     r = res["results"]
     dc["last_results"] = r               # (diagnostics: bench.py --fit align)
-    st = r[:, I["status"]].to(torch.int64).cpu().numpy()
-    bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR |
-                         _lib.ST_NOSPACE))[0]
-    if len(bad):
-        from .pplib import _raise_status
-        _raise_status(int(st[bad[0]]))
+    # the status bits are checked by raise_pending() once the iteration's
+    # rotate-and-sum is queued (the read-back is the iteration's one host
+    # sync; here it would idle the device while the host queued the rest)
+    dc.setdefault("_pending", []).append(r[:, I["status"]].to(torch.int64))
     phi = r[:, I["params"]][:, 0]
     DM = r[:, I["params"]][:, 1]
     nu_ref = r[:, I["nu_out"]][:, 0]
@@ -283,6 +285,23 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     ph = torch.where(ok, ph, zero)
     wt = torch.where(ok, res["scales"] / dc["e2"], zero)
     return ph, wt
+
+
+def raise_pending(R):
+    """The reference's exceptions for the failed rows of the iteration's
+    fits (pptoaslib.py:1068-1079): reads back the status bits _fit_rows
+    queued, after the caller has queued the work that uses the fits."""
+    from .pplib import _raise_status
+    for dc in (R.__dict__.get("_dev_inputs"), getattr(R, "_dup_dev", None)):
+        if not dc or not dc.get("_pending"):
+            continue
+        sts, dc["_pending"] = dc["_pending"], []
+        for st in sts:
+            st = st.cpu().numpy()
+            bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR |
+                                 _lib.ST_NOSPACE))[0]
+            if len(bad):
+                _raise_status(int(st[bad[0]]))
 
 
 def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
@@ -421,6 +440,7 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
                     engine.align_accum(R.data[:, ipol], phases, weights,
                                        out[ipol], wsum if ipol == 0 else w,
                                        dev=dev)
+                raise_pending(R)
         except Exception as exc:        # raised on every rank, below
             if not comm:
                 raise

@@ -70,6 +70,10 @@ def parse():
                     "PSRFITS files (16-bit DATA + DAT_SCL/DAT_OFFS, one "
                     "polarisation) and read through the PSRCHIVE-free fast "
                     "path (raw bytes to the device, unpacked there)")
+    ap.add_argument("--timeline", default=None,
+                    help="--fit gettoas: write the host timeline of the "
+                    "last timed step (pulseportraiture_amd.timeline spans, "
+                    "per stage and thread) to this JSON file")
     ap.add_argument("--zap-frac", type=float, default=0.0,
                     help="fraction of channels masked (zapped) in every "
                     "sub-int, as GetTOAs passes its ok_ichans (default 0)")
@@ -81,6 +85,10 @@ def parse():
                     help="sum every harmonic (PPF_OPT_NO_HCUT: no per-channel "
                     "cutoff of harmonics below 1e-28 of the template's peak "
                     "power)")
+    ap.add_argument("--mom-x", action="store_true",
+                    help="phase/DM fits take their Taylor moments from the "
+                    "stored cross spectrum (k_xspec_w + k_moments, "
+                    "PPF_OPT_MOM_X) instead of the fused k_xmom_g pass")
     ap.add_argument("--solver", default="newton", choices=["newton", "scipy"],
                     help="minimiser of the scattering fits (--fit full/scat): "
                     "the Newton trust region (default) or scipy trust-ncg's "
@@ -455,12 +463,39 @@ def bench_gettoas(args):
         step()
     torch.cuda.synchronize(dev)
     dist.barrier()
+    from pulseportraiture_amd import timeline
+    if args.timeline:
+        timeline.ENABLED = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        timeline.dump()
+        ts = time.perf_counter()
         gt = step()
     torch.cuda.synchronize(dev)
+    te = time.perf_counter()
     dist.barrier()
     dt = dist.max_over_ranks(time.perf_counter() - t0, dev)
+    if args.timeline and rank == 0:
+        spans = timeline.dump()
+        summ = {}
+        for name, th, a, b in spans:
+            e = summ.setdefault(name, dict(count=0, total_ms=0.0, threads=[]))
+            e["count"] += 1
+            e["total_ms"] += (b - a) * 1e3
+            if th not in e["threads"]:
+                e["threads"].append(th)
+        busy = {}
+        for name, th, a, b in spans:
+            if "." not in name or name.startswith("main."):
+                busy[th] = busy.get(th, 0.0) + (b - a) * 1e3
+        with open(args.timeline, "w") as fh:
+            json.dump(dict(step_ms=(te - ts) * 1e3, ntoa=nfile * per,
+                           stages={k: dict(v, mean_ms=v["total_ms"] /
+                                           v["count"])
+                                   for k, v in sorted(summ.items())},
+                           spans=[(n, th, round((a - ts) * 1e3, 3),
+                                   round((b - ts) * 1e3, 3))
+                                  for n, th, a, b in spans]), fh, indent=1)
     ntoa = nfile * per
     out = dict(metric="GetTOAs end-to-end sub-int TOAs/sec (phase+DM, "
                       "%dch×%dbin, host archives, PCIe + bookkeeping "
@@ -679,7 +714,7 @@ def main():
                     chan_mask=None if mask_t is None else mask_t[sl],
                     dev=dev, workspace=ws,
                     n_x=(c1 - c0) if n_x_all else 0, no_hcut=args.no_hcut,
-                    solver=args.solver,
+                    solver=args.solver, mom_x=args.mom_x,
                     max_workspace=1 << 62)
                 ws = res["workspace"]
                 outs.append(res["results"])
@@ -747,7 +782,7 @@ def main():
         "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
                      bytes=steps_subints * dsum_unit),
     }
-    if scat_fit:
+    if scat_fit or args.mom_x:
         kern["xspec"] = dict(name="k_xspec_w<%d, 0>" % L2N, ms=stage_ms[1],
                              unit=xspec_unit,
                              bytes=steps_subints * xspec_unit +
@@ -763,7 +798,14 @@ def main():
         kern["pass"] = dict(name="k_pass<true>", ms=pass_ms, unit=pass_unit,
                             launches=int(pass_launches),
                             bytes=evals * pass_unit + pass_launches * xh * 8)
-    else:
+    if args.mom_x and not scat_fit:
+        #  k_moments (first launch: every sub-int): read X below the cutoff
+        #   and dphi, write 32 complex moments + the centre residual
+        kern["xmom"] = dict(name="k_moments", ms=kern_ms[0],
+                            unit=xh * 16 + nchan * 16 + nchan * (32 * 16 + 8),
+                            bytes=steps_subints * (xh * 16 + nchan * 16 +
+                                                   nchan * (32 * 16 + 8)))
+    elif not scat_fit:
         kern["xmom"] = dict(name="k_xmom_g<%d, 0, true, true>" % L2N,
                             ms=kern_ms[0], unit=xmom_unit,
                             bytes=steps_subints * xmom_unit +
@@ -839,7 +881,7 @@ def main():
                            fits_per_step=total * args.passes,
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
                            harmonic_cutoff=not args.no_hcut,
-                           solver=args.solver,
+                           solver=args.solver, mom_x=args.mom_x,
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),

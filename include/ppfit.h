@@ -75,7 +75,7 @@ enum ppf_option {
                                 cross-spectrum pass is not launched (a
                                 sub-int that would need X ends with
                                 PPF_ST_NOSPACE) */
-    PPF_OPT_SCIPY_TR = 4     /* the fits follow scipy's trust-ncg path
+    PPF_OPT_SCIPY_TR = 4,    /* the fits follow scipy's trust-ncg path
                                 step by step (pptoaslib.py:1055-1060:
                                 radius 1 in raw parameter units,
                                 CG-Steihaug subproblem).  Default: the
@@ -89,6 +89,13 @@ enum ppf_option {
                                 fits half the data passes.
                                 Bounded (method='TNC') fits always take the
                                 scipy path with projected steps. */
+    PPF_OPT_MOM_X = 8        /* phase/DM/GM fits on the wave-FFT shapes take
+                                their Taylor moments from the cross spectrum
+                                X (one spectrum pass writing X below the
+                                harmonic cutoff, then k_moments), instead of
+                                the fused pass that re-FFTs the data rows
+                                for every moment centre: every sub-int then
+                                holds an X slot (x_subints is ignored) */
 };
 
 enum ppf_mode {

@@ -23,6 +23,7 @@ ST_NOSPACE = 0x1000
 OPT_NO_HCUT = 1           # ppf_fit_desc.options
 OPT_NO_X = 2
 OPT_SCIPY_TR = 4          # scattering fits follow scipy's trust-ncg path
+OPT_MOM_X = 8             # phase/DM/GM fits: moments from the stored cross spectrum
 ABI_VERSION = 3
 
 # ppf_result: 32 doubles (include/ppfit.h)

@@ -62,6 +62,22 @@ bool pow2_in_range(int nbin) {
     return nbin >= 32 && nbin <= 8192 && (nbin & (nbin - 1)) == 0;
 }
 
+// nbin the FFT kernels take: even, 32..8192, nbin / 2 = 2^a 3^b 5^c 7^d
+// (power-of-two nbin on the register / radix-4 paths, the others on the
+// mixed-radix LDS FFT)
+bool nbin_supported(int nbin) {
+    return nbin >= 32 && nbin <= 8192 && (nbin & 1) == 0 && ppf::fft_len_supported(nbin / 2);
+}
+
+// log2 of a power-of-two FFT length, 0 otherwise (the kernels' "not a power
+// of two" marker: no wave-FFT path, mixed-radix LDS FFT)
+int fft_log2(int n) {
+    if (n < 1 || (n & (n - 1))) return 0;
+    int l = 0;
+    while ((1 << l) < n) ++l;
+    return l;
+}
+
 int ilog2(int n) {
     int l = 0;
     while ((1 << l) < n) ++l;
@@ -95,10 +111,11 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gP, gw, Msum, state, partials, active, mom, dphi, mres, Mpow, MP, KC,
-        needx, xslot, rclist, Bt, total;
+    size_t M, X, chan, stats, x0, gP, gw, Msum, gpart, gwx, gflag, state, partials, active, mom, dphi,
+        mres, hcen, Mpow, MP, KC, needx, xslot, rclist, Bt, total;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
+    int momx;     // wave shapes, PPF_OPT_MOM_X: every fit's moments from X (k_xspec_w + k_moments)
     int xcap;     // X slots
 };
 
@@ -110,9 +127,11 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
-    L.fused = ppf::xspec_wave_supported(ilog2(d->nbin / 2), L.cb) ? 1 : 0;
+    L.fused = ppf::xspec_wave_supported(fft_log2(d->nbin / 2), L.cb) ? 1 : 0;
+    L.momx = (L.fused && (d->options & PPF_OPT_MOM_X)) ? 1 : 0;
     L.xcap = (L.fused && d->x_subints > 0 && d->x_subints < d->nsub) ? d->x_subints : d->nsub;
     if (L.fused && (d->options & PPF_OPT_NO_X)) L.xcap = 0;
+    if (L.momx) L.xcap = d->nsub;
     L.cbd = d->nchan < 128 ? d->nchan : 128;          // k_dsum channel block
     L.nblkd = (d->nchan + L.cbd - 1) / L.cbd;
     size_t o = 0;
@@ -127,6 +146,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
     L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
     L.mres = o;  o += align256(sizeof(double) * nsub * 2 * nchan);
+    L.hcen = o;  o += L.momx ? align256(sizeof(double) * nsub * 2 * nchan) : 0;
     L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.MP = o;    o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
     L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
@@ -138,6 +158,12 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
         L.gP = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * (size_t)d->nbin);
         L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * 2);
         L.Msum = o; o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nharm);
+        if (L.fused) {   // guess spectrum fused into k_xspec_w (k_gflag)
+            const size_t ng = (size_t)ppf::guess_slots(fft_log2(d->nbin / 2));
+            L.gpart = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * ng);
+            L.gwx = o;   o += align256(sizeof(double) * nsub * (size_t)L.nblk * 3);
+            L.gflag = o; o += align256(nsub);
+        }
     }
     L.total = o;
     return L;
@@ -146,8 +172,9 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
 int check_fit_desc(ppf_ctx *ctx, const ppf_fit_desc *d) {
     if (!d) return fail(ctx, PPF_EINVAL, "null descriptor");
     if (d->nsub < 1 || d->nchan < 1) return fail(ctx, PPF_EINVAL, "nsub=%d nchan=%d", d->nsub, d->nchan);
-    if (!pow2_in_range(d->nbin))
-        return fail(ctx, PPF_EUNSUP, "nbin=%d: must be a power of two in [32, 8192]", d->nbin);
+    if (!nbin_supported(d->nbin))
+        return fail(ctx, PPF_EUNSUP,
+                    "nbin=%d: must be even, in [32, 8192], with nbin/2 = 2^a 3^b 5^c 7^d", d->nbin);
     if (d->data_dtype != PPF_F32 && d->data_dtype != PPF_F64)
         return fail(ctx, PPF_EINVAL, "data_dtype=%d", d->data_dtype);
     if (d->nmodel < 1) return fail(ctx, PPF_EINVAL, "nmodel=%d", d->nmodel);
@@ -300,7 +327,7 @@ const char *ppf_last_error(const ppf_ctx *ctx) {
 }
 
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc) {
-    if (!desc || desc->nsub < 1 || desc->nchan < 1 || !pow2_in_range(desc->nbin)) return 0;
+    if (!desc || desc->nsub < 1 || desc->nchan < 1 || !nbin_supported(desc->nbin)) return 0;
     return fit_layout(desc).total;
 }
 
@@ -328,7 +355,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ctx->ran[slot][2] = d->guess != 0;
     ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
-    ppf::RfftArgs ra{d->nbin, ilog2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
+    ppf::RfftArgs ra{d->nbin, fft_log2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_rfft_rows");
     double *Mpow = (double *)(ws + L.Mpow);
@@ -347,13 +374,23 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     const int use_moments = 1;
     uint8_t *needx = (uint8_t *)(ws + L.needx);
     int32_t *xslot = (int32_t *)(ws + L.xslot);
-    if ((e = ppf::launch_classify(d->nsub, d->fit_flags, d->init, d->log10_tau, L.fused, L.xcap,
+    if ((e = ppf::launch_classify(d->nsub, d->fit_flags, d->init, d->log10_tau, L.fused && !L.momx, L.xcap,
                                   needx, xslot, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_classify");
+    // fused guess: the sub-ints k_xspec_w streams whose mean-model cutoff
+    // fits its guess harmonics accumulate the guess spectrum there
+    uint8_t *gflag = nullptr;
+    if (d->guess && L.fused && fft_log2(d->nbin / 2) == 10) {   // (xspec_guess_fused)
+        gflag = (uint8_t *)(ws + L.gflag);
+        const int klim = 64 * ppf::guess_npl(fft_log2(d->nbin / 2));
+        if ((e = ppf::launch_gflag(d->nsub, d->nchan, needx, (const int32_t *)(ws + L.KC),
+                                   d->model_index, klim, gflag, st)) != hipSuccess)
+            return hip_fail(ctx, e, "k_gflag");
+    }
     mark(1);
 
     ppf::XspecArgs xa{};
-    xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = ilog2(d->nbin / 2);
+    xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = fft_log2(d->nbin / 2);
     xa.kc = kc; xa.nblk = L.nblk; xa.cb = L.cb; xa.dtype = d->data_dtype;
     // k_xspec_w: channel-block-major (mode 2) when the model spectra
     // outgrow the L2s, sub-int-major otherwise; k_xmom_g stages its model
@@ -369,13 +406,23 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.X = (double2 *)(ws + L.X); xa.chan = (double *)(ws + L.chan);
     xa.Mpow = Mpow;
     xa.xslot = xslot;
+    xa.gflag = gflag;
+    if (gflag) {
+        xa.gpart = (double2 *)(ws + L.gpart);
+        xa.gw = (double *)(ws + L.gwx);
+        xa.guess_weights = d->guess_weights;
+        xa.guess_DM = d->guess_DM;
+        xa.nu_fits = d->nu_fits;
+        xa.guess_ref = d->guess_ref;
+    }
     const bool wave = L.fused != 0;
     // fused moment pass (k_xmom) only on the wave-FFT shapes; elsewhere the
     // moments are taken from X (k_moments)
-    const bool fused = wave && use_moments;
-    xa.needx = fused ? needx : nullptr;
-    // fused: only k_pass reads X, and only below its channels' cutoffs
-    xa.KC = fused ? (const int32_t *)(ws + L.KC) : nullptr;
+    const bool fused = wave && use_moments && !L.momx;
+    xa.needx = (fused || L.momx) ? needx : nullptr;
+    // fused: only k_pass reads X, and only below its channels' cutoffs;
+    // momx: k_moments reads it below the same cutoffs
+    xa.KC = (fused || L.momx) ? (const int32_t *)(ws + L.KC) : nullptr;
     if (wave) {
         // (nothing to do when the caller has ruled out X: every sub-int is
         // fitted from k_xmom_g's moments)
@@ -397,6 +444,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         da.guess_weights = d->guess_weights;
         da.guess_ref = d->guess_ref; da.nu_fits = d->nu_fits;
         da.gP = (double *)(ws + L.gP); da.gw = (double *)(ws + L.gw);
+        da.gflag = gflag;
         mark(7);
         if ((e = ppf::launch_dsum(da, st)) != hipSuccess) return hip_fail(ctx, e, "k_dsum");
         mark(8);
@@ -405,7 +453,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
             return hip_fail(ctx, e, "k_model_sum");
         ppf::GuessArgs ga{};
-        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = ilog2(d->nbin / 2);
+        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = fft_log2(d->nbin / 2);
         ga.kc = kc; ga.nblkd = L.nblkd; ga.Ns = d->guess_Ns; ga.mask = d->chan_mask;
         ga.guess_ref = d->guess_ref;
         ga.freqs = d->freqs; ga.P = d->P; ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau;
@@ -413,6 +461,10 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.KC = (const int32_t *)(ws + L.KC);
         ga.x0 = (double *)(ws + L.x0); ga.Msum = msum; ga.Mft = Mft;
         ga.model_index = d->model_index;
+        ga.gflag = gflag;
+        ga.gpart = xa.gpart;
+        ga.gwx = xa.gw;
+        ga.nblk = L.nblk;
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
     }
     mark(3);
@@ -448,6 +500,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
     sa.mres = (double *)(ws + L.mres);
+    sa.mom16 = L.momx;
+    sa.hcen = L.momx ? (double *)(ws + L.hcen) : nullptr;
     sa.xslot = xslot;
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");
@@ -504,7 +558,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             }
             if (sa.moments && any_mom) {
                 const bool full = iter == 0 && g == 0;
-                if (full && fused) mark(5);
+                if (full) mark(5);
                 if (fused && !full) {
                     // re-centring passes: usually few sub-ints, so 8-channel
                     // blocks (4x the workgroups, a quarter of the rounds
@@ -521,7 +575,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
                     e = fused ? ppf::launch_xmom(ma, full, st) : ppf::launch_moments(sa, st);
                 }
                 if (e != hipSuccess) return hip_fail(ctx, e, fused ? "k_xmom" : "k_moments");
-                if (full && fused) {
+                if (full) {
                     mark(6);
                     ctx->ran[slot][4] = true;
                 }
@@ -556,7 +610,7 @@ int ppf_fit2_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream) {
 int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
                      const double *phases, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nrows < 0 || (nrows > 0 && (!in || !phases || !out)))
         return fail(ctx, PPF_EINVAL, "bad rotate arguments");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
@@ -567,7 +621,7 @@ int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::RotateArgs a{nbin, ilog2(nbin / 2), in_dtype, in, phases, T, T2, out};
+    ppf::RotateArgs a{nbin, fft_log2(nbin / 2), in_dtype, in, phases, T, T2, out};
     if ((e = ppf::launch_rotate(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_rotate");
     return PPF_OK;
 }
@@ -583,7 +637,7 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int
                     const void *in, const double *phases, const double *weights, double *out,
                     double *wsum, void *workspace, size_t workspace_bytes, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nsub < 0 || nchan <= 0) return fail(ctx, PPF_EINVAL, "bad align shape");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
     if (nsub == 0) return PPF_OK;
@@ -599,7 +653,7 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
     ppf::AlignArgs a{};
-    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = in_dtype;
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = in_dtype;
     a.ngroup = ppf::align_groups(nsub, nchan);
     a.in = in; a.phases = phases; a.weights = weights; a.T = T; a.T2 = T2;
     char *ws = (char *)workspace;
@@ -616,7 +670,7 @@ int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_d
                          const int32_t *model_row, const double *scales, const double *errs,
                          double dof, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nrows < 0 || (nrows > 0 && (!in || !phases || !model || !model_row || !scales || !errs ||
                                     !out)))
         return fail(ctx, PPF_EINVAL, "bad resid_chi2 arguments");
@@ -628,7 +682,7 @@ int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_d
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::ResidArgs a{nbin, ilog2(nbin / 2), in_dtype, in, phases, model, model_row, scales, errs,
+    ppf::ResidArgs a{nbin, fft_log2(nbin / 2), in_dtype, in, phases, model, model_row, scales, errs,
                      dof, T, T2, out};
     if ((e = ppf::launch_resid_chi2(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_resid_chi2");
     return PPF_OK;
@@ -637,7 +691,7 @@ int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_d
 int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
                     int32_t frac, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nrows < 0 || frac < 1 || (nrows > 0 && (!in || !out)))
         return fail(ctx, PPF_EINVAL, "bad noise arguments");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
@@ -648,7 +702,7 @@ int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::NoiseArgs a{nbin, ilog2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
+    ppf::NoiseArgs a{nbin, fft_log2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
     if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise");
     return PPF_OK;
 }
@@ -713,7 +767,7 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
                           const double *noise, int32_t Ns, double lo, double hi, double *out,
                           void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nprof < 0 || Ns < 1 || Ns > 65536 || (nprof > 0 && (!data || !model || !out)))
         return fail(ctx, PPF_EINVAL, "bad phase-shift arguments");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
@@ -725,7 +779,7 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
     ppf::PhaseShiftArgs a{};
-    a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
+    a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
     a.Ns = Ns; a.lo = lo; a.hi = hi; a.data = data; a.model = model; a.model_index = model_index;
     a.noise = noise; a.T = T; a.T2 = T2; a.out = out;
     if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
@@ -737,7 +791,7 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
                              const double *scattering_index, const double *freqs,
                              const double *nu_ref, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nport < 0 || nchan < 1 || ngauss < 0 ||
         (nport > 0 && (!params || !scattering_index || !freqs || !nu_ref || !out)))
         return fail(ctx, PPF_EINVAL, "bad gauss_portrait arguments");
@@ -757,7 +811,7 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2);
+    a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2);
     a.ngauss = ngauss; a.npar = 2 + 6 * ngauss;
     a.params = params; a.scat_index = scattering_index; a.freqs = freqs; a.nu_ref = nu_ref;
     a.T = T; a.T2 = T2; a.out = out;
@@ -786,7 +840,7 @@ int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_
     ppf::SplineArgs a{};
     a.nport = nport; a.nchan = nchan; a.nbin_model = nbin_model; a.nbin = nbin; a.ncomp = ncomp;
     a.nknots = nknots; a.degree = degree;
-    a.log2N0 = ilog2(nbin_model / 2); a.log2N1 = ilog2(nbin / 2);
+    a.log2N0 = fft_log2(nbin_model / 2); a.log2N1 = fft_log2(nbin / 2);
     a.mean_prof = mean_prof; a.eigvec = eigvec; a.knots = knots; a.coefs = coefs; a.freqs = freqs;
     a.out = out;
     int rc;
@@ -803,7 +857,7 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, con
                     double nu_ref, double noise, uint64_t seed, int64_t first_sub,
                     int32_t out_dtype, void *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nsub < 0 || nchan < 1 || (nsub > 0 && (!model || !freqs || !phi || !DM || !P || !out)))
         return fail(ctx, PPF_EINVAL, "bad synth arguments");
     if (out_dtype != PPF_F32 && out_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "out_dtype");
@@ -819,10 +873,10 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, con
     const size_t nharm = (size_t)nbin / 2 + 1;
     e = hipMallocAsync((void **)&Mft, sizeof(double2) * nchan * nharm, st);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMallocAsync(synth)");
-    ppf::RfftArgs ra{nbin, ilog2(nbin / 2), PPF_F64, model, T, T2, Mft};
+    ppf::RfftArgs ra{nbin, fft_log2(nbin / 2), PPF_F64, model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, nchan, st)) != hipSuccess) return hip_fail(ctx, e, "k_rfft_rows");
     ppf::SynthArgs a{};
-    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = ilog2(nbin / 2); a.dtype = out_dtype;
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = out_dtype;
     a.Mft = Mft; a.freqs = freqs; a.phi = phi; a.DM = DM; a.P = P; a.nu_ref = nu_ref;
     a.noise = noise; a.seed = seed; a.first = first_sub; a.T = T; a.T2 = T2; a.out = out;
     if ((e = ppf::launch_synth(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_synth");

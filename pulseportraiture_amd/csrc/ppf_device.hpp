@@ -248,6 +248,143 @@ __device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Mixed-radix LDS FFT for N = 2^a 3^b 5^c 7^d <= 4096 (nbin = 2N not a power
+// of two: 1000, 1536, 600, ...; numpy's pocketfft takes any length,
+// pptoaslib.py:1022-1025, pplib.py:2455).  Stockham autosort as lds_fft:
+// stage with radix R and span L reads x_q = buf[j + q N/R] (j < N/R,
+// k = j mod L), twiddles x_q by T[q k N/(R L)], takes the R-point DFT and
+// writes buf[(j - k) R + k + q L].  Radices: 4s (one 2 first when the
+// power of two is odd), then 3s, 5s, 7s.  Power-of-two N goes to lds_fft
+// (bitwise unchanged).
+// ---------------------------------------------------------------------------
+constexpr int kMaxFftN = 4096;
+
+// Stage radices of N in order; returns their count, 0 when N has a prime
+// factor above 7 (or N < 2).
+__host__ __device__ inline int fft_radices(int N, int *r) {
+    if (N < 2) return 0;
+    int n = N, p2 = 0, c = 0;
+    while ((n & 1) == 0) { n >>= 1; ++p2; }
+    if (p2 & 1) r[c++] = 2;
+    for (int i = 0; i < p2 / 2; ++i) r[c++] = 4;
+    const int odd[3] = {3, 5, 7};
+    for (int f : odd)
+        while (n % f == 0) { n /= f; r[c++] = f; }
+    return n == 1 ? c : 0;
+}
+__host__ __device__ inline bool fft_len_supported(int N) {
+    int r[32];
+    return N >= 2 && N <= kMaxFftN && fft_radices(N, r) > 0;
+}
+__host__ __device__ inline bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// cos / sin (2 pi m / R), m < R, for the odd radices (exact decimal expansions)
+__device__ constexpr double kCos3[3] = {1.0, -0.5, -0.5};
+__device__ constexpr double kSin3[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+__device__ constexpr double kCos5[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410,
+                                        -0.80901699437494742410, 0.30901699437494742410};
+__device__ constexpr double kSin5[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917,
+                                        -0.58778525229247312917, -0.95105651629515357212};
+__device__ constexpr double kCos7[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429,
+                                        -0.90096886790241912624, -0.90096886790241912624,
+                                        -0.22252093395631440429, 0.62348980185873353053};
+__device__ constexpr double kSin7[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702,
+                                        0.43388373911755812048, -0.43388373911755812048,
+                                        -0.97492791218182360702, -0.78183148246802980871};
+
+// R-point DFT in place (natural order), forward exp(-2 pi i m q / R)
+template <int R>
+__device__ __forceinline__ void dft_small(double2 (&x)[R], bool inv) {
+    if constexpr (R == 2) {
+        const double2 a = x[0], b = x[1];
+        x[0] = cadd(a, b);
+        x[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        const double2 s02 = cadd(x[0], x[2]), d02 = csub(x[0], x[2]);
+        const double2 s13 = cadd(x[1], x[3]), d13 = csub(x[1], x[3]);
+        const double2 id13 = inv ? cmk(-d13.y, d13.x) : cmk(d13.y, -d13.x);
+        x[0] = cadd(s02, s13);
+        x[1] = cadd(d02, id13);
+        x[2] = csub(s02, s13);
+        x[3] = csub(d02, id13);
+    } else {
+        const double *C = R == 3 ? kCos3 : (R == 5 ? kCos5 : kCos7);
+        const double *S = R == 3 ? kSin3 : (R == 5 ? kSin5 : kSin7);
+        const double sg = inv ? 1.0 : -1.0;
+        double2 y[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) {
+            double2 acc = x[0];
+#pragma unroll
+            for (int q = 1; q < R; ++q) {
+                const int e = (m * q) % R;
+                acc = cadd(acc, cmul(x[q], cmk(C[e], sg * S[e])));
+            }
+            y[m] = acc;
+        }
+#pragma unroll
+        for (int m = 0; m < R; ++m) x[m] = y[m];
+    }
+}
+
+template <int R>
+__device__ void mr_stage(double2 *buf, int N, int L, const double2 *__restrict__ T, bool inv) {
+    constexpr int QM = (kMaxFftN / R + kBlock - 1) / kBlock;   // butterflies / thread
+    const int nb = N / R, ts = N / (R * L);
+    double2 x[QM][R];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int j = threadIdx.x + q * kBlock;
+        if (j < nb) {
+            const int k = j % L;
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[q][r] = buf[j + r * nb];
+            if (k) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) x[q][r] = cmul(x[q][r], twid(T, r * k * ts, inv));
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int j = threadIdx.x + q * kBlock;
+        if (j < nb) {
+            const int k = j % L;
+            dft_small<R>(x[q], inv);
+            const int o = (j - k) * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[o + r * L] = x[q][r];
+        }
+    }
+    __syncthreads();
+}
+
+// Any supported N (fft_len_supported); every thread of the block calls it.
+__device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, bool inverse);
+__device__ __noinline__ void lds_fft_mixed(double2 *buf, int N, const double2 *__restrict__ T,
+                                           bool inverse) {
+    int r[32];
+    const int ns = fft_radices(N, r);
+    int L = 1;
+    for (int s = 0; s < ns; ++s) {
+        switch (r[s]) {
+            case 2: mr_stage<2>(buf, N, L, T, inverse); break;
+            case 3: mr_stage<3>(buf, N, L, T, inverse); break;
+            case 4: mr_stage<4>(buf, N, L, T, inverse); break;
+            case 5: mr_stage<5>(buf, N, L, T, inverse); break;
+            default: mr_stage<7>(buf, N, L, T, inverse); break;
+        }
+        L *= r[s];
+    }
+}
+__device__ __forceinline__ void lds_fft_n(double2 *buf, int N, const double2 *__restrict__ T,
+                                          bool inverse) {
+    if (is_pow2(N)) lds_fft(buf, __builtin_ctz((unsigned)N), T, inverse);
+    else lds_fft_mixed(buf, N, T, inverse);
+}
+
 // Compile-time-size variant of lds_fft (exact register footprint, unrolled
 // passes); T may live in LDS or global memory.
 template <int LOG2N, bool INV>
@@ -317,8 +454,9 @@ __device__ __forceinline__ void lds_fft_t(double2 *buf, const double2 *T) {
 // Real FFT post-pass: X_k (k = 0..N) from Z = FFT_N(x_even + i x_odd).
 // T2[k] = exp(-i pi k / N), k < N.
 __device__ __forceinline__ double2 rfft_bin(const double2 *buf, int N, const double2 *__restrict__ T2, int k) {
-    double2 zk = buf[k & (N - 1)];
-    double2 zc = cconj(buf[(N - k) & (N - 1)]);
+    // k in [0, N]: Z_{k mod N} and Z_{(N - k) mod N} (any N)
+    double2 zk = buf[k == N ? 0 : k];
+    double2 zc = cconj(buf[k == 0 ? 0 : N - k]);
     double2 e = cscale(cadd(zk, zc), 0.5);
     double2 o = cscale(csub(zk, zc), 0.5);       // (Z_k - conj Z_{N-k}) / 2
     double2 w = (k < N) ? T2[k] : cmk(-1.0, 0.0);

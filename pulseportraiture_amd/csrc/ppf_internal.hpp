@@ -33,7 +33,21 @@ struct XspecArgs {
     const int32_t *KC;           // [nmodel][nchan] harmonic cutoff (k_model_cut) or null: X is
                                  // written only below the cutoff of each 64-channel group
     const int32_t *xslot;        // [nsub] X slot of each sub-int (k_classify), or null: slot = s
+    // GetTOAs guess spectrum fused into the wave pass (gflag[s] set, see
+    // k_gflag): sum_n w_n D_nk exp(2 pi i k dphi_n(DM_guess)) of the block's
+    // rows for the harmonics guess_pairs() covers, per (sub-int, block)
+    const uint8_t *gflag;        // [nsub] or null (no fused guess)
+    double2 *gpart;              // [nsub][nblk][guess_slots(log2N)]
+    double *gw;                  // [nsub][nblk][3] (sum w, count, sum w^2 errs_FT^2)
+    const double *guess_weights, *guess_DM, *nu_fits;
+    int guess_ref;
 };
+
+// Fused guess harmonics of an N = 2^log2N point wave FFT: k < 64 guess_npl
+// (the FFTFIT sums stop at the mean model's cutoff; a sub-int whose cutoff
+// is higher takes the time-domain pass, k_dsum)
+__host__ __device__ constexpr int guess_npl(int log2N) { return log2N >= 10 ? 7 : (log2N == 9 ? 3 : (log2N == 8 ? 2 : 1)); }
+__host__ __device__ constexpr int guess_slots(int log2N) { return 64 * guess_npl(log2N); }
 
 // k_dsum: GetTOAs guess profile, time-domain dedispersion (pptoas.py:461-464)
 struct DsumArgs {
@@ -45,6 +59,7 @@ struct DsumArgs {
     const double *freqs, *P, *guess_DM, *guess_weights;
     double *gP;                  // [nsub][nblkd][nbin] partial profiles
     double *gw;                  // [nsub][nblkd][2] (sum w, count)
+    const uint8_t *gflag;        // [nsub]: 1 = fused into k_xspec_w (skip), or null
 };
 
 // k_xmom: fused re-FFT + cross spectrum + Taylor moments (no X in HBM)
@@ -85,6 +100,11 @@ struct GuessArgs {
     const double2 *Mft;
     const int32_t *model_index;
     const int32_t *KC;           // [nmodel][nchan] harmonic cutoff (k_model_cut) or null
+    // fused guess spectrum (k_xspec_w) for the sub-ints with gflag set
+    const uint8_t *gflag;        // [nsub] or null
+    const double2 *gpart;        // [nsub][nblk][guess_slots(log2N)]
+    const double *gwx;           // [nsub][nblk][3]
+    int nblk;
 };
 
 struct TRState;
@@ -118,6 +138,10 @@ struct SolveArgs {
     double2 *mom;                // [nsub][2][nchan][kMoments]
     double *dphi;                // [nsub][nchan][2]: d phi_n / d(DM, GM)
     double *mres;                // [nsub][2][nchan]: moment-centre residual per channel
+    // PPF_OPT_MOM_X: 16 moments per channel, expanded in u = (k - h_n) / h_n
+    // about the centre h_n of the wave's harmonic band [0, cutoff)
+    int mom16;
+    double *hcen;                // [nsub][2][nchan]: h_n of each moment set (mom16)
     const int32_t *xslot;        // [nsub] X slot (k_classify; -1 none, -2 no room) or null
     unsigned *rc_count;          // sub-ints k_tr_mom sent back for a new moment centre
     int32_t *rc_list;            // [nsub] their indices (slot order of the atomic)
@@ -266,6 +290,8 @@ hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st);
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_xspec(const XspecArgs &a, hipStream_t st);
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st);
+hipError_t launch_gflag(int nsub, int nchan, const uint8_t *needx, const int32_t *KC,
+                        const int32_t *model_index, int klim, uint8_t *gflag, hipStream_t st);
 hipError_t launch_dsum(const DsumArgs &a, hipStream_t st);
 bool xspec_wave_supported(int log2N, int cb);
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);

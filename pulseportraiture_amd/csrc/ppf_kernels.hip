@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void k_rfft_rows(RfftArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, false);
+    lds_fft_n(lds, a.nbin >> 1, a.T, false);
     double2 *o = a.out + row * (int64_t)(N + 1);
     for (int k = threadIdx.x; k <= N; k += kBlock) o[k] = rfft_bin(lds, N, a.T2, k);
 }
@@ -180,6 +180,73 @@ __global__ __launch_bounds__(kBlock) void k_xspec(XspecArgs a) {
             chan[3] = mpow[0] * inv_e2;    // S_n at tau = 0
         }
         n = nn;
+    }
+}
+
+// ===========================================================================
+// k_xspec_any: k_xspec for nbin / 2 not a power of two (mixed-radix LDS FFT,
+// lds_fft_n): the same per-row arithmetic, rows loaded straight into LDS
+// ===========================================================================
+template <int DT>
+__global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    __shared__ double red[kWaves * 4];
+    const int N = a.nbin >> 1, NH = N + 1;
+    const int tid = threadIdx.x;
+    int s, cb;
+    if (a.xcd_swizzle) {
+        const int per = a.nblk / 8, x = blockIdx.x % 8, r = blockIdx.x / 8;
+        cb = x * per + r % per;
+        s = r / per;
+    } else {
+        s = blockIdx.x / a.nblk;
+        cb = blockIdx.x % a.nblk;
+    }
+    if (a.needx && !a.needx[s]) return;
+    const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double sqrt_half_nbin = sqrt((double)(2 * N) / 2.0);
+    for (int n = c0; n < c1; ++n) {
+        const int64_t crow = (int64_t)s * a.nchan + n;
+        if (mask && !mask[n]) {
+            if (tid < 4) a.chan[crow * 4 + tid] = 0.0;
+            continue;
+        }
+        load_row(lds, a.data, DT, crow, a.nbin);
+        __syncthreads();
+        lds_fft_n(lds, N, a.T, false);
+        double acc[2] = {0.0, 0.0};
+        for (int k = tid; k <= N; k += kBlock) {
+            const double p2 = cabs2(rfft_bin(lds, N, a.T2, k));
+            if (k >= a.kc) acc[0] += p2;
+            if (k >= 1) acc[1] += p2;
+        }
+        block_sum<2>(acc, red);
+        double errs_FT;
+        if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
+        else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)(2 * N)) * sqrt_half_nbin;
+        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+        double2 *Xrow = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan + n;
+        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+        double mpow[1] = {0.0};
+        for (int k = tid; k <= N; k += kBlock) {
+            if (k == 0) {
+                Xrow[0] = cmk(0.0, 0.0);
+            } else {
+                const double2 M = Mrow[k];
+                mpow[0] += cabs2(M);
+                Xrow[(int64_t)k * a.nchan] = cscale(cmulc(rfft_bin(lds, N, a.T2, k), M), inv_e2);
+            }
+        }
+        block_sum<1>(mpow, red);          // (its barriers also end this row's reads)
+        if (tid == 0) {
+            double *chan = a.chan + crow * 4;
+            chan[0] = errs_FT;
+            chan[1] = inv_e2;
+            chan[2] = acc[1] * inv_e2;
+            chan[3] = mpow[0] * inv_e2;
+        }
     }
 }
 
@@ -312,7 +379,8 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
     __shared__ double red[kWaves * 4];
     const int tid = threadIdx.x;
     const int s = blockIdx.x / a.nblkd, blk = blockIdx.x % a.nblkd;
-    const int nbin = a.nbin, bmask = nbin - 1;
+    if (a.gflag && a.gflag[s]) return;        // guess fused into k_xspec_w
+    const int nbin = a.nbin;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     double v[2] = {0.0, 0.0};
@@ -345,8 +413,10 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
             for (int j = 0; j < JB; ++j) {
                 const int t = t0 + tid + j * kBlock;
                 if (t < nbin) {
-                    const int ia = (t + i0) & bmask;
-                    p[j] = fma(wa, (double)x[ia], fma(wb, (double)x[(ia + 1) & bmask], p[j]));
+                    // (t + i0) mod nbin and its successor (any nbin)
+                    const int ia = t + i0 >= nbin ? t + i0 - nbin : t + i0;
+                    const int ib = ia + 1 == nbin ? 0 : ia + 1;
+                    p[j] = fma(wa, (double)x[ia], fma(wb, (double)x[ib], p[j]));
                 }
             }
             if (t0 == 0) { wsum += w; wcnt += 1.0; }
@@ -389,6 +459,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     ElT *xs = reinterpret_cast<ElT *>(dlds) + wave * NB;
     const int s = blockIdx.x / a.nblkd, blk = blockIdx.x % a.nblkd;
+    if (a.gflag && a.gflag[s]) return;        // guess fused into k_xspec_w
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     const double *gwt = a.guess_weights + (int64_t)s * a.nchan;
@@ -504,28 +575,49 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const int N = a.nbin >> 1, nharm = N + 1, s = blockIdx.x, tid = threadIdx.x;
     double2 *z = lds, *xm = lds + N;
     double *sh = reinterpret_cast<double *>(xm + nharm + 1);
+    // fused (k_xspec_w accumulated the guess spectrum of its rows in the
+    // Fourier domain): the block partials of the covered harmonics
+    const bool fused = a.gflag && a.gflag[s];
+    const int NL = guess_slots(a.log2N);
     if (tid == 0) {
-        double w0 = 0.0, w1 = 0.0;
-        for (int b = 0; b < a.nblkd; ++b) {
-            w0 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 0];
-            w1 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 1];
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        if (fused) {
+            for (int b = 0; b < a.nblk; ++b) {
+                w0 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 0];
+                w1 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 1];
+                w2 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 2];
+            }
+        } else {
+            for (int b = 0; b < a.nblkd; ++b) {
+                w0 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 0];
+                w1 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 1];
+            }
         }
-        sh[0] = w0; sh[1] = w1;
+        sh[0] = w0; sh[1] = w1; sh[2] = w2;
     }
-    // weighted dedispersed profile: sum of the k_dsum block partials (fixed
-    // order), packed z_j = p_2j + i p_2j+1 for the real FFT
-    for (int j = tid; j < N; j += kBlock) {
-        double pe = 0.0, po = 0.0;
-        for (int b = 0; b < a.nblkd; ++b) {
-            const double *pp = a.gP + ((int64_t)s * a.nblkd + b) * a.nbin;
-            pe += pp[2 * j];
-            po += pp[2 * j + 1];
+    if (!fused) {
+        // weighted dedispersed profile: sum of the k_dsum block partials
+        // (fixed order), packed z_j = p_2j + i p_2j+1 for the real FFT
+        for (int j = tid; j < N; j += kBlock) {
+            double pe = 0.0, po = 0.0;
+            for (int b = 0; b < a.nblkd; ++b) {
+                const double *pp = a.gP + ((int64_t)s * a.nblkd + b) * a.nbin;
+                pe += pp[2 * j];
+                po += pp[2 * j + 1];
+            }
+            z[j] = cmk(pe, po);
         }
-        z[j] = cmk(pe, po);
     }
     __syncthreads();
     const double wsum = sh[0], cnt = sh[1];
-    lds_fft(z, a.log2N, a.T, false);
+    if (!fused) lds_fft_n(z, a.nbin >> 1, a.T, false);
+    // R_k of the fused partials (k < NL; 0 above: past every channel's cutoff)
+    auto fused_bin = [&](int k) {
+        double2 r = cmk(0.0, 0.0);
+        if (k >= 1 && k < NL)
+            for (int b = 0; b < a.nblk; ++b) r = cadd(r, a.gpart[((int64_t)s * a.nblk + b) * NL + k]);
+        return r;
+    };
     double pw[1] = {0.0};
     const int mi = a.model_index ? a.model_index[s] : 0;
     const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
@@ -551,7 +643,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
             }
         }
         if (!kv) continue;
-        double2 R = cscale(rfft_bin(z, N, a.T2, k), 1.0 / wsum);
+        double2 R = cscale(fused ? fused_bin(k) : rfft_bin(z, N, a.T2, k), 1.0 / wsum);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
             double u = kTwoPi * (double)k * a.guess_tau[s];
@@ -564,7 +656,8 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     }
     block_sum<1>(pw, red);
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
-    const double err = sig * sqrt((double)a.nbin / 2.0);
+    // fused: the profile's expected noise, sqrt(sum w^2 errs_FT^2) / W
+    const double err = fused ? sqrt(sh[2]) / wsum : sig * sqrt((double)a.nbin / 2.0);
     // the mean model has no harmonic above the largest channel cutoff
     // (k_model_cut): the FFTFIT sums stop there
     double kmx[1] = {1.0};
@@ -611,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, false);
+    lds_fft_n(lds, a.nbin >> 1, a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
     // harmonics handled by this thread: k = tid + 256 i, k < N (pre-pass pairs k, N-k)
@@ -635,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, true);
+    lds_fft_n(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     double2 *o = reinterpret_cast<double2 *>(a.out) + row * (int64_t)N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
@@ -651,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, false);
+    lds_fft_n(lds, a.nbin >> 1, a.T, false);
     double acc[1] = {0.0};
     for (int k = threadIdx.x + a.kc; k <= N; k += kBlock) acc[0] += cabs2(rfft_bin(lds, N, a.T2, k));
     block_sum<1>(acc, red);
@@ -672,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     const int mi = a.model_index ? a.model_index[prof] : 0;
     load_row(fbuf, a.model, 1, mi, a.nbin);
     __syncthreads();
-    lds_fft(fbuf, a.log2N, a.T, false);
+    lds_fft_n(fbuf, a.nbin >> 1, a.T, false);
     double pp[1] = {0.0};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
         double2 M = rfft_bin(fbuf, N, a.T2, k);
@@ -682,7 +775,7 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     __syncthreads();
     load_row(fbuf, a.data, a.dtype, prof, a.nbin);
     __syncthreads();
-    lds_fft(fbuf, a.log2N, a.T, false);
+    lds_fft_n(fbuf, a.nbin >> 1, a.T, false);
     double acc[3] = {0.0, 0.0, pp[0]};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
         double2 D = rfft_bin(fbuf, N, a.T2, k);
@@ -757,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
         lds[k] = irfft_prebin(X1, X2, a.T2[k]);
     }
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, true);
+    lds_fft_n(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     const int64_t row = (int64_t)s * a.nchan + n;
     for (int j = threadIdx.x; j < N; j += kBlock) {
@@ -880,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
         // taus = (tau / nbin) * (freqs / nu_ref)**alpha; B_k = 1 / (1 + 2 pi i k tau_n)
         const double tn = tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]);
         __syncthreads();
-        lds_fft(lds, a.log2N, a.T, false);
+        lds_fft_n(lds, a.nbin >> 1, a.T, false);
         double2 Xk[KMAX], Xn[KMAX];
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
@@ -904,7 +997,7 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
             if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
         }
         __syncthreads();
-        lds_fft(lds, a.log2N, a.T, true);
+        lds_fft_n(lds, a.nbin >> 1, a.T, true);
         const double sc = 1.0 / (double)N;
         double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
         for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
@@ -918,6 +1011,13 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
 // ===========================================================================
 // host-side launchers
 // ===========================================================================
+// per-thread harmonic slots of the block kernels' KMAX instantiations (1, 2,
+// 4, 8, 16): the smallest that holds ceil(N / kBlock)
+static inline int kmax_pow2(int N) {
+    int q = (N + kBlock - 1) / kBlock, k = 1;
+    while (k < q) k <<= 1;
+    return k;
+}
 static inline int log2i(int n) {
     int l = 0;
     while ((1 << l) < n) ++l;
@@ -953,11 +1053,18 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
         case 10: launch_xspec_t<10>(a, st); break;
         case 11: launch_xspec_t<11>(a, st); break;
         case 12: launch_xspec_t<12>(a, st); break;
+        case 0: {      // nbin / 2 not a power of two
+            dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(kBlock);
+            const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+            if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_any<0>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_xspec_any<1>), g, b, lds, st, a);
+            break;
+        }
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
-bool dsum_wave_supported(int nbin) { return nbin >= 256 && nbin <= 2048; }
+bool dsum_wave_supported(int nbin) { return nbin >= 256 && nbin <= 2048 && is_pow2(nbin); }
 
 template <int DT, int L2>
 static void launch_dsum_w(const DsumArgs &a, hipStream_t st) {
@@ -1007,7 +1114,7 @@ hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nport * a.nchan)), b(kBlock);
-    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+    switch (kmax_pow2(a.nbin / 2)) {
         case 1: hipLaunchKernelGGL(k_gauss_port<1>, g, b, lds, st, a); break;
         case 2: hipLaunchKernelGGL(k_gauss_port<2>, g, b, lds, st, a); break;
         case 4: hipLaunchKernelGGL(k_gauss_port<4>, g, b, lds, st, a); break;
@@ -1020,7 +1127,7 @@ hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
-    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+    switch (kmax_pow2(a.nbin / 2)) {
         case 1: hipLaunchKernelGGL(k_rotate<1>, g, b, lds, st, a); break;
         case 2: hipLaunchKernelGGL(k_rotate<2>, g, b, lds, st, a); break;
         case 4: hipLaunchKernelGGL(k_rotate<4>, g, b, lds, st, a); break;
@@ -1063,7 +1170,7 @@ __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
         wtot += w;
         load_row(lds, a.in, a.dtype, row, a.nbin);
         __syncthreads();
-        lds_fft(lds, a.log2N, a.T, false);
+        lds_fft_n(lds, a.nbin >> 1, a.T, false);
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
             const int k = threadIdx.x + i * kBlock;
@@ -1116,7 +1223,7 @@ __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, true);
+    lds_fft_n(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)n * N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cadd(o[j], cscale(lds[j], sc));
@@ -1137,7 +1244,7 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
         hipError_t e = launch_align_part_w(a, st);
         if (e != hipSuccess) return e;
     }
-    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+    switch (kmax_pow2(a.nbin / 2)) {
         case 1: if (!wave) hipLaunchKernelGGL(k_align_part<1>, gp, b, lds, st, a);
                 hipLaunchKernelGGL(k_align_fin<1>, gf, b, lds, st, a); break;
         case 2: if (!wave) hipLaunchKernelGGL(k_align_part<2>, gp, b, lds, st, a);
@@ -1167,7 +1274,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, false);
+    lds_fft_n(lds, a.nbin >> 1, a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
 #pragma unroll
@@ -1188,7 +1295,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft(lds, a.log2N, a.T, true);
+    lds_fft_n(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N, s = a.scales[row];
     const double *m = a.model + (int64_t)a.model_row[row] * a.nbin;
     double acc[1] = {0.0};
@@ -1207,7 +1314,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
 hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
-    switch ((a.nbin / 2 + kBlock - 1) / kBlock) {
+    switch (kmax_pow2(a.nbin / 2)) {
         case 1: hipLaunchKernelGGL(k_resid_chi2<1>, g, b, lds, st, a); break;
         case 2: hipLaunchKernelGGL(k_resid_chi2<2>, g, b, lds, st, a); break;
         case 4: hipLaunchKernelGGL(k_resid_chi2<4>, g, b, lds, st, a); break;
@@ -1303,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
     double2 *spec = lds + NM;              // output spectrum Y_k, k <= N1
     for (int j = tid; j < N0; j += kBlock) buf[j] = cmk(value(2 * j), value(2 * j + 1));
     __syncthreads();
-    lds_fft(buf, a.log2N0, a.T0, false);
+    lds_fft_n(buf, a.nbin_model >> 1, a.T0, false);
     const int num = a.nbin, Nx = a.nbin_model;
     const int Nm = num < Nx ? num : Nx, nyq = Nm / 2 + 1;
     const double scale = (double)num / (double)Nx;
@@ -1325,7 +1432,7 @@ __global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
         buf[k] = irfft_prebin(Xk, Xn, a.T21[k]);
     }
     __syncthreads();
-    lds_fft(buf, a.log2N1, a.T1, true);
+    lds_fft_n(buf, a.nbin >> 1, a.T1, true);
     const double sc = 1.0 / (double)N1;
     double2 *o2 = reinterpret_cast<double2 *>(o);
     for (int j = tid; j < N1; j += kBlock) o2[j] = cscale(buf[j], sc);

@@ -194,6 +194,32 @@ __global__ __launch_bounds__(kClassifyBlock) void k_classify(int nsub, const int
     }
 }
 
+// k_gflag: the sub-ints whose GetTOAs guess spectrum k_xspec_w accumulates
+// (ppf_xspec.hip, GS): those it streams (needx) whose mean model has no
+// harmonic above the fused range (max_n KC[model][n] <= klim, the FFTFIT sums
+// of k_guess stop at that cutoff); the others take k_dsum.
+__global__ __launch_bounds__(kBlock) void k_gflag(int nsub, int nchan, const uint8_t *needx,
+                                                  const int32_t *KC, const int32_t *model_index,
+                                                  int klim, uint8_t *gflag) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= nsub) return;
+    int ok = 0;
+    if (!needx || needx[s]) {
+        const int64_t m = model_index ? model_index[s] : 0;
+        int mx = 0;
+        for (int n = 0; n < nchan; ++n) mx = max(mx, KC[m * nchan + n]);
+        ok = mx <= klim ? 1 : 0;
+    }
+    gflag[s] = (uint8_t)ok;
+}
+
+hipError_t launch_gflag(int nsub, int nchan, const uint8_t *needx, const int32_t *KC,
+                        const int32_t *model_index, int klim, uint8_t *gflag, hipStream_t st) {
+    hipLaunchKernelGGL(k_gflag, dim3((unsigned)((nsub + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       nsub, nchan, needx, KC, model_index, klim, gflag);
+    return hipGetLastError();
+}
+
 // ===========================================================================
 // k_tr_init: one wave per sub-integration (4 per workgroup)
 // ===========================================================================
@@ -300,6 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
     const int mmode = (a.moments && !scat && nf > 0 && cnt > 0.0) ? 1 : 0;
     if (lane == 0) {
         S.mmode = mmode;
+        S.mom16 = (mmode && a.mom16) ? 1 : 0;
         S.need_mom = mmode;
         S.mtarget = 0;
         S.macc = 0;
@@ -953,6 +980,9 @@ constexpr double kXMax = 4.5;
 // Below |x| = 2.3 the first 24 moments hold the same bound (2.3^22 / 22! <
 // 1.6e-13): the evaluation then skips the last quarter of the moments.
 constexpr double kX24 = 2.3;
+// 16 moments (mom16): x^14 / 14! < 1.6e-13 for |x| <= 0.73, with x = 2 pi h_n
+// Delta and h_n the centre of the channel band's harmonics (k_moments)
+constexpr double kX16 = 0.73;
 constexpr int kMomChans = 64;                    // channels per k_moments workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -960,7 +990,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // MFMA f64 16x16x4: A = Y (16 channels x 4 harmonics; one wave = 16
 // channels), B = u^m (4 harmonics x 16 moments), two B tiles (m < 16, m >=
 // 16) and separate real / imaginary A.  The harmonic sum is the MFMA K loop.
-__global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_moments(SolveArgs a) {
     const int nblk = (a.nchan + kMomChans - 1) / kMomChans;
     const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const TRState &S = a.state[s];
@@ -969,7 +999,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
     const int q = S.mtarget;
     const double c0 = S.mc[q][0], c1 = S.mc[q][1], c2 = S.mc[q][2];
     const int nharm = (a.nbin >> 1) + 1;
-    const double h = 0.5 * (double)(nharm - 1), ih = 1.0 / h;
+    const double h = 0.5 * (double)(nharm - 1);
     const int ci = lane & 15, kk = lane >> 4;
     const int nbase = blk * kMomChans + wave * 16;
     const int n = nbase + ci;
@@ -982,34 +1012,64 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
     }
     const double2 *Xr = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * nharm * a.nchan +
                          (valid ? n : 0);   // X[slot][k][n]
+    // harmonic cutoff of the wave's 16 channels (k_model_cut; they lie in one
+    // aligned 64-channel group): X past it carries |M_k| < 1e-14 of the
+    // channel's peak, and k_xspec_w writes X only below the group's largest
+    // cutoff
+    int kend = nharm;
+    if (a.KC) {
+        const int mi = a.model_index ? a.model_index[s] : 0;
+        const int nn = min(n, a.nchan - 1);
+        kend = (int)wave_max((double)a.KC[(int64_t)mi * a.nchan + nn]);
+    }
+    // mom16: 16 moments in u = (k - hw) / hw, hw = kend / 2 the centre of
+    // the band the wave sums (|u| <= 1 there), one B tile; h_n recorded
+    // for k_tr_mom
+    const bool m16 = S.mom16 != 0;
+    const double hw = m16 ? 0.5 * (double)(kend > 2 ? kend : 2) : h, ihw = 1.0 / hw;
+    if (m16 && valid && kk == 0) a.hcen[((int64_t)s * 2 + q) * a.nchan + n] = hw;
     const double2 W4 = cexp2pi(4.0 * phin);
     f64x4 dre0 = {0.0, 0.0, 0.0, 0.0}, dre1 = dre0, dim0 = dre0, dim1 = dre0;
     double2 E = cmk(1.0, 0.0);
-    // 8 K-steps (32 harmonics) per iteration: all 8 loads in flight first
-    constexpr int KU = 8;
-    for (int kb = 0; kb < nharm; kb += 4 * KU) {
-        double2 xv[KU];
+    // batches of 4 K-steps (16 harmonics), software-pipelined: the next
+    // batch's loads are in flight while this one's MFMAs run
+    constexpr int KU = 4;
+    double2 xa[KU], xb[KU];
+    auto ld = [&](double2 (&xv)[KU], int kb) {
 #pragma unroll
         for (int t = 0; t < KU; ++t) {
             const int k = kb + 4 * t + kk;
-            xv[t] = (valid && k < nharm) ? Xr[(int64_t)k * a.nchan] : cmk(0.0, 0.0);
+            xv[t] = (valid && k < kend) ? Xr[(int64_t)k * a.nchan] : cmk(0.0, 0.0);
         }
+    };
+    auto mm = [&](const double2 (&xv)[KU], int kb) {
 #pragma unroll
         for (int t = 0; t < KU; ++t) {
             const int k = kb + 4 * t + kk;
             // phasor by recurrence, re-seeded exactly every 64 harmonics
-            E = (((4 * t) & 63) == 0 && (kb & 63) == 0) ? cexp2pi((double)k * phin) : cmul(E, W4);
+            // (kb is a multiple of 16: only t = 0 can re-seed)
+            if (t == 0 && (kb & 63) == 0) E = cexp2pi((double)k * phin);
+            else E = cmul(E, W4);
             const double2 y = cmul(xv[t], E);
-            const double u = ((double)k - h) * ih;
+            const double u = ((double)k - hw) * ihw;
             const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4, u16 = u8 * u8;
             const double uj = ((ci & 1) ? u : 1.0) * ((ci & 2) ? u2 : 1.0) *
                               ((ci & 4) ? u4 : 1.0) * ((ci & 8) ? u8 : 1.0);
-            const double ujh = uj * u16;
             dre0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, uj, dre0, 0, 0, 0);
             dim0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, uj, dim0, 0, 0, 0);
-            dre1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, ujh, dre1, 0, 0, 0);
-            dim1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, ujh, dim1, 0, 0, 0);
+            if (!m16) {
+                const double ujh = uj * u16;
+                dre1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, ujh, dre1, 0, 0, 0);
+                dim1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, ujh, dim1, 0, 0, 0);
+            }
         }
+    };
+    ld(xa, 0);
+    for (int kb = 0; kb < kend; kb += 4 * KU) {
+        ld(xb, kb + 4 * KU);
+        mm(xa, kb);
+#pragma unroll
+        for (int t = 0; t < KU; ++t) xa[t] = xb[t];
     }
     // D[row][col]: col = lane & 15 = moment, row = (lane >> 4) + 4 r = channel
     double2 *M = a.mom + ((int64_t)s * 2 + q) * a.nchan * kMoments;
@@ -1018,7 +1078,7 @@ __global__ __launch_bounds__(kBlock) void k_moments(SolveArgs a) {
         const int ch = nbase + kk + 4 * r;
         if (ch < a.nchan) {
             M[(int64_t)ch * kMoments + ci] = cmk(dre0[r], dim0[r]);
-            M[(int64_t)ch * kMoments + 16 + ci] = cmk(dre1[r], dim1[r]);
+            if (!m16) M[(int64_t)ch * kMoments + 16 + ci] = cmk(dre1[r], dim1[r]);
         }
     }
 }
@@ -1111,6 +1171,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
     const double *chan = a.chan + (int64_t)s * a.nchan * 4;
     const double2 *MOM = a.mom + (int64_t)s * 2 * a.nchan * kMoments;
     const double *MRES = a.mres + (int64_t)s * 2 * a.nchan;
+    // mom16: per-channel expansion centres h_n and 16 moments (radius kX16)
+    const bool m16 = L.mom16 != 0;
+    const double *HC = m16 ? a.hcen + (int64_t)s * 2 * a.nchan : MRES;
+    const double xmax = m16 ? kX16 : kXMax;
     double *stats = a.stats + (int64_t)s * 2 * a.nchan * 10;
     const int flagmask = L.flagmask;
     const int nit = (a.nchan + kBlock - 1) / kBlock;
@@ -1129,24 +1193,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
             if (!L.mvalid[cand]) continue;
             const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
             const double *rc = MRES + (int64_t)cand * a.nchan;
-            double xm[1] = {0.0};
+            const double *hc = HC + (int64_t)cand * a.nchan;
+            double xm[1] = {0.0};          // max_n h_n |Delta_n|
             for (int n0 = 0; n0 < a.nchan; n0 += 4 * kBlock) {   // 4 channels' loads, then use
-                double v1[4], v2[4], vr[4];
+                double v1[4], v2[4], vr[4], vh[4];
                 bool ok[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int n = n0 + tid + kBlock * j, nc = min(n, a.nchan - 1);
                     v1[j] = dp[2 * nc]; v2[j] = dp[2 * nc + 1]; vr[j] = rc[nc];
+                    vh[j] = m16 ? hc[nc] : h;
                     ok[j] = n < a.nchan && (!use_mask || mk[nc] != 0);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    if (ok[j]) xm[0] = fmax(xm[0], fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
+                    if (ok[j]) xm[0] = fmax(xm[0], vh[j] * fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
             }
             block_max<1>(xm, red);
-            if (kTwoPi * h * xm[0] <= kXMax) {
+            if (kTwoPi * xm[0] <= xmax) {
                 qsel = cand;
-                xsel = kTwoPi * h * xm[0];
+                xsel = kTwoPi * xm[0];
             }
         }
         TP(1);
@@ -1166,6 +1232,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         const double e0 = t0 - L.mc[qsel][0], e1 = t1 - L.mc[qsel][1], e2 = t2 - L.mc[qsel][2];
         const double2 *Mq = MOM + (int64_t)qsel * a.nchan * kMoments;
         const double *rq = MRES + (int64_t)qsel * a.nchan;
+        const double *hq = HC + (int64_t)qsel * a.nchan;
         double *st = stats + (int64_t)L.slot_eval * a.nchan * 10;
         double acc[10];
 #pragma unroll
@@ -1175,7 +1242,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         // in flight while the current one is summed
         constexpr int KQ = kMoments / 4;
         double2 qa[KQ], qb[KQ];
-        double c_d1, c_d2, c_rq, c_S;           // channel scalars, prefetched with quarter 0
+        double c_d1, c_d2, c_rq, c_S, c_h;      // channel scalars, prefetched with quarter 0
         int c_ok;
         auto ldq = [&](int i, int quarter, double2 (&b)[KQ]) {
             const int n = min(tid + kBlock * i, a.nchan - 1);
@@ -1186,35 +1253,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         auto ldc = [&](int i) {
             const int n = min(tid + kBlock * i, a.nchan - 1);
             c_d1 = dp[2 * n]; c_d2 = dp[2 * n + 1]; c_rq = rq[n]; c_S = chan[n * 4 + 3];
+            c_h = m16 ? hq[n] : h;
             c_ok = mk[n];
         };
-        const bool q4 = xsel > kX24;           // uniform: all 32 moments needed
+        const bool q4 = !m16 && xsel > kX24;   // uniform: all 32 moments needed
         ldq(0, 0, qa);
         ldc(0);
         for (int i = 0; i < nit; ++i) {
             const int n = tid + kBlock * i;
             ldq(i, 1, qb);
             const bool valid = n < a.nchan && (!use_mask || c_ok != 0);
-            const double d1 = c_d1, d2 = c_d2, Sn = c_S;
+            const double d1 = c_d1, d2 = c_d2, Sn = c_S, hn_ = c_h;
             const double del = e0 + e1 * d1 + e2 * d2 + c_rq;
-            const double x = kTwoPi * h * del;
+            const double x = kTwoPi * hn_ * del;
             double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
             double r0 = 1.0, r1 = 0.0, r2 = 0.0;
             taylor_seg<0, KQ, 0>(qa, x, r0, r1, r2, G0, G1, G2);
-            ldq(i, 2, qa);
-            taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
-            if (q4) ldq(i, 3, qb);
-            taylor_seg<2 * KQ, 3 * KQ, 2 * KQ>(qa, x, r0, r1, r2, G0, G1, G2);
-            if (i + 1 < nit) {
-                ldq(i + 1, 0, qa);
-                ldc(i + 1);
+            if (m16) {
+                // 16 moments: the next channel's first quarter is in flight
+                // while the second is summed
+                if (i + 1 < nit) {
+                    ldq(i + 1, 0, qa);
+                    ldc(i + 1);
+                }
+                taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+            } else {
+                ldq(i, 2, qa);
+                taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+                if (q4) ldq(i, 3, qb);
+                taylor_seg<2 * KQ, 3 * KQ, 2 * KQ>(qa, x, r0, r1, r2, G0, G1, G2);
+                if (i + 1 < nit) {
+                    ldq(i + 1, 0, qa);
+                    ldc(i + 1);
+                }
+                if (q4) taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
             }
-            if (q4) taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
             if (!valid) continue;
-            const double2 eix = cexp2pi(h * del);
+            const double2 eix = cexp2pi(hn_ * del);
             const double2 F = cmul(eix, G0);
-            const double2 K1 = cscale(cmul(eix, cadd(G0, G1)), h);
-            const double2 K2 = cscale(cmul(eix, cadd(cadd(G0, G2), cscale(G1, 2.0))), h * h);
+            const double2 K1 = cscale(cmul(eix, cadd(G0, G1)), hn_);
+            const double2 K2 = cscale(cmul(eix, cadd(cadd(G0, G2), cscale(G1, 2.0))), hn_ * hn_);
             const double C = F.x, Cp = -kTwoPi * K1.y, Cpp = -kTwoPi * kTwoPi * K2.x;
             double *sn = st + (int64_t)n * 10;
             sn[0] = C; sn[1] = Cp; sn[2] = Cpp; sn[6] = Sn;

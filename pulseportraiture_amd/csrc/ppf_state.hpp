@@ -21,8 +21,9 @@ struct TRState {
     int k, status, nfev, phase;
     int slot_cur, slot_eval, flagmask, nchanx;
     int scat, hb, g_sum, g_tau;
-    int g_alpha, newton, sub, pad2;    // newton: Newton trust region; sub: channel-group stride of
-                                       // its warm start (1: every channel; tr_update_newton)
+    int g_alpha, newton, sub, mom16;   // newton: Newton trust region; sub: channel-group stride of
+                                       // its warm start (1: every channel; tr_update_newton);
+                                       // mom16: 16 band-centred moments (k_moments, PPF_OPT_MOM_X)
     // moment mode (no scattering): two moment sets centred at mc[q]
     int mmode, need_mom, mtarget, macc;
     int mvalid[2], meval, nmom;

@@ -136,8 +136,28 @@ __host__ __device__ constexpr int tw_slots() {
 template <int LOG2N>
 __host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() + (wfft::use_xor<LOG2N>() ? 4 : 2); }
 
-template <int LOG2N, int DT>
-__global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
+// GS: the sub-ints with gflag set (k_gflag: every channel's harmonic cutoff
+// below NL = 64 guess_npl) also accumulate the GetTOAs guess spectrum
+// (pptoas.py:461-464 in the Fourier domain, as rotate_data does it):
+// G_k = sum_n w_n D_nk exp(2 pi i k dphi_n), dphi_n = Dconst DM_guess / P
+// (nu_n^-2 - nu_ref^-2), for 1 <= k < NL.  No register holds them: pass 2
+// of the post-pass stores a row's terms in the wave-buffer slots of the
+// harmonics N - k, which X no longer needs (its write-out stops below the
+// cutoff), and the write-out phase adds the round's rows to a workgroup sum
+// in LDS in wave order (deterministic).  The profile's noise for the
+// FFTFIT scale is its expectation from the channels' noise:
+// err^2 = sum_n w_n^2 errs_FT,n^2 / W^2.
+// minimum waves per SIMD: at 1024 points the LDS admits two 4-wave
+// workgroups per CU (two waves per SIMD), and the fused-guess variant must
+// keep that register budget (<= 256)
+template <int LOG2N>
+__host__ __device__ constexpr int xspec_wpe() { return LOG2N == 10 ? 2 : 1; }
+// the fused guess runs at 1024 points only: below, its extra registers cost
+// a wave per SIMD or spill (those shapes take k_dsum)
+__host__ __device__ constexpr bool xspec_guess_fused(int log2N) { return log2N == 10; }
+template <int LOG2N, int DT, bool GS>
+__global__ __launch_bounds__(64 * xsw<LOG2N>()) __attribute__((amdgpu_waves_per_eu(xspec_wpe<LOG2N>())))
+void k_xspec_w(XspecArgs a) {
     constexpr int kXSW = xsw<LOG2N>();
     using P = wfft::Plan<LOG2N>;
     constexpr int N = P::N, R = P::R, NH = N + 1;
@@ -202,6 +222,39 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
     auto usable = [&](int n) {
         return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
     };
+    // fused guess: per-lane channel weight and dedispersion phase of
+    // channel cbase + lane; the workgroup sum G[1..NL) after the twiddles
+    constexpr int NL = 64 * guess_npl(LOG2N);
+    bool gon = false;
+    double g_w = 0.0, g_dg = 0.0, g_w2e2 = 0.0;
+    double2 *gacc = lds + kXSW * SL + (PPF_TW_LDS ? tw_slots<LOG2N>() : 0);
+    if constexpr (GS) {
+        gon = a.gflag[s] != 0;                         // uniform
+        if (gon) {
+            for (int t = threadIdx.x; t < NL; t += 64 * kXSW) gacc[t] = cmk(0.0, 0.0);
+            // nu_ref: mean usable frequency of the sub-int (GetTOAs) or
+            // nu_fit (ppalign), as k_dsum
+            const double *fr = a.freqs + (int64_t)s * a.nchan;
+            double v0 = 0.0, v1 = 0.0;
+            for (int nn = lane; nn < a.nchan; nn += 64)
+                if (!mask || mask[nn]) { v0 += fr[nn]; v1 += 1.0; }
+            v0 = wave_sum(v0);
+            v1 = wave_sum(v1);
+            const double mu = v0 / v1;
+            double nu_ref_m2 = 1.0 / (mu * mu);
+            if (a.guess_ref) {
+                const double nf = a.nu_fits[(int64_t)s * 3];
+                if (nf == nf) nu_ref_m2 = 1.0 / (nf * nf);
+            }
+            const double Dg = kDconst * a.guess_DM[s] / a.P[s];
+            if (cbase + lane < cend) {
+                const double f = fr[cbase + lane];
+                g_w = a.guess_weights[(int64_t)s * a.nchan + cbase + lane];
+                g_dg = Dg * (1.0 / (f * f) - nu_ref_m2);
+            }
+            __syncthreads();
+        }
+    }
     RowT zr[R];
     auto fetch = [&](int n) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
@@ -268,13 +321,31 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
 
+            // guess phasor of this row: El = w e^{2 pi i k dphi} at k = lane
+            // + 64 i by recurrence (step e^{2 pi i 64 dphi}: lane 1's phasor
+            // squared six times)
+            double2 El = cmk(0.0, 0.0), Est = El;
+            if (GS && gon) {
+                const int r = n - cbase;
+                const double wn = readlane_d(g_w, r), dg = readlane_d(g_dg, r);
+                const double2 E1 = cexp2pi((double)lane * dg);
+                El = cscale(E1, wn);
+                Est = cmk(readlane_d(E1.x, 1), readlane_d(E1.y, 1));
+#pragma unroll
+                for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
+                g_w2e2 += wn * wn * errs_FT * errs_FT;
+            }
             {
                 // in place: X_k -> pad(k), X_{N-k} -> pad(N-k); the pair
-                // (0, N) keeps X_N in pad(N/2) (read above as Dm)
+                // (0, N) keeps X_N in pad(N/2) (read above as Dm).  (Skipping
+                // the pairs past the block's cutoff, and X_{N-k} when the
+                // cutoff is below N/2, measured slower: C3 k_xspec_w 27.8 ->
+                // 28.6 ms, C2 with MOM_X 27.3 -> 28.3 ms)
                 double2 w = w_seed;
 #pragma unroll
                 for (int i = 0; i < NP; ++i) {
                     const int klo = lane + 64 * i, khi = N - klo;
+                    if (GS && gon && 64 * i >= NL) break;   // (uniform) beyond the cutoff
                     double2 Dlo, Dhi;
                     rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
                     w = cmul(w, w_step);
@@ -295,8 +366,15 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
                     }
                     buf[wfft::pad<LOG2N>(klo)] =
                         (klo == 0) ? cmk(0.0, 0.0) : cscale(cmulc(Dlo, Mlo), inv_e2);
-                    buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
-                        cscale(cmulc(Dhi, Mhi), inv_e2);
+                    if (GS && gon) {
+                        // X_{N-k} is past the cutoff: its slot takes the
+                        // row's guess term of harmonic k (k = 0: dropped)
+                        if (klo != 0) buf[wfft::pad<LOG2N>(khi)] = cmul(Dlo, El);
+                        El = cmul(El, Est);
+                    } else {
+                        buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
+                            cscale(cmulc(Dhi, Mhi), inv_e2);
+                    }
                     SCHED_CUT();
                 }
             }
@@ -325,7 +403,39 @@ __global__ __launch_bounds__(64 * xsw<LOG2N>()) void k_xspec_w(XspecArgs a) {
                 }
             }
         }
+        if (GS && gon) {
+            // the round's rows' guess terms, in wave order
+            for (int t = threadIdx.x; t < NL; t += 64 * kXSW) {
+                if (t == 0) continue;
+                double2 acc = gacc[t];
+#pragma unroll
+                for (int w2 = 0; w2 < kXSW; ++w2)
+                    if (usable(cbase + r * kXSW + w2)) acc = cadd(acc, lds[w2 * SL + wfft::pad<LOG2N>(N - t)]);
+                gacc[t] = acc;
+            }
+        }
         __syncthreads();
+    }
+    if constexpr (GS) {
+        if (gon) {
+            double2 *gp = a.gpart + ((int64_t)s * a.nblk + cb) * NL;
+            for (int t = threadIdx.x; t < NL; t += 64 * kXSW) gp[t] = gacc[t];
+            // the block's weight sum and usable-channel count (every wave
+            // holds the block's weights in its lanes), and sum w^2 errs_FT^2
+            // per wave, added in wave order (buffer slot 0 is free after the
+            // last round's barrier)
+            const double wsum = wave_sum(mlane ? g_w : 0.0), cnt = wave_sum(mlane ? 1.0 : 0.0);
+            if (lane == 0) reinterpret_cast<double *>(buf)[0] = g_w2e2;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double acc = 0.0;
+                for (int w2 = 0; w2 < kXSW; ++w2) acc += reinterpret_cast<const double *>(lds + w2 * SL)[0];
+                double *o = a.gw + ((int64_t)s * a.nblk + cb) * 3;
+                o[0] = wsum;
+                o[1] = cnt;
+                o[2] = acc;
+            }
+        }
     }
 }
 
@@ -756,7 +866,10 @@ static void launch_w(const XspecArgs &a, hipStream_t st) {
     const size_t lds = ((size_t)xsw<L2>() * xspec_slw<L2>() + (PPF_TW_LDS ? tw_slots<L2>() : 0)) *
                        sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * xsw<L2>());
-    hipLaunchKernelGGL((k_xspec_w<L2, DT>), g, b, lds, st, a);
+    if (a.gflag && xspec_guess_fused(L2))
+        hipLaunchKernelGGL((k_xspec_w<L2, DT, xspec_guess_fused(L2)>), g, b,
+                           lds + (size_t)guess_slots(L2) * sizeof(double2), st, a);
+    else hipLaunchKernelGGL((k_xspec_w<L2, DT, false>), g, b, lds, st, a);
 }
 
 bool xspec_wave_supported(int log2N, int cb) {

@@ -72,12 +72,23 @@ def barrier():
         dist.barrier()
 
 
+def collective_device(device=None):
+    """Device of a small tensor handed to a collective: None (CPU) under
+    gloo; under nccl (RCCL has no CPU path) the given device, else this
+    rank's current HIP device."""
+    b = backend()
+    if b == "gloo":
+        return None
+    if device is None and b == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
 def max_over_ranks(x, device=None):
     """Max of a python float over ranks (used for timings)."""
     if not dist.is_initialized():
         return x
-    if backend() == "gloo":
-        device = None
+    device = collective_device(device)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -110,8 +121,7 @@ def raise_if_any_failed(err, device=None):
         if err is not None:
             raise err
         return
-    if backend() == "gloo":
-        device = None
+    device = collective_device(device)
     t = torch.tensor([1.0 if err is not None else 0.0], dtype=torch.float64,
                      device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -129,6 +129,7 @@ def x_subints(fit_flags, init, log10_tau, nsub):
 
 
 SOLVER = os.environ.get("PPF_SOLVER", "newton")
+MOM_X = os.environ.get("PPF_MOM_X", "0") == "1"
 
 
 def _solver(name):
@@ -144,7 +145,7 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
               guess_Ns=100, guess_tau=None, dev=None, workspace=None,
               n_x=None, no_hcut=False, max_workspace=None, guess_ref=0,
-              bounds=None, solver=None):
+              bounds=None, solver=None, mom_x=None):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
@@ -160,6 +161,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     passes over the cross spectrum for scattering fits and half the data
     passes for ppalign's) or "scipy" (scipy trust-ncg's own path,
     PPF_OPT_SCIPY_TR); None = SOLVER (env PPF_SOLVER, default "newton").
+    mom_x: take the moments of the phase/DM/GM fits from the stored cross
+    spectrum (PPF_OPT_MOM_X); None = MOM_X (env PPF_MOM_X).
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
@@ -237,10 +240,11 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     cfg = dict(model=model_t, log10_tau=log10_tau, option=option,
                is_toa=is_toa, mode=mode, max_iter=max_iter, guess=guess,
                guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref,
-               solver=_solver(solver))
+               solver=_solver(solver),
+               mom_x=MOM_X if mom_x is None else bool(mom_x))
     lib = _lib.load()
     need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
-    if need <= (64 << 20) or nsub == 1:
+    if max_workspace is None and (need <= (64 << 20) or nsub == 1):
         # small batches (the single-call APIs) skip the free-memory query
         return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
     if max_workspace is None:
@@ -303,7 +307,8 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.x_subints = int(max(n_x, 1)) if n_x < (c1 - c0) else 0
     d.options = (_lib.OPT_NO_HCUT if cfg["no_hcut"] else 0) | \
         (_lib.OPT_NO_X if n_x == 0 else 0) | \
-        (_lib.OPT_SCIPY_TR if cfg.get("solver") == "scipy" else 0)
+        (_lib.OPT_SCIPY_TR if cfg.get("solver") == "scipy" else 0) | \
+        (_lib.OPT_MOM_X if cfg.get("mom_x") else 0)
     d.guess_ref = int(cfg["guess_ref"])
     d.bounds = pp(per_sub["bounds"])
     return d
@@ -314,8 +319,9 @@ def _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg):
     nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
-                                  " (nbin must be a power of two in "
-                                  "[32, 8192])" % (d.nsub, d.nchan, d.nbin))
+                                  " (nbin must be even, in [32, 8192], with "
+                                  "nbin/2 = 2^a 3^b 5^c 7^d)" %
+                                  (d.nsub, d.nchan, d.nbin))
     return nbytes
 
 

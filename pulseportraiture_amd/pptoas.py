@@ -10,9 +10,11 @@ corrections, TOA flags, DeltaDM).  Archive I/O stays on PSRCHIVE via
 
 Reference: /root/reference/pptoas.py (file:line cited per block).
 """
+import contextlib
 import os
 import threading
 import time
+import warnings
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -21,6 +23,7 @@ import torch
 from . import _lib, engine
 from . import dist as _dist
 from . import pplib as _pplib
+from .timeline import span
 from .pplib import (DataBunch, file_is_type, guess_fit_freq, read_model,
                     scattering_alpha, write_TOAs, weighted_mean,
                     scattering_times, scattering_portrait_FT,
@@ -412,8 +415,13 @@ class GetTOAs(object):
         # archive to the next (the 2-channel rule, pptoas.py:523-525), which
         # only a rank that has seen every earlier archive can reproduce.
         rank, world = _rank_world()
+        # (nor method='TNC' without bounds: its default tau bound comes from
+        # the nbin of the first sub-int fitted in serial order,
+        # pptoas.py:503-513, which a rank starting at a later archive cannot
+        # see)
         by_archive = world > 1 and len(datafiles) >= world and \
-            not (self.fit_DM and self.fit_GM)
+            not (self.fit_DM and self.fit_GM) and \
+            not (method == "TNC" and bounds is None)
         mine = range(len(datafiles))
         if by_archive:
             a0, na = _dist.shard(len(datafiles), rank, world)
@@ -445,12 +453,18 @@ class GetTOAs(object):
         mine = list(mine)
         loads = {}
 
+        # the loader thread works on this rank's device: the HIP current
+        # device is per host thread, and a new thread starts on GPU 0
+        ldev = engine.device() if torch.cuda.is_available() else None
+
         def _load(f):
-            return load_data(f, dedisperse=False, dededisperse=False,
-                             tscrunch=tscrunch, pscrunch=True, fscrunch=False,
-                             rm_baseline=rm_baseline, flux_prof=False,
-                             refresh_arch=False, return_arch=False,
-                             quiet=quiet)
+            with (torch.cuda.device(ldev) if ldev is not None else
+                  contextlib.nullcontext()):
+                return load_data(f, dedisperse=False, dededisperse=False,
+                                 tscrunch=tscrunch, pscrunch=True,
+                                 fscrunch=False, rm_baseline=rm_baseline,
+                                 flux_prof=False, refresh_arch=False,
+                                 return_arch=False, quiet=quiet)
         pending = None
         err = None
         try:
@@ -459,17 +473,23 @@ class GetTOAs(object):
                     if pos + ahead < len(mine) and mine[pos + ahead] not in loads:
                         nxt = mine[pos + ahead]
                         loads[nxt] = loader.submit(_load, datafiles[nxt])
-                job = self._prep_archive(iarch, datafiles[iarch], ctx, stager,
-                                         loads.pop(iarch))
+                with span("prep"):
+                    job = self._prep_archive(iarch, datafiles[iarch], ctx,
+                                             stager, loads.pop(iarch))
                 if job is None:
                     continue
                 fut = pool.submit(self._fit_archive, job, ctx)
                 if pending is not None:
-                    self._book_archive(pending[0], pending[1].result(), ctx,
-                                       start)
+                    with span("main.wait_fit"):
+                        r = pending[1].result()
+                    with span("book"):
+                        self._book_archive(pending[0], r, ctx, start)
                 pending = (job, fut)
             if pending is not None:
-                self._book_archive(pending[0], pending[1].result(), ctx, start)
+                with span("main.wait_fit"):
+                    r = pending[1].result()
+                with span("book"):
+                    self._book_archive(pending[0], r, ctx, start)
         except Exception as exc:            # every rank raises, below
             if not by_archive:
                 raise
@@ -482,7 +502,7 @@ class GetTOAs(object):
             stager.close()
         if by_archive:
             # a failed rank must not leave the others in the gather
-            _dist.raise_if_any_failed(err)
+            _dist.raise_if_any_failed(err, ldev)
             self._gather_archives(marks)
 
     def _gather_archives(self, marks):
@@ -529,7 +549,8 @@ class GetTOAs(object):
         fit_duration = 0.0
         try:
             if loaded is not None:
-                data = loaded.result()
+                with span("prep.wait_load"):
+                    data = loaded.result()
             else:
                 data = load_data(datafile, dedisperse=False,
                                  dededisperse=False, tscrunch=tscrunch,
@@ -576,6 +597,12 @@ class GetTOAs(object):
             return None
         d = data
         nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
+        if bary and not d.get("doppler_known", True):
+            # psrfits.load_data has no ephemeris: its Doppler factors are 1
+            warnings.warn("%s: Doppler factors unknown on the PSRFITS fast "
+                          "path (no PSRCHIVE ephemeris); DM, GM and nu_ref_tau "
+                          "stay topocentric (bary=True has no effect)" %
+                          datafile, RuntimeWarning)
         if d.source is None:
             d.source = "noname"
         obs = DataBunch(telescope=d.telescope, backend=d.backend,
@@ -593,12 +620,17 @@ class GetTOAs(object):
         nok = len(ok_isubs)
         # the portraits stay in HBM: the fit worker orders itself after
         # their generation on this thread's stream (models_ev)
+        _sp = span("prep.models")
+        _sp.__enter__()
         models, model_index = self._models(d, ok_isubs, fit_scat, quiet,
                                            host=False)
         models_ev = None
         if isinstance(models, torch.Tensor) and models.is_cuda:
             models_ev = torch.cuda.Event()
             models_ev.record(torch.cuda.current_stream(models.device))
+        _sp.__exit__(None, None, None)
+        _sp = span("prep.batch")
+        _sp.__enter__()
         # ---- gather the batch (pptoas.py:384-529) --------------------
         mask = np.zeros((nok, nchan), dtype=np.uint8)
         init = np.zeros((nok, 5))
@@ -675,6 +707,7 @@ class GetTOAs(object):
             else:
                 self._ff[0] = list(np.copy(self.fit_flags))
             flags_b[j] = self._ff[0]
+        _sp.__exit__(None, None, None)
         rank, world = (0, 1) if ctx["by_archive"] else _rank_world()
         first, count = _dist.shard(nok, rank, world)
         sel = ok_isubs[first:first + count]
@@ -721,7 +754,10 @@ class GetTOAs(object):
         dev = job["dev"]
         nccl = _dist.backend() == "nccl"
         with torch.cuda.device(dev), torch.cuda.stream(_worker_stream(dev)):
-            data_t = job["staged"].wait()
+            with span("fit.wait_staged"):
+                data_t = job["staged"].wait()
+            _sp = span("fit.batch")
+            _sp.__enter__()
             if job.get("models_ev") is not None:
                 cur = torch.cuda.current_stream(dev)
                 cur.wait_event(job["models_ev"])
@@ -739,6 +775,7 @@ class GetTOAs(object):
                 table = _dist.allgather_rows(table if nccl else table.cpu(),
                                              nok, job["world"])
             r = _unpack(table.cpu().numpy(), nchan)
+            _sp.__exit__(None, None, None)
         job["staged"].release()
         r["batch_duration"] = time.time() - t_fit
         return r

@@ -536,6 +536,9 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
                                   "reads archives as stored")
     if state not in (None, "Intensity"):
         raise NotImplementedError("state=%r needs PSRCHIVE" % state)
+    from .timeline import span
+    _sp = span("load.open")
+    _sp.__enter__()
     f = PSRFITS(filename)
     nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
     if npol > 1 and not (pscrunch or state == "Intensity"):
@@ -559,6 +562,7 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     scl, offs = f.scales_offsets()
     weights = f.weights()
     dev = engine.device(dev)
+    _sp.__exit__(None, None, None)
     # the scales, offsets and weights travel with the DATA bytes: one
     # page-locked buffer per device holds [DATA rows | DAT_SCL | DAT_OFFS |
     # weights] (float32, 256-B aligned), so the small columns cost no
@@ -592,7 +596,10 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
             # (starting each chunk's upload as soon as it lands, beside the
             # reads of the rest, was measured slower end to end: 6.2-6.8k
             # vs 7.7k TOAs/s in one call)
-            f.read_data_into(nbytes, host.numpy())
+            with span("load.read"):
+                f.read_data_into(nbytes, host.numpy())
+            _sp = span("load.device")
+            _sp.__enter__()
             raw_d.copy_(host, non_blocking=True)
             out = engine.unpack_psrfits(
                 raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
@@ -607,6 +614,9 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
             ev.record(st)
         ev.synchronize()
         packed = packed.cpu().numpy()
+        _sp.__exit__(None, None, None)
+    _sp = span("load.meta")
+    _sp.__enter__()
     n1, n2 = nsub * nchan * 3, nsub * nbin
     stats = packed[:n1].reshape(nsub, nchan, 3)
     total = packed[n1:n1 + n2].reshape(nsub, nbin)
@@ -636,7 +646,8 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     data = pplib.DataBunch(
         arch=None, backend=str(p.get("BACKEND", "")).strip(),
         backend_delay=float(p.get("BE_DELAY", 0.0)),
-        bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub), DM=DM,
+        bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub),
+        doppler_known=False, DM=DM,
         dmc=0, epochs=epochs, filename=filename, flux_prof=np.array([]),
         freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
         integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
@@ -650,4 +661,5 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
         subtimes=list(tsub), telescope=telescope,
         telescope_code=_telescope_code(telescope), weights=weights)
     f.close()
+    _sp.__exit__(None, None, None)
     return data

@@ -84,6 +84,12 @@ FITS = [
          seed=108, noise=12.0, dm_off=1.5e-2),
     dict(name="lowsnr_all_512x2048", nchan=512, nbin=2048,
          flags=[1, 1, 1, 1, 1], seed=109, tau=2e-3, noise=12.0),
+    # round 4: nbin not a power of two (numpy's rfft takes any length,
+    # pptoaslib.py:1022-1025): the mixed-radix LDS FFT (2^2 5^3, 2^8 3)
+    dict(name="pd_128x1000", nchan=128, nbin=1000, flags=[1, 1, 0, 0, 0],
+         seed=110),
+    dict(name="pdta_128x1536", nchan=128, nbin=1536, flags=[1, 1, 0, 1, 1],
+         seed=111, tau=2e-3),
 ]
 
 
@@ -192,6 +198,9 @@ TOAS = [
     # (g) method='Newton-CG' (pptoaslib.py:1049-1050)
     dict(name="ncg", nfile=1, nsub=2, nchan=64, nbin=512, seed=212,
          kw=dict(method="Newton-CG")),
+    # (h) round 4: nbin = 1000 through the whole get_TOAs loop (guess
+    # profile, its FFTFIT, the fit) on the mixed-radix FFT
+    dict(name="nb1000", nfile=1, nsub=3, nchan=64, nbin=1000, seed=213),
 ]
 
 

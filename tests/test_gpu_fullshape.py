@@ -33,7 +33,8 @@ def _kept_harmonic_fraction(model):
                                   "c3_pdta_512x2048", "narrow_pd_512x2048",
                                   "pd_64x4096", "pdta_64x128",
                                   "lowsnr_pd_512x2048", "lowsnr_pd_64x512",
-                                  "lowsnr_all_512x2048"])
+                                  "lowsnr_all_512x2048", "pd_128x1000",
+                                  "pdta_128x1536"])
 def test_fullshape_fit_matches_reference(name):
     """configs[2]'s fit (phi, DM, GM, tau, alpha) and phi+DM+tau+alpha at
     512 x 2048, a narrow-component template at 512 x 2048 (no harmonic
@@ -41,7 +42,8 @@ def test_fullshape_fit_matches_reference(name):
     shapes nbin = 4096 and 128, and three low-S/N fits (S/N 45 and 26 with
     the initial DM several bins off at the band edges: the moment path's
     truncation bound is relative to sum_k |Y_k|, loosest when |C_n| is
-    small; S/N 133 with all five parameters), through the drop-in
+    small; S/N 133 with all five parameters), nbin = 1000 and 1536 (not
+    powers of two: the mixed-radix LDS FFT), through the drop-in
     fit_portrait_full."""
     from pulseportraiture_amd import pptoaslib
     c, data, model, freqs = F.fit_case(name)
@@ -208,7 +210,7 @@ def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True,
 
 
 BRANCHES = ["scatgm", "scatfix", "opts", "chan12", "tscr", "tnc", "tncscat",
-            "ncg"]
+            "ncg", "nb1000"]
 
 
 @pytest.mark.timeout(300)

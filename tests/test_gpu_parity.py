@@ -32,12 +32,13 @@ def test_noise_matches_reference(ppl):
     np.testing.assert_allclose(ppl.get_noise(m["rot_port"], chans=True),
                                m["noise_port"], rtol=1e-12)
     assert abs(ppl.get_noise(m["rot_prof"]) / m["noise_prof"] - 1) < 1e-12
-    for nb in (256, 2048):
+    # nbin 1000: nbin/2 = 2^2 5^3 on the mixed-radix LDS FFT
+    for nb in (256, 1000, 2048):
         np.testing.assert_allclose(
             ppl.get_noise(m["noise_in_%d" % nb], chans=True),
             m["noise_out_%d" % nb], rtol=1e-12)
-    with pytest.raises(NotImplementedError):     # nbin must be a power of 2
-        ppl.get_noise(m["noise_in_1000"], chans=True)
+    with pytest.raises(NotImplementedError):     # nbin/2 = 3 x 167
+        ppl.get_noise(np.ones((2, 1002)), chans=True)
 
 
 def test_noise_fp32_input_equals_fp64(ppl):
@@ -176,6 +177,44 @@ def test_batch_equals_single_and_is_deterministic():
             nu_outs=nu_outs[i:i + 1]))
         np.testing.assert_array_equal(s["results"][0], b1["results"][i])
         np.testing.assert_array_equal(s["scales"][0], b1["scales"][i])
+    # an explicit workspace budget below the batch's need splits it into
+    # chunks (engine.fit_batch); every table equals the one-call run
+    ch = engine.results_numpy(engine.fit_batch(data, model, freqs, P, init,
+                                               flags, max_workspace=1 << 16,
+                                               **kw))
+    for k in ("results", "scales", "scale_errs", "channel_snrs",
+              "covariance"):
+        np.testing.assert_array_equal(ch[k], b1[k], err_msg=k)
+
+
+def test_moments_from_x_equal_fused_pass():
+    """PPF_OPT_MOM_X (moments from the stored cross spectrum, k_moments)
+    lands on the fused pass's fits (k_xmom_g): same stationary point to well
+    inside the parity bar (the two sum the same harmonics in another order
+    and expand around the exact, not the bin-rounded, centre)."""
+    from pulseportraiture_amd import engine, _lib
+    cases = ["pd_64x512", "pd_nuout_64x512", "pdg_64x512"]
+    cs = [G.full_case(n) for n in cases]
+    data = np.stack([c["data"] for c in cs])
+    model = np.stack([c["model"].astype(float) for c in cs])
+    kw = dict(nu_fits=np.stack([c["nu_fits"] for c in cs]),
+              nu_outs=np.stack([c["nu_outs"] for c in cs]),
+              model_index=np.arange(3))
+    args = (data, model, np.stack([c["freqs"] for c in cs]),
+            np.array([float(c["P"]) for c in cs]),
+            np.stack([c["init"] for c in cs]), np.stack([c["flags"] for c in cs]))
+    a = engine.results_numpy(engine.fit_batch(*args, mom_x=False, **kw))
+    b = engine.results_numpy(engine.fit_batch(*args, mom_x=True, **kw))
+    I = _lib.RESULT_INDEX
+    ra, rb = a["results"], b["results"]
+    err = ra[:, I["param_errs"]]
+    dp = np.abs(rb[:, I["params"]] - ra[:, I["params"]])
+    dp[:, 0] = np.abs((dp[:, 0] + 0.5) % 1.0 - 0.5)
+    ok = err > 0
+    assert np.all(dp[ok] <= 1e-3 * err[ok]), (dp, err)
+    np.testing.assert_allclose(rb[:, I["red_chi2"]], ra[:, I["red_chi2"]],
+                               rtol=1e-10)
+    np.testing.assert_allclose(b["scales"], a["scales"], rtol=1e-7, atol=0)
 
 
 def test_masked_channels_equal_subset_fit(ppt):

@@ -46,3 +46,37 @@ def test_raise_pending_ignores_converged_status_bits():
     # errors: only NO_ROOT, SINGULAR and NOSPACE raise
     R = SimpleNamespace(_dev_inputs={"_pending": [_rows(1, 2, 3)]})
     ppalign.raise_pending(R)
+
+
+# ---------------------------------------------------------- collectives -----
+def test_collective_device_under_nccl_is_the_current_hip_device(monkeypatch):
+    """RCCL has no CPU path: the error flag of raise_if_any_failed (and the
+    timing max) must live on this rank's HIP device when the caller passes
+    none (the archive-sharded get_TOAs did, round 3 ADVICE)."""
+    from pulseportraiture_amd import dist
+    monkeypatch.setattr(dist, "backend", lambda: "nccl")
+    monkeypatch.setattr(dist.torch.cuda, "current_device", lambda: 3)
+    assert dist.collective_device() == torch.device("cuda", 3)
+    assert dist.collective_device(torch.device("cuda", 1)) == \
+        torch.device("cuda", 1)
+    monkeypatch.setattr(dist, "backend", lambda: "gloo")
+    assert dist.collective_device(torch.device("cuda", 1)) is None
+
+
+def test_raise_if_any_failed_puts_the_flag_on_the_device(monkeypatch):
+    from pulseportraiture_amd import dist
+    seen = []
+    real_tensor = torch.tensor
+
+    def fake_tensor(v, dtype=None, device=None):
+        seen.append(device)
+        return real_tensor(v, dtype=dtype)
+    monkeypatch.setattr(dist, "is_dist", lambda: True)
+    monkeypatch.setattr(dist, "backend", lambda: "nccl")
+    monkeypatch.setattr(dist.torch.cuda, "current_device", lambda: 2)
+    monkeypatch.setattr(dist.torch, "tensor", fake_tensor)
+    monkeypatch.setattr(dist.dist, "all_reduce", lambda t, op=None: None)
+    dist.raise_if_any_failed(None)
+    with pytest.raises(KeyError):
+        dist.raise_if_any_failed(KeyError("x"))
+    assert seen == [torch.device("cuda", 2)] * 2

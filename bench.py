@@ -35,6 +35,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TF = 78.6            # MI355X spec: FP64 vector = FP64 matrix = 78.6 TFLOPS (half the 157.3 FP32 rate, MI355X_MICROARCH.md)
 
 
+MOMX = {"auto": None, "x": True, "fused": False}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,10 +88,13 @@ def parse():
                     help="sum every harmonic (PPF_OPT_NO_HCUT: no per-channel "
                     "cutoff of harmonics below 1e-28 of the template's peak "
                     "power)")
-    ap.add_argument("--mom-x", action="store_true",
-                    help="phase/DM fits take their Taylor moments from the "
-                    "stored cross spectrum (k_xspec_w + k_moments, "
-                    "PPF_OPT_MOM_X) instead of the fused k_xmom_g pass")
+    ap.add_argument("--mom-x", default="auto", choices=["auto", "x", "fused"],
+                    help="where phase/DM fits take their Taylor moments: "
+                    "the library's choice (auto: from the stored cross "
+                    "spectrum at nbin 2048 with the guess fused into the "
+                    "spectrum pass), always from X (k_xspec_w + k_moments, "
+                    "PPF_OPT_MOM_X) or always from the fused k_xmom_g pass "
+                    "(PPF_OPT_FUSED_MOM)")
     ap.add_argument("--solver", default="newton", choices=["newton", "scipy"],
                     help="minimiser of the scattering fits (--fit full/scat): "
                     "the Newton trust region (default) or scipy trust-ncg's "
@@ -714,7 +720,7 @@ def main():
                     chan_mask=None if mask_t is None else mask_t[sl],
                     dev=dev, workspace=ws,
                     n_x=(c1 - c0) if n_x_all else 0, no_hcut=args.no_hcut,
-                    solver=args.solver, mom_x=args.mom_x,
+                    solver=args.solver, mom_x=MOMX[args.mom_x],
                     max_workspace=1 << 62)
                 ws = res["workspace"]
                 outs.append(res["results"])
@@ -782,7 +788,11 @@ def main():
         "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
                      bytes=steps_subints * dsum_unit),
     }
-    if scat_fit or args.mom_x:
+    # the library's MOM_X rule (ppf_api.cpp fit_layout): X moments when asked,
+    # or with the guess at nbin 2048 unless the fused pass is forced
+    momx_used = not scat_fit and (args.mom_x == "x" or (
+        args.mom_x == "auto" and nbin == 2048))
+    if scat_fit or momx_used:
         kern["xspec"] = dict(name="k_xspec_w<%d, 0>" % L2N, ms=stage_ms[1],
                              unit=xspec_unit,
                              bytes=steps_subints * xspec_unit +
@@ -798,7 +808,7 @@ def main():
         kern["pass"] = dict(name="k_pass<true>", ms=pass_ms, unit=pass_unit,
                             launches=int(pass_launches),
                             bytes=evals * pass_unit + pass_launches * xh * 8)
-    if args.mom_x and not scat_fit:
+    if momx_used:
         #  k_moments (first launch: every sub-int): read X below the cutoff
         #   and dphi, write 32 complex moments + the centre residual
         kern["xmom"] = dict(name="k_moments", ms=kern_ms[0],
@@ -882,6 +892,8 @@ def main():
                            nchan=nchan, nbin=nbin, chunk=args.chunk,
                            harmonic_cutoff=not args.no_hcut,
                            solver=args.solver, mom_x=args.mom_x,
+                           moments="cross spectrum (k_xspec_w + k_moments)"
+                           if momx_used else "fused pass (k_xmom_g)",
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),

@@ -89,13 +89,20 @@ enum ppf_option {
                                 fits half the data passes.
                                 Bounded (method='TNC') fits always take the
                                 scipy path with projected steps. */
-    PPF_OPT_MOM_X = 8        /* phase/DM/GM fits on the wave-FFT shapes take
+    PPF_OPT_MOM_X = 8,       /* phase/DM/GM fits on the wave-FFT shapes take
                                 their Taylor moments from the cross spectrum
                                 X (one spectrum pass writing X below the
-                                harmonic cutoff, then k_moments), instead of
-                                the fused pass that re-FFTs the data rows
-                                for every moment centre: every sub-int then
-                                holds an X slot (x_subints is ignored) */
+                                harmonic cutoff, then k_moments: 16 moments
+                                about the centre of each channel band's
+                                harmonics), instead of the fused pass that
+                                re-FFTs the data rows for every moment
+                                centre (k_xmom_g): every sub-int then holds
+                                an X slot (x_subints is ignored).  Default
+                                (neither this nor PPF_OPT_FUSED_MOM) where
+                                the GetTOAs guess rides along in the
+                                spectrum pass: guess != 0 and nbin = 2048 */
+    PPF_OPT_FUSED_MOM = 16   /* force the fused k_xmom_g pass (no X for the
+                                phase/DM/GM fits) */
 };
 
 enum ppf_mode {

@@ -128,7 +128,12 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
     L.fused = ppf::xspec_wave_supported(fft_log2(d->nbin / 2), L.cb) ? 1 : 0;
-    L.momx = (L.fused && (d->options & PPF_OPT_MOM_X)) ? 1 : 0;
+    // moments from X: on request, or by default where the GetTOAs guess is
+    // fused into the spectrum pass (1024-point rows): there the X pass
+    // replaces both the guess pass (k_dsum) and k_xmom_g's re-FFT
+    const bool mom_auto = d->guess && fft_log2(d->nbin / 2) == 10;
+    L.momx = (L.fused && !(d->options & PPF_OPT_FUSED_MOM) &&
+              ((d->options & PPF_OPT_MOM_X) || mom_auto)) ? 1 : 0;
     L.xcap = (L.fused && d->x_subints > 0 && d->x_subints < d->nsub) ? d->x_subints : d->nsub;
     if (L.fused && (d->options & PPF_OPT_NO_X)) L.xcap = 0;
     if (L.momx) L.xcap = d->nsub;

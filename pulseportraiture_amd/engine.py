@@ -129,7 +129,11 @@ def x_subints(fit_flags, init, log10_tau, nsub):
 
 
 SOLVER = os.environ.get("PPF_SOLVER", "newton")
-MOM_X = os.environ.get("PPF_MOM_X", "0") == "1"
+# phase/DM/GM moments: None = the library's choice (from the stored cross
+# spectrum where the GetTOAs guess rides along in the spectrum pass), True /
+# False = always from X / always from the fused k_xmom_g pass (env PPF_MOM_X
+# = 1 / 0)
+MOM_X = {"1": True, "0": False}.get(os.environ.get("PPF_MOM_X", ""), None)
 
 
 def _solver(name):
@@ -162,7 +166,9 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     passes for ppalign's) or "scipy" (scipy trust-ncg's own path,
     PPF_OPT_SCIPY_TR); None = SOLVER (env PPF_SOLVER, default "newton").
     mom_x: take the moments of the phase/DM/GM fits from the stored cross
-    spectrum (PPF_OPT_MOM_X); None = MOM_X (env PPF_MOM_X).
+    spectrum (True, PPF_OPT_MOM_X) or from the fused pass (False,
+    PPF_OPT_FUSED_MOM); None = MOM_X (env PPF_MOM_X; unset: the library
+    chooses).
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
@@ -308,7 +314,8 @@ def _desc(per_sub, c0, c1, n_x, cfg):
     d.options = (_lib.OPT_NO_HCUT if cfg["no_hcut"] else 0) | \
         (_lib.OPT_NO_X if n_x == 0 else 0) | \
         (_lib.OPT_SCIPY_TR if cfg.get("solver") == "scipy" else 0) | \
-        (_lib.OPT_MOM_X if cfg.get("mom_x") else 0)
+        (_lib.OPT_MOM_X if cfg.get("mom_x") is True else 0) | \
+        (_lib.OPT_FUSED_MOM if cfg.get("mom_x") is False else 0)
     d.guess_ref = int(cfg["guess_ref"])
     d.bounds = pp(per_sub["bounds"])
     return d

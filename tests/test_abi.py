@@ -63,8 +63,23 @@ def test_workspace_query_and_validation_without_gpu():
     d.options = _lib.OPT_NO_X          # ignored off the fused path
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == nb3
     d.options = 0
-    d.nbin = 1000   # not a power of two
-    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0
+    # nbin 1000 (nbin/2 = 2^2 5^3) runs on the mixed-radix LDS FFT; nbin/2
+    # with a prime factor above 7 (1002 = 2 x 3 x 167), odd nbin and nbin
+    # past 8192 are refused
+    d.nbin = 1000
+    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0
+    for nb in (1002, 1001, 8194, 16):
+        d.nbin = nb
+        assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
+    # with the GetTOAs guess at nbin 2048 the phase/DM fits take their
+    # moments from X by default (every sub-int holds a slot); the fused
+    # pass can be forced
+    d.nbin, d.x_subints, d.options, d.guess = 2048, 2, 0, 1
+    nbg = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+    d.options = _lib.OPT_FUSED_MOM
+    assert nbg - lib.ppf_fit_workspace_bytes(ctypes.byref(d)) >= \
+        8 * 512 * 1025 * 16
+    d.options, d.guess = 0, 0
     # a NULL context is rejected before touching the device
     assert lib.ppf_fit_batch(None, ctypes.byref(d), None) == _lib.PPF_EINVAL
 

@@ -612,14 +612,19 @@ def test_no_x_option_and_x_slots():
         assert got == bad, (n_x, st)
 
 
-@pytest.mark.parametrize("solver,min_rc", [("scipy", 8), ("newton", 2)])
-def test_recentring_passes_batch_independent_and_deterministic(solver, min_rc):
+@pytest.mark.parametrize("solver,min_rc,mom_x", [("scipy", 8, None),
+                                                 ("newton", 2, None),
+                                                 ("newton", 2, True)])
+def test_recentring_passes_batch_independent_and_deterministic(solver, min_rc,
+                                                               mom_x):
     """Re-centring launches take the sub-ints k_tr_mom listed through an
     atomic slot counter, packed eight to a workgroup on 8-channel blocks, so
     the packing differs from run to run and from batch to batch: a sub-int's
     result must not (bitwise), in fits where many sub-ints re-centre (with
     scipy's path most do; the Newton trust region's scaled steps leave the
-    expansion radius far less often, 3 of 48 here)."""
+    expansion radius far less often, 3 of 48 here; with the moments taken
+    from X, mom_x, a re-centring is a k_moments launch over the listed
+    sub-ints)."""
     from pulseportraiture_amd import _lib, engine, synth
     nsub, nchan, nbin = 48, 256, 1024
     b = synth.make_batch(nsub, nchan, nbin, first=777)
@@ -638,7 +643,7 @@ def test_recentring_passes_batch_independent_and_deterministic(solver, min_rc):
             nu_outs=np.full((n, 3), np.nan), guess=True,
             guess_weights=np.ones((n, nchan)),
             guess_DM=np.full(n, dm_start), guess_Ns=nbin, guess_ref=1,
-            errs=errs[sl], solver=solver))
+            errs=errs[sl], solver=solver, mom_x=mom_x))
     I = _lib.RESULT_INDEX
     full = fit(slice(0, nsub))
     again = fit(slice(0, nsub))

@@ -33,6 +33,17 @@ from .pptoaslib import unpack_result, _status_message, _nu_zero_messages
 
 max_nfile = 999                    # pptoas.py:33
 rm_baseline = bool(_pplib.F0_fact)  # pptoas.py:36-39
+# whole-array batch gathering and bookkeeping for archives whose fitted
+# sub-ints share channels, frequencies and fit flags (bit-identical to the
+# per-sub-int loops, which remain the general path; False forces those)
+FAST_HOST = True
+
+
+def _is_fits(filename):
+    try:
+        return file_is_type(filename, "FITS")
+    except (OSError, TypeError):
+        return False
 
 
 def load_data(filename, **kwargs):
@@ -458,13 +469,16 @@ class GetTOAs(object):
         ldev = engine.device() if torch.cuda.is_available() else None
 
         def _load(f):
+            # defer: a PSRFITS file's read is done and its device work
+            # queued here; _prep_archive waits for it (psrfits._Pending)
             with (torch.cuda.device(ldev) if ldev is not None else
                   contextlib.nullcontext()):
                 return load_data(f, dedisperse=False, dededisperse=False,
                                  tscrunch=tscrunch, pscrunch=True,
                                  fscrunch=False, rm_baseline=rm_baseline,
                                  flux_prof=False, refresh_arch=False,
-                                 return_arch=False, quiet=quiet)
+                                 return_arch=False, quiet=quiet,
+                                 **({"defer": True} if _is_fits(f) else {}))
         pending = None
         err = None
         try:
@@ -551,6 +565,9 @@ class GetTOAs(object):
             if loaded is not None:
                 with span("prep.wait_load"):
                     data = loaded.result()
+                    fin = getattr(data, "finish", None)
+                    if fin is not None and not isinstance(data, dict):
+                        data = fin()
             else:
                 data = load_data(datafile, dedisperse=False,
                                  dededisperse=False, tscrunch=tscrunch,
@@ -631,82 +648,14 @@ class GetTOAs(object):
         _sp.__exit__(None, None, None)
         _sp = span("prep.batch")
         _sp.__enter__()
-        # ---- gather the batch (pptoas.py:384-529) --------------------
-        mask = np.zeros((nok, nchan), dtype=np.uint8)
-        init = np.zeros((nok, 5))
-        flags_b = np.zeros((nok, 5), dtype=np.int32)
-        nu_fit_b = np.zeros((nok, 3))
-        nu_out_b = np.full((nok, 3), np.nan)
-        guess_tau = np.zeros(nok)
-        for j, isub in enumerate(ok_isubs):
-            ok = np.asarray(d.ok_ichans[isub], dtype=int)
-            mask[j, ok] = 1
-            freqsx = d.freqs[isub, ok]
-            SNRsx = d.SNRs[isub, 0, ok]
-            P = d.Ps[isub]
-            if nu_fit_tuple is None:
-                nu_fit = guess_fit_freq(freqsx, SNRsx)
-                nu_fit_DM = nu_fit_GM = nu_fit_tau = nu_fit
-            else:
-                nu_fit_DM = nu_fit_GM = nu_fit_tuple[0]
-                nu_fit_tau = nu_fit_tuple[-1]
-            nu_fits_a[isub] = [nu_fit_DM, nu_fit_GM, nu_fit_tau]
-            nu_fit_b[j] = nu_fits_a[isub]
-            if nu_ref_tuple is None:
-                nu_ref_DM = nu_ref_GM = nu_ref_tau = None
-            else:
-                nu_ref_DM = nu_ref_GM = nu_ref_tuple[0]
-                nu_ref_tau = nu_ref_tuple[-1]
-                if bary and nu_ref_tau:
-                    nu_ref_tau /= d.doppler_factors[isub]
-            nu_refs_a[isub] = [nu_ref_DM, nu_ref_GM, nu_ref_tau]
-            nu_out_b[j] = [np.nan if v is None else v for v in
-                           nu_refs_a[isub]]
-            tau_guess = alpha_guess = 0.0
-            if fit_scat:
-                if self.scat_guess is not None:
-                    tg_s, tg_ref, alpha_guess = self.scat_guess
-                    tau_guess = (tg_s / P) * (nu_fit_tau / tg_ref) ** \
-                        alpha_guess
-                else:
-                    alpha_guess = self.alpha if hasattr(self, "alpha") \
-                        else scattering_alpha
-                    tau_guess = (self.gparams[1] / P) * (
-                        nu_fit_tau / self.model_nu_ref) ** alpha_guess \
-                        if hasattr(self, "gparams") else 0.0
-                guess_tau[j] = tau_guess
-                if self.log10_tau:
-                    if tau_guess == 0.0:
-                        tau_guess = nbin ** -1
-                    tau_guess = np.log10(tau_guess)
-            init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
-            if ctx["bounds"][0] is None and ctx["method"] == "TNC":
-                # pptoas.py:503-513: set once, at the first sub-int fitted
-                ctx["bounds"][0] = [
-                    (None, None), (None, None), (None, None),
-                    (0.0, None) if not self.log10_tau else
-                    (np.log10((10 * nbin) ** -1), None), (-10.0, 10.0)]
-            # the reference's fit_flags is one list that lives across
-            # sub-ints and archives: the 2-channel rule edits whatever the
-            # previous sub-int left in it (pptoas.py:519-529, SURVEY.md
-            # appendix B)
-            if len(freqsx) == 1:
-                self._ff[0] = [1, 0, 0, 0, 0]
-                if not quiet:
-                    print("TOA #%d only has 1 frequency channel...fitting "
-                          "for phase only..." % (j + 1))
-            elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
-                if self._ff[0] is None:
-                    raise UnboundLocalError(
-                        "local variable 'fit_flags' referenced before "
-                        "assignment (pptoas.py:525)")
-                self._ff[0][2] = 0
-                if not quiet:
-                    print("TOA #%d only has 2 frequency channels...fitting "
-                          "for phase and DM only..." % (j + 1))
-            else:
-                self._ff[0] = list(np.copy(self.fit_flags))
-            flags_b[j] = self._ff[0]
+        fast = self._gather_uniform(d, ok_isubs, ctx, nu_fits_a, nu_refs_a,
+                                    DM_stored) if FAST_HOST else None
+        if fast is not None:
+            mask, init, flags_b, nu_fit_b, nu_out_b, guess_tau = fast
+        else:
+            mask, init, flags_b, nu_fit_b, nu_out_b, guess_tau = \
+                self._gather_rows(d, ok_isubs, ctx, nu_fits_a, nu_refs_a,
+                                  DM_stored)
         _sp.__exit__(None, None, None)
         rank, world = (0, 1) if ctx["by_archive"] else _rank_world()
         first, count = _dist.shard(nok, rank, world)
@@ -740,6 +689,162 @@ class GetTOAs(object):
                     world=world,
                     staged=staged if staged is not None else stager.stage(rows),
                     fit_duration=fit_duration)
+
+    def _tau_guess(self, P, nu_fit_tau, nbin):
+        """pptoas.py:461-480: the initial scattering time (and index) of a
+        sub-int; returns (tau_guess linear, init tau, alpha_guess)."""
+        if self.scat_guess is not None:
+            tg_s, tg_ref, alpha_guess = self.scat_guess
+            tau_guess = (tg_s / P) * (nu_fit_tau / tg_ref) ** alpha_guess
+        else:
+            alpha_guess = self.alpha if hasattr(self, "alpha") \
+                else scattering_alpha
+            tau_guess = (self.gparams[1] / P) * (
+                nu_fit_tau / self.model_nu_ref) ** alpha_guess \
+                if hasattr(self, "gparams") else 0.0
+        lin = tau_guess
+        if self.log10_tau:
+            if tau_guess == 0.0:
+                tau_guess = nbin ** -1
+            tau_guess = np.log10(tau_guess)
+        return lin, tau_guess, alpha_guess
+
+    def _set_tnc_bounds(self, ctx, nbin):
+        if ctx["bounds"][0] is None and ctx["method"] == "TNC":
+            # pptoas.py:503-513: set once, at the first sub-int fitted
+            ctx["bounds"][0] = [
+                (None, None), (None, None), (None, None),
+                (0.0, None) if not self.log10_tau else
+                (np.log10((10 * nbin) ** -1), None), (-10.0, 10.0)]
+
+    def _gather_uniform(self, d, ok_isubs, ctx, nu_fits_a, nu_refs_a,
+                        DM_stored):
+        """_gather_rows for the usual archive, in whole-array operations:
+        every fitted sub-int has the same usable channels (at least 3, so
+        the 1/2-channel flag rules of pptoas.py:519-529 do not apply) and the
+        same channel frequencies.  The values are bit-identical to the
+        per-sub-int loop (guess_fit_freq's sums are the same pairwise row
+        sums; tests/test_host_logic.py checks it).  None when the archive is
+        not of that kind."""
+        nok = len(ok_isubs)
+        if not nok:
+            return None
+        oks = [d.ok_ichans[isub] for isub in ok_isubs]
+        ok = np.asarray(oks[0], dtype=int)
+        if len(ok) < 3 or not all(o is oks[0] or np.array_equal(o, ok)
+                                  for o in oks[1:]):
+            return None
+        rows = np.asarray(ok_isubs)
+        F = np.asarray(d.freqs)[rows]
+        if not (F == F[0]).all():
+            return None
+        nchan, nbin = d.nchan, d.nbin
+        nu_fit_tuple, nu_ref_tuple = ctx["nu_fit_tuple"], ctx["nu_ref_tuple"]
+        mask = np.zeros((nok, nchan), dtype=np.uint8)
+        mask[:, ok] = 1
+        if nu_fit_tuple is None:
+            # guess_fit_freq (pplib.py:2715-2729) of every row at once
+            freqsx = F[0, ok]
+            nu0 = (freqsx.min() + freqsx.max()) * 0.5
+            w = np.asarray(d.SNRs)[rows, 0][:, ok] * freqsx ** -2
+            nu_fit = nu0 + np.sum((freqsx - nu0) * w, axis=1) / \
+                np.sum(w, axis=1)
+            nf = [(v, v, v) for v in nu_fit]
+        else:
+            nf = [(nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1])] * nok
+        nu_fit_b = np.array(nf, dtype=float).reshape(nok, 3)
+        nu_out_b = np.full((nok, 3), np.nan)
+        bary = ctx["bary"]
+        for j, isub in enumerate(ok_isubs):
+            nu_fits_a[isub] = list(nf[j])
+            if nu_ref_tuple is None:
+                nu_refs_a[isub] = [None, None, None]
+            else:
+                nu_ref_tau = nu_ref_tuple[-1]
+                if bary and nu_ref_tau:
+                    nu_ref_tau /= d.doppler_factors[isub]
+                nu_refs_a[isub] = [nu_ref_tuple[0], nu_ref_tuple[0],
+                                   nu_ref_tau]
+                nu_out_b[j] = [np.nan if v is None else v for v in
+                               nu_refs_a[isub]]
+        init = np.zeros((nok, 5))
+        init[:, 1] = DM_stored
+        guess_tau = np.zeros(nok)
+        if ctx["fit_scat"]:
+            for j, isub in enumerate(ok_isubs):
+                guess_tau[j], init[j, 3], init[j, 4] = self._tau_guess(
+                    d.Ps[isub], nf[j][2], nbin)
+        self._set_tnc_bounds(ctx, nbin)
+        self._ff[0] = list(np.copy(self.fit_flags))
+        flags_b = np.zeros((nok, 5), dtype=np.int32)
+        flags_b[:] = self._ff[0]
+        return mask, init, flags_b, nu_fit_b, nu_out_b, guess_tau
+
+    def _gather_rows(self, d, ok_isubs, ctx, nu_fits_a, nu_refs_a, DM_stored):
+        """The batch's per-sub-int inputs (pptoas.py:384-529), one sub-int
+        at a time."""
+        quiet, fit_scat = ctx["quiet"], ctx["fit_scat"]
+        nu_fit_tuple, nu_ref_tuple, bary = ctx["nu_fit_tuple"], \
+            ctx["nu_ref_tuple"], ctx["bary"]
+        nok, nchan, nbin = len(ok_isubs), d.nchan, d.nbin
+        mask = np.zeros((nok, nchan), dtype=np.uint8)
+        init = np.zeros((nok, 5))
+        flags_b = np.zeros((nok, 5), dtype=np.int32)
+        nu_fit_b = np.zeros((nok, 3))
+        nu_out_b = np.full((nok, 3), np.nan)
+        guess_tau = np.zeros(nok)
+        for j, isub in enumerate(ok_isubs):
+            ok = np.asarray(d.ok_ichans[isub], dtype=int)
+            mask[j, ok] = 1
+            freqsx = d.freqs[isub, ok]
+            SNRsx = d.SNRs[isub, 0, ok]
+            P = d.Ps[isub]
+            if nu_fit_tuple is None:
+                nu_fit = guess_fit_freq(freqsx, SNRsx)
+                nu_fit_DM = nu_fit_GM = nu_fit_tau = nu_fit
+            else:
+                nu_fit_DM = nu_fit_GM = nu_fit_tuple[0]
+                nu_fit_tau = nu_fit_tuple[-1]
+            nu_fits_a[isub] = [nu_fit_DM, nu_fit_GM, nu_fit_tau]
+            nu_fit_b[j] = nu_fits_a[isub]
+            if nu_ref_tuple is None:
+                nu_ref_DM = nu_ref_GM = nu_ref_tau = None
+            else:
+                nu_ref_DM = nu_ref_GM = nu_ref_tuple[0]
+                nu_ref_tau = nu_ref_tuple[-1]
+                if bary and nu_ref_tau:
+                    nu_ref_tau /= d.doppler_factors[isub]
+            nu_refs_a[isub] = [nu_ref_DM, nu_ref_GM, nu_ref_tau]
+            nu_out_b[j] = [np.nan if v is None else v for v in
+                           nu_refs_a[isub]]
+            tau_guess = alpha_guess = 0.0
+            if fit_scat:
+                guess_tau[j], tau_guess, alpha_guess = self._tau_guess(
+                    P, nu_fit_tau, nbin)
+            init[j] = [0.0, DM_stored, 0.0, tau_guess, alpha_guess]
+            self._set_tnc_bounds(ctx, nbin)
+            # the reference's fit_flags is one list that lives across
+            # sub-ints and archives: the 2-channel rule edits whatever the
+            # previous sub-int left in it (pptoas.py:519-529, SURVEY.md
+            # appendix B)
+            if len(freqsx) == 1:
+                self._ff[0] = [1, 0, 0, 0, 0]
+                if not quiet:
+                    print("TOA #%d only has 1 frequency channel...fitting "
+                          "for phase only..." % (j + 1))
+            elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
+                if self._ff[0] is None:
+                    raise UnboundLocalError(
+                        "local variable 'fit_flags' referenced before "
+                        "assignment (pptoas.py:525)")
+                self._ff[0][2] = 0
+                if not quiet:
+                    print("TOA #%d only has 2 frequency channels...fitting "
+                          "for phase and DM only..." % (j + 1))
+            else:
+                self._ff[0] = list(np.copy(self.fit_flags))
+            flags_b[j] = self._ff[0]
+        return mask, init, flags_b, nu_fit_b, nu_out_b, guess_tau
 
     def _fit_archive(self, job, ctx):
         """Device stage (worker thread): this rank's share of the archive's
@@ -800,6 +905,120 @@ class GetTOAs(object):
             dev=dev)
         return _pack(res)
 
+    def _book_uniform(self, job, r, ctx, fit_duration, out):
+        """_book_archive's per-sub-int loop for an archive fitted with one
+        set of fit flags (and no flux): the result columns are scattered in
+        whole-array operations, only the TOA objects are built per sub-int.
+        Bit-identical to the loop (tests/test_host_logic.py); returns the
+        summed fit duration."""
+        d, datafile = job["d"], job["datafile"]
+        ok_isubs, nok = job["ok_isubs"], job["nok"]
+        nu_refs_a, mask = job["nu_refs_a"], job["mask"]
+        nchan, nbin = job["nchan"], job["nbin"]
+        ff = [int(v) for v in job["flags_b"][0]]
+        I = _lib.RESULT_INDEX
+        Rt = r["results"]
+        st = Rt[:, I["status"]].astype(np.int64)
+        # the messages and failures of the loop, in its order
+        nz_text = _pptl._nu_zero_text(ff)
+        for j, isub in enumerate(ok_isubs):
+            if nz_text is not None and not all(nu_refs_a[isub]):
+                print(nz_text)
+            s = int(st[j])
+            _raise_status(s)
+            if (s & 0xff) not in (0, 1, 2, 4):
+                _status_message(s & 0xff, datafile + "_%d" % isub)
+        dur = r["batch_duration"] / nok
+        for _ in range(nok):
+            fit_duration += dur
+        rows = np.asarray(ok_isubs)
+        okb = mask.astype(bool)
+        params, perrs = Rt[:, I["params"]], Rt[:, I["param_errs"]]
+        nuo = Rt[:, I["nu_out"]]
+        DMv, GMv = params[:, 1].copy(), params[:, 2].copy()
+        if self.bary:
+            dfs = np.asarray(d.doppler_factors)[rows]
+            if ff[1]:
+                DMv *= dfs
+            if ff[2]:
+                GMv *= np.array([df ** 3 for df in dfs])
+        out["phis"][rows], out["phi_errs"][rows] = params[:, 0], perrs[:, 0]
+        out["DMs"][rows], out["DM_errs"][rows] = DMv, perrs[:, 1]
+        out["GMs"][rows], out["GM_errs"][rows] = GMv, perrs[:, 2]
+        out["taus"][rows], out["tau_errs"][rows] = params[:, 3], perrs[:, 3]
+        out["alphas"][rows], out["alpha_errs"][rows] = params[:, 4], \
+            perrs[:, 4]
+        out["nfevals"][rows] = Rt[:, I["nfeval"]].astype(int)
+        out["rcs"][rows] = st & 0xff
+        out["scales"][rows] = np.where(okb, r["scales"], 0.0)
+        out["scale_errs"][rows] = np.where(okb, r["scale_errs"], 0.0)
+        out["channel_snrs"][rows] = np.where(okb, r["channel_snrs"], 0.0)
+        out["snrs"][rows] = Rt[:, I["snr"]]
+        out["red_chi2s"][rows] = Rt[:, I["red_chi2"]]
+        nfit = self.nfit
+        out["covariances"][rows] = r["covariance"][:, :nfit, :nfit]
+        F = np.asarray(d.freqs)[rows]
+        nchx = okb.sum(axis=1)
+        fmax = np.where(okb, F, -np.inf).max(axis=1)
+        fmin = np.where(okb, F, np.inf).min(axis=1)
+        snr_c, gof_c = Rt[:, I["snr"]], Rt[:, I["red_chi2"]]
+        cov01 = ctx["nu_ref_tuple"] is not None and all(ff[:2])
+        common = [("be", d.backend), ("fe", d.frontend),
+                  ("f", d.frontend + "_" + d.backend), ("nbin", nbin),
+                  ("nch", nchan)]
+        chbw = abs(d.bw) / nchan
+        TOAs, TOA_errs = out["TOAs"], out["TOA_errs"]
+        for j, isub in enumerate(ok_isubs):
+            P = d.Ps[isub]
+            phi = params[j, 0]
+            toa = d.epochs[isub] + _MJD((phi * P + d.backend_delay) /
+                                        (3600 * 24.))
+            toa_err = perrs[j, 0] * P * 1e6
+            df = d.doppler_factors[isub] if self.bary else 1.0
+            nu_refs_a[isub] = [nuo[j, 0], nuo[j, 1], nuo[j, 2]]
+            TOAs[isub], TOA_errs[isub] = toa, toa_err
+            toa_flags = {}
+            if ff[2]:
+                toa_flags["gm"] = GMv[j]
+                toa_flags["gm_err"] = perrs[j, 2]
+            if ff[3]:
+                tau, tau_err = params[j, 3], perrs[j, 3]
+                if self.log10_tau:
+                    toa_flags["scat_time"] = 10 ** tau * P / df * 1e6
+                    toa_flags["log10_scat_time"] = tau + np.log10(P / df)
+                    toa_flags["log10_scat_time_err"] = tau_err
+                else:
+                    toa_flags["scat_time"] = tau * P / df * 1e6
+                    toa_flags["scat_time_err"] = tau_err * P / df * 1e6
+                toa_flags["scat_ref_freq"] = nuo[j, 2] * df
+                toa_flags["scat_ind"] = params[j, 4]
+            if ff[4]:
+                toa_flags["scat_ind_err"] = perrs[j, 4]
+            toa_flags.update(common)
+            toa_flags["nchx"] = int(nchx[j])
+            toa_flags["bw"] = fmax[j] - fmin[j]
+            toa_flags["chbw"] = chbw
+            toa_flags["subint"] = isub
+            toa_flags["tobs"] = d.subtimes[isub]
+            toa_flags["fratio"] = fmax[j] / fmin[j]
+            toa_flags["tmplt"] = self.modelfile
+            toa_flags["snr"] = snr_c[j]
+            if cov01:
+                toa_flags["phi_DM_cov"] = r["covariance"][j, 0, 1]
+            toa_flags["gof"] = gof_c[j]
+            if ctx["print_phase"]:
+                toa_flags["phs"] = phi
+                toa_flags["phs_err"] = perrs[j, 0]
+            if ctx["print_parangle"]:
+                toa_flags["par_angle"] = d.parallactic_angles[isub]
+            for k, v in ctx["addtnl_toa_flags"].items():
+                toa_flags[k] = v
+            self.TOA_list.append(TOA(
+                datafile, nuo[j, 0], toa, toa_err, d.telescope,
+                d.telescope_code, DMv[j] if ff[1] else None,
+                perrs[j, 1] if ff[1] else None, toa_flags))
+        return fit_duration
+
     def _book_archive(self, job, r, ctx, start):
         """Per-sub-integration host bookkeeping (pptoas.py:567-792)."""
         quiet = ctx["quiet"]
@@ -840,7 +1059,19 @@ class GetTOAs(object):
         nfevals = np.zeros(nsub, dtype="int")
         rcs = np.zeros(nsub, dtype="int")
         # ---- per-sub-integration bookkeeping (pptoas.py:567-711) -----
-        for j, isub in enumerate(ok_isubs):
+        uniform = (FAST_HOST and not print_flux and nok > 0 and
+                   bool((flags_b == flags_b[0]).all()) and
+                   int(np.count_nonzero(flags_b[0])) == self.nfit and
+                   bool(mask.any(axis=1).all()))
+        if uniform:
+            fit_duration = self._book_uniform(job, r, ctx, fit_duration, dict(
+                phis=phis, phi_errs=phi_errs, TOAs=TOAs, TOA_errs=TOA_errs,
+                DMs=DMs, DM_errs=DM_errs, GMs=GMs, GM_errs=GM_errs, taus=taus,
+                tau_errs=tau_errs, alphas=alphas, alpha_errs=alpha_errs,
+                scales=scales, scale_errs=scale_errs, snrs=snrs,
+                channel_snrs=channel_snrs, red_chi2s=red_chi2s,
+                covariances=covariances, nfevals=nfevals, rcs=rcs))
+        for j, isub in enumerate([] if uniform else ok_isubs):
             fit_flags_j = [int(v) for v in flags_b[j]]
             ok = mask[j].astype(bool)
             R = r["results"][j]

@@ -83,18 +83,27 @@ def _status_message(rc, sub_id):
                          (rc, rcstring))
 
 
-def _nu_zero_messages(fit_flags, nu_outs):
-    """Reproduce get_nu_zeros' prints (pptoaslib.py:941, 947-948)."""
-    if bool(np.all(nu_outs)):
-        return
+def _nu_zero_text(fit_flags):
+    """The line get_nu_zeros prints for these fit flags when a reference
+    frequency is not given (pptoaslib.py:941, 947-948), or None."""
     flags = [int(bool(f)) for f in fit_flags]
     known = ([1, 1, 0, 0, 0], [1, 0, 1, 0, 0], [0, 0, 0, 1, 1],
              [1, 1, 0, 1, 0], [1, 1, 1, 0, 0], [1, 1, 0, 1, 1],
              [1, 1, 1, 1, 0])
     if flags == [1, 1, 1, 1, 1]:
-        print("Approximating zero-covariance frequencies...")
-    elif flags not in known and sum(flags) > 1:
-        print("No zero-covariance frequencies found.")
+        return "Approximating zero-covariance frequencies..."
+    if flags not in known and sum(flags) > 1:
+        return "No zero-covariance frequencies found."
+    return None
+
+
+def _nu_zero_messages(fit_flags, nu_outs):
+    """Reproduce get_nu_zeros' prints (pptoaslib.py:941, 947-948)."""
+    if bool(np.all(nu_outs)):
+        return
+    text = _nu_zero_text(fit_flags)
+    if text is not None:
+        print(text)
 
 
 def unpack_result(R, scales, scale_errs, channel_snrs, cov, fit_flags,

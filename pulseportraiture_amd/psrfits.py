@@ -516,150 +516,208 @@ _TLS = threading.local()
 def load_data(filename, state=None, dedisperse=False, dededisperse=False,
               tscrunch=False, pscrunch=False, fscrunch=False, rm_baseline=True,
               flux_prof=False, refresh_arch=True, return_arch=True, quiet=False,
-              dev=None):
+              dev=None, defer=False):
     """pplib.load_data (pplib.py:2749-2915) for fold-mode PSRFITS without
-    PSRCHIVE.  The DATA bytes are copied from the memory-mapped file into a
-    pinned buffer and uploaded; the device unpacks them, sums the
-    polarisations (total intensity: the only state get_TOAs asks for,
-    pscrunch=True), removes the baseline and measures every profile
+    PSRCHIVE.  The DATA bytes are read from the file into a page-locked
+    buffer and uploaded; the device unpacks them, sums the polarisations
+    (total intensity: the only state get_TOAs asks for, pscrunch=True),
+    removes the baseline and measures every profile
     (ppf_unpack_psrfits_batch), and get_noise_PS gives noise_stds (the
     reference's use_get_noise = True, pplib.py:74, 2841-2848).  The rows stay
     on the device (`subints.device_rows`); get_TOAs fits them without a
     second upload.  Options that need PSRCHIVE's predictor or state machine
     (dedisperse, tscrunch, fscrunch, other polarisation states) raise
-    NotImplementedError."""
-    import torch
-    from . import engine, pplib
+    NotImplementedError.
+
+    defer=True returns a _Pending whose finish() gives the DataBunch: the
+    read is done and the device work queued, but nothing waits for the
+    device (get_TOAs' loader thread reads the next archive meanwhile)."""
     if dedisperse or tscrunch or fscrunch:
         raise NotImplementedError("load_data(dedisperse / tscrunch / fscrunch)"
                                   " needs PSRCHIVE; the PSRFITS fast path "
                                   "reads archives as stored")
     if state not in (None, "Intensity"):
         raise NotImplementedError("state=%r needs PSRCHIVE" % state)
-    from .timeline import span
-    _sp = span("load.open")
-    _sp.__enter__()
-    f = PSRFITS(filename)
-    nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
-    if npol > 1 and not (pscrunch or state == "Intensity"):
-        raise NotImplementedError("the PSRFITS fast path returns total "
-                                  "intensity (pscrunch=True) only")
-    pt = f.pol_type.upper()
-    if npol == 1 or pt.startswith("IQUV") or pt == "INTEN":
-        pol_mode = 0
-    elif pt.startswith("AABB") or pt.startswith("AA+BB"):
-        pol_mode = 1
-    else:
-        raise NotImplementedError("POL_TYPE %s" % f.pol_type)
-    raw, edt = f.data_bytes()
-    elem = {np.dtype(">i2"): 0, np.dtype("u1"): 1, np.dtype(">f4"): 2}.get(edt)
-    if elem is None:
-        raise NotImplementedError("DATA element type %s" % edt)
-    # only the polarisations total intensity needs cross PCIe: DATA is
-    # [npol][nchan][nbin] per sub-int, so AA and BB are its first two
-    # npol blocks (2 B / sample / pol for 16-bit data)
-    nbytes = (2 if pol_mode == 1 else 1) * nchan * nbin * edt.itemsize
-    scl, offs = f.scales_offsets()
-    weights = f.weights()
-    dev = engine.device(dev)
-    _sp.__exit__(None, None, None)
-    # the scales, offsets and weights travel with the DATA bytes: one
-    # page-locked buffer per device holds [DATA rows | DAT_SCL | DAT_OFFS |
-    # weights] (float32, 256-B aligned), so the small columns cost no
-    # separate pageable copies; load_data returns only after the uploads it
-    # fed have completed
-    nraw = -(-nsub * nbytes // 256) * 256
-    nsc = nsub * npol * nchan
-    naux = 4 * (2 * nsc + nsub * nchan)
-    if not hasattr(_TLS, "streams"):
-        _TLS.streams, _TLS.pinned = {}, {}
-    with torch.cuda.device(dev):
-        st = _TLS.streams.get(dev.index)
-        if st is None:
-            st = _TLS.streams[dev.index] = torch.cuda.Stream(dev)
-        buf = _TLS.pinned.get(dev.index)
-        if buf is None or buf.numel() < nraw + naux:
-            buf = _TLS.pinned[dev.index] = torch.empty(
-                max(nraw + naux, 1), dtype=torch.uint8, pin_memory=True)
-        host = buf[:nsub * nbytes].view(nsub, nbytes)
-        aux = buf[nraw:nraw + naux].view(torch.float32)
-        a = aux.numpy()
-        a[:nsc] = scl.reshape(-1)
-        a[nsc:2 * nsc] = offs.reshape(-1)
-        a[2 * nsc:] = weights.reshape(-1)
-        dbuf = torch.empty(nraw + naux, dtype=torch.uint8, device=dev)
-        raw_d = dbuf[:nsub * nbytes].view(nsub, nbytes)
-        aux_d = dbuf[nraw:nraw + naux].view(torch.float32)
-        with torch.cuda.stream(st):
-            aux_d.copy_(aux, non_blocking=True)
+    pend = _Pending(filename, pscrunch, state, rm_baseline, quiet, dev)
+    return pend if defer else pend.finish()
 
-            # (starting each chunk's upload as soon as it lands, beside the
-            # reads of the rest, was measured slower end to end: 6.2-6.8k
-            # vs 7.7k TOAs/s in one call)
+
+# page-locked DATA buffers per device, used in turn: a buffer is refilled
+# only once the upload that read it has completed (its event)
+_PINNED = {}
+_PINNED_LOCK = threading.Lock()
+
+
+def _pinned_buffer(dev, nbytes):
+    import torch
+    with _PINNED_LOCK:
+        pool = _PINNED.setdefault(dev.index, [[None, None], [None, None]])
+        slot = pool.pop(0)
+        pool.append(slot)
+    buf, ev = slot
+    if ev is not None:
+        ev.synchronize()
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+        slot[0] = buf
+    return buf, slot
+
+
+class _Pending(object):
+    """load_data's two halves: __init__ parses the file, reads the DATA
+    bytes into a page-locked buffer and queues the upload and the device
+    unpack / baseline / noise on this thread's copy stream; finish() waits
+    for the device and builds the DataBunch."""
+
+    def __init__(self, filename, pscrunch, state, rm_baseline, quiet, dev):
+        import torch
+        from . import engine
+        from .timeline import span
+        self.filename, self.quiet = filename, quiet
+        with span("load.open"):
+            f = self.f = PSRFITS(filename)
+            nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
+            if npol > 1 and not (pscrunch or state == "Intensity"):
+                raise NotImplementedError("the PSRFITS fast path returns total "
+                                          "intensity (pscrunch=True) only")
+            pt = f.pol_type.upper()
+            if npol == 1 or pt.startswith("IQUV") or pt == "INTEN":
+                pol_mode = 0
+            elif pt.startswith("AABB") or pt.startswith("AA+BB"):
+                pol_mode = 1
+            else:
+                raise NotImplementedError("POL_TYPE %s" % f.pol_type)
+            raw, edt = f.data_bytes()
+            elem = {np.dtype(">i2"): 0, np.dtype("u1"): 1,
+                    np.dtype(">f4"): 2}.get(edt)
+            if elem is None:
+                raise NotImplementedError("DATA element type %s" % edt)
+            # only the polarisations total intensity needs cross PCIe: DATA
+            # is [npol][nchan][nbin] per sub-int, so AA and BB are its first
+            # two npol blocks (2 B / sample / pol for 16-bit data)
+            nbytes = (2 if pol_mode == 1 else 1) * nchan * nbin * edt.itemsize
+            scl, offs = f.scales_offsets()
+            self.weights = f.weights()
+            dev = engine.device(dev)
+            # host metadata that does not wait for the device
+            self.imjd, self.frac = f.epochs()
+            self.Ps = f.periods()
+            self.freqs = f.freqs()
+        # the scales, offsets and weights travel with the DATA bytes: one
+        # page-locked buffer holds [DATA rows | DAT_SCL | DAT_OFFS | weights]
+        # (float32, 256-B aligned), so the small columns cost no separate
+        # pageable copies
+        nraw = -(-nsub * nbytes // 256) * 256
+        nsc = nsub * npol * nchan
+        naux = 4 * (2 * nsc + nsub * nchan)
+        if not hasattr(_TLS, "streams"):
+            _TLS.streams = {}
+        with torch.cuda.device(dev):
+            st = _TLS.streams.get(dev.index)
+            if st is None:
+                st = _TLS.streams[dev.index] = torch.cuda.Stream(dev)
+            buf, slot = _pinned_buffer(dev, nraw + naux)
+            host = buf[:nsub * nbytes].view(nsub, nbytes)
+            aux = buf[nraw:nraw + naux].view(torch.float32)
+            a = aux.numpy()
+            a[:nsc] = scl.reshape(-1)
+            a[nsc:2 * nsc] = offs.reshape(-1)
+            a[2 * nsc:] = self.weights.reshape(-1)
             with span("load.read"):
                 f.read_data_into(nbytes, host.numpy())
-            _sp = span("load.device")
-            _sp.__enter__()
-            raw_d.copy_(host, non_blocking=True)
-            out = engine.unpack_psrfits(
-                raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
-                aux_d[nsc:2 * nsc], wts=aux_d[2 * nsc:], pol_mode=pol_mode,
-                rm_baseline=rm_baseline, dev=dev)
-            noise = engine.noise_rows(out["rows"], dev=dev)
-            # one download: stats [nsub, nchan, 3], total [nsub, nbin],
-            # noise [nsub, nchan] (all float64)
-            packed = torch.cat([out["stats"].reshape(-1),
-                                out["total"].reshape(-1), noise.reshape(-1)])
-            ev = torch.cuda.Event()
-            ev.record(st)
-        ev.synchronize()
-        packed = packed.cpu().numpy()
-        _sp.__exit__(None, None, None)
-    _sp = span("load.meta")
-    _sp.__enter__()
-    n1, n2 = nsub * nchan * 3, nsub * nbin
-    stats = packed[:n1].reshape(nsub, nchan, 3)
-    total = packed[n1:n1 + n2].reshape(nsub, nbin)
-    noise = packed[n1 + n2:].reshape(nsub, nchan)
-    del host, raw_d, aux_d
-    p, h = f.primary, f.subint.header
-    imjd, frac = f.epochs()
-    epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(imjd, frac)]
-    Ps = f.periods()
-    freqs = f.freqs()
-    weights_norm = np.where(weights == 0.0, 0.0, 1.0)
-    ok_isubs = np.compress(weights_norm.mean(axis=1), list(range(nsub)))
-    ok_ichans = [np.compress(weights_norm[isub], list(range(nchan)))
-                 for isub in range(nsub)]
-    masks = _Masks(weights_norm, nbin)
-    prof = total.sum(axis=0)
-    prof_SNR, prof_noise = _window_snr(prof)
-    telescope = str(p.get("TELESCOP", "")).strip()
-    tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
-        if f.subint.has("TSUBINT") else np.zeros(nsub)
-    par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
-        if f.subint.has("PAR_ANG") else np.zeros(nsub)
-    DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
-    if not quiet:
-        print("\nReading data from %s on source %s (PSRFITS fast path)..." %
-              (filename, p.get("SRC_NAME", "")))
-    data = pplib.DataBunch(
-        arch=None, backend=str(p.get("BACKEND", "")).strip(),
-        backend_delay=float(p.get("BE_DELAY", 0.0)),
-        bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub),
-        doppler_known=False, DM=DM,
-        dmc=0, epochs=epochs, filename=filename, flux_prof=np.array([]),
-        freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
-        integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
-        nchan=nchan, noise_stds=noise[:, None, :], npol=1, nsub=nsub,
-        nu0=float(p.get("OBSFREQ", freqs.mean())), ok_ichans=ok_ichans,
-        ok_isubs=ok_isubs, parallactic_angles=par,
-        phases=pplib.get_bin_centers(nbin), prof=prof / max(1.0, weights_norm.sum()),
-        prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=Ps,
-        SNRs=stats[:, None, :, 2].copy(), source=str(p.get("SRC_NAME", "")).strip(),
-        state="Intensity", subints=DeviceRows(out["rows"], ev),
-        subtimes=list(tsub), telescope=telescope,
-        telescope_code=_telescope_code(telescope), weights=weights)
-    f.close()
-    _sp.__exit__(None, None, None)
-    return data
+            with span("load.queue"):
+                dbuf = torch.empty(nraw + naux, dtype=torch.uint8, device=dev)
+                raw_d = dbuf[:nsub * nbytes].view(nsub, nbytes)
+                aux_d = dbuf[nraw:nraw + naux].view(torch.float32)
+                with torch.cuda.stream(st):
+                    aux_d.copy_(aux, non_blocking=True)
+                    raw_d.copy_(host, non_blocking=True)
+                    up = torch.cuda.Event()
+                    up.record(st)
+                    slot[1] = up                    # the buffer is free after it
+                    out = engine.unpack_psrfits(
+                        raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
+                        aux_d[nsc:2 * nsc], wts=aux_d[2 * nsc:],
+                        pol_mode=pol_mode, rm_baseline=rm_baseline, dev=dev)
+                    noise = engine.noise_rows(out["rows"], dev=dev)
+                    # one download: stats [nsub, nchan, 3], total [nsub,
+                    # nbin], noise [nsub, nchan] (all float64)
+                    packed = torch.cat([out["stats"].reshape(-1),
+                                        out["total"].reshape(-1),
+                                        noise.reshape(-1)])
+                    self.packed_h = torch.empty(packed.shape, dtype=packed.dtype,
+                                                pin_memory=True)
+                    self.packed_h.copy_(packed, non_blocking=True)
+                    self.ev = torch.cuda.Event()
+                    self.ev.record(st)
+            self.rows = out["rows"]
+            self._keep = (dbuf, packed)
+        # the rest of the metadata, and the unmap (milliseconds for a large
+        # file), on this (loading) thread too
+        with span("load.close"):
+            self.tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
+                if f.subint.has("TSUBINT") else np.zeros(nsub)
+            self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
+                if f.subint.has("PAR_ANG") else np.zeros(nsub)
+            del raw
+            f.close()
+
+    def finish(self):
+        from . import pplib
+        from .timeline import span
+        with span("load.wait"):
+            self.ev.synchronize()
+        self._keep = None
+        with span("load.meta"):
+            return self._bunch()
+
+    def _bunch(self):
+        from . import pplib
+        f, filename, weights = self.f, self.filename, self.weights
+        nsub, nchan, nbin = f.nsub, f.nchan, f.nbin
+        packed = self.packed_h.numpy()
+        n1, n2 = nsub * nchan * 3, nsub * nbin
+        stats = packed[:n1].reshape(nsub, nchan, 3)
+        total = packed[n1:n1 + n2].reshape(nsub, nbin)
+        noise = packed[n1 + n2:].reshape(nsub, nchan)
+        p, h = f.primary, f.subint.header
+        epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(self.imjd,
+                                                                self.frac)]
+        freqs = self.freqs
+        weights_norm = np.where(weights == 0.0, 0.0, 1.0)
+        ok_isubs = np.compress(weights_norm.mean(axis=1), list(range(nsub)))
+        chans = np.arange(nchan)
+        okc = weights_norm != 0.0
+        if okc.all():
+            ok_ichans = [chans] * nsub
+        else:
+            ok_ichans = [chans[okc[isub]] for isub in range(nsub)]
+        masks = _Masks(weights_norm, nbin)
+        prof = total.sum(axis=0)
+        prof_SNR, prof_noise = _window_snr(prof)
+        telescope = str(p.get("TELESCOP", "")).strip()
+        tsub, par = self.tsub, self.par
+        DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
+        if not self.quiet:
+            print("\nReading data from %s on source %s (PSRFITS fast "
+                  "path)..." % (filename, p.get("SRC_NAME", "")))
+        data = pplib.DataBunch(
+            arch=None, backend=str(p.get("BACKEND", "")).strip(),
+            backend_delay=float(p.get("BE_DELAY", 0.0)),
+            bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub),
+            doppler_known=False, DM=DM,
+            dmc=0, epochs=epochs, filename=filename, flux_prof=np.array([]),
+            freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
+            integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
+            nchan=nchan, noise_stds=noise[:, None, :], npol=1, nsub=nsub,
+            nu0=float(p.get("OBSFREQ", freqs.mean())), ok_ichans=ok_ichans,
+            ok_isubs=ok_isubs, parallactic_angles=par,
+            phases=pplib.get_bin_centers(nbin),
+            prof=prof / max(1.0, weights_norm.sum()),
+            prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=self.Ps,
+            SNRs=stats[:, None, :, 2].copy(),
+            source=str(p.get("SRC_NAME", "")).strip(),
+            state="Intensity", subints=DeviceRows(self.rows, self.ev),
+            subtimes=list(tsub), telescope=telescope,
+            telescope_code=_telescope_code(telescope), weights=weights)
+        return data

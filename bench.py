@@ -19,6 +19,7 @@ Rank 0 prints ONE JSON line.  It carries `roofline` for the dominant kernel
 and `cpu_baseline` (the NumPy/SciPy oracle on a bounded sample, 1 core).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -906,7 +907,12 @@ def main():
                mean_passes_per_fit=round(mean_passes, 3),
                mean_evals_per_fit=round(mean_nfev, 3),
                fits_converged_frac=round(float(np.mean(
-                   (status & 0xff) == 2)), 5))
+                   (status & 0xff) == 2)), 5),
+               # the gathered result records of the last step (every sub-int
+               # of every rank, global order): equal across world sizes
+               # (tests/test_gpu_dist.py)
+               results_sha256=hashlib.sha256(
+                   np.ascontiguousarray(res_np).tobytes()).hexdigest())
     # sanity: fitted DM / phase agree with the injected truths
     if rank == 0:
         dm = res_np[:count, I["params"]][:, 1]

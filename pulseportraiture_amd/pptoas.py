@@ -614,8 +614,11 @@ class GetTOAs(object):
             return None
         d = data
         nsub, nchan, nbin = d.nsub, d.nchan, d.nbin
-        if bary and not d.get("doppler_known", True):
+        if bary and not d.get("doppler_known", True) and \
+                not ctx.get("bary_warned"):
             # psrfits.load_data has no ephemeris: its Doppler factors are 1
+            # (warned once per get_TOAs call, naming the first such archive)
+            ctx["bary_warned"] = True
             warnings.warn("%s: Doppler factors unknown on the PSRFITS fast "
                           "path (no PSRCHIVE ephemeris); DM, GM and nu_ref_tau "
                           "stay topocentric (bary=True has no effect)" %

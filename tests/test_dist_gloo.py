@@ -314,3 +314,175 @@ def test_gettoas_archive_sharding_equals_serial(nfile, skip):
     assert got[0][0] == list(range(len(got[0][0])))
     for r in (0, 1):
         assert got[r][1] == ref
+
+
+# ---------------------------------------------------------------------------
+# GetTOAs' own batch gathering, sharding, table all-gather and bookkeeping
+# for the scattering fits (configs[2] full: phi, DM, GM, tau, alpha;
+# configs[4] scat: phi, DM, tau, alpha), with the device fit replaced by a
+# deterministic CPU function of each sub-int's inputs: two ranks over gloo
+# end with the serial run's attributes and TOAs, bit for bit
+# ---------------------------------------------------------------------------
+def _fit_fake(data, models, freqs, Ps, init, flags, nu_fits=None,
+              nu_outs=None, errs=None, chan_mask=None, guess_tau=None,
+              guess_weights=None, **kw):
+    """ppf_fit_batch's output records as a function of the per-sub-int
+    inputs only (never of the row's position in the batch)."""
+    from pulseportraiture_amd import _lib
+    x = np.asarray(data, dtype=np.float64)
+    n, nchan = x.shape[:2]
+    init, flags = np.asarray(init, float), np.asarray(flags, float)
+    nu_fits, nu_outs = np.asarray(nu_fits, float), np.asarray(nu_outs, float)
+    mask = np.asarray(chan_mask, float)
+    tg = np.zeros(n) if guess_tau is None else np.asarray(guess_tau, float)
+    rs = (x.sum(axis=2) * mask).sum(axis=1)
+    I = _lib.RESULT_INDEX
+    R = np.zeros((n, _lib.RESULT_DOUBLES))
+    R[:, I["params"]] = init + 1e-6 * rs[:, None] * flags
+    R[:, I["param_errs"]] = 1e-3 + 1e-4 * flags + tg[:, None]
+    R[:, I["nu_out"]] = np.where(np.isnan(nu_outs), nu_fits, nu_outs)
+    R[:, I["nu_fit"]] = nu_fits
+    R[:, I["chi2"]] = rs
+    R[:, I["red_chi2"]] = 1.0 + 1e-3 * mask.sum(axis=1)
+    R[:, I["snr"]] = 10.0 + 1e-3 * rs
+    R[:, I["nfeval"]] = 5 + flags.sum(axis=1)
+    R[:, I["status"]] = 2
+    cov = 1e-6 * (init[:, :, None] + init[:, None, :] + np.eye(5))
+    t = torch.from_numpy
+    return dict(results=t(R), scales=t(x.mean(axis=2) * mask),
+                scale_errs=t(np.asarray(errs, float) * mask),
+                channel_snrs=t(np.asarray(guess_weights, float) *
+                               np.asarray(freqs, float) * 1e-3),
+                covariance=t(cov))
+
+
+class _CPUStaged(object):
+    def __init__(self, rows):
+        self.rows = rows
+
+    def wait(self):
+        return torch.from_numpy(np.ascontiguousarray(self.rows))
+
+    def release(self):
+        self.rows = None
+
+
+class _CPUStager(object):
+    def stage(self, rows):
+        return _CPUStaged(np.asarray(rows))
+
+    def close(self):
+        pass
+
+
+def _scat_archives(nfile):
+    from pulseportraiture_amd.pplib import DataBunch, MJD
+    out = {}
+    for f in range(nfile):
+        rng = np.random.default_rng(300 + f)
+        nsub, nchan, nbin = 5, 6, 32
+        ok = np.arange(nchan) if f % 2 == 0 else np.array([0, 1, 2, 4, 5])
+        wts = np.ones((nsub, nchan))
+        wts[:, np.setdiff1d(np.arange(nchan), ok)] = 0.0
+        name = "s%d.fits" % f
+        out[name] = DataBunch(
+            arch=None, backend="be", backend_delay=0.0, bw=400.0,
+            doppler_factors=1.0 + rng.uniform(-1e-4, 1e-4, nsub), DM=30.0,
+            dmc=0, epochs=[MJD(57000 + f, 0.01 * i) for i in range(nsub)],
+            filename=name, flux_prof=np.array([]),
+            freqs=np.tile(np.linspace(400.0, 800.0, nchan), (nsub, 1)),
+            frontend="fe", integration_length=50.0, masks=None, nbin=nbin,
+            nchan=nchan, noise_stds=rng.uniform(0.5, 1.5, (nsub, 1, nchan)),
+            npol=1, nsub=nsub, nu0=600.0, ok_ichans=[ok] * nsub,
+            ok_isubs=np.arange(nsub), parallactic_angles=np.zeros(nsub),
+            phases=np.arange(nbin) / nbin, prof=np.zeros(nbin),
+            prof_noise=1.0, prof_SNR=20.0,
+            Ps=np.full(nsub, 0.005) + 1e-6 * f,
+            SNRs=rng.uniform(5, 50, (nsub, 1, nchan)), source="J0000+0000",
+            state="Intensity",
+            subints=rng.normal(size=(nsub, 1, nchan, nbin)).astype(np.float32),
+            subtimes=[10.0] * nsub, telescope="GBT", telescope_code="1",
+            weights=wts)
+    return out
+
+
+def _scat_gettoas(nfile):
+    from pulseportraiture_amd import pptoas
+
+    class G(pptoas.GetTOAs):
+        def __init__(self):
+            for a in pptoas._ATTRS:
+                setattr(self, a, [])
+            self.datafiles = ["s%d.fits" % i for i in range(nfile)]
+            self.quiet = True
+            self.modelfile = "t.gmodel"
+            self.gparams = [0.0, 2e-3]
+            self.model_nu_ref = 600.0
+            self.ird = {"DM": 0.0, "wids": [], "irf_types": []}
+
+        def _models(self, d, ok_isubs, fit_scat, quiet, host=True):
+            return (np.zeros((1, d.nchan, d.nbin)),
+                    np.zeros(len(ok_isubs), dtype=np.int32))
+    return G()
+
+
+def _scat_run(mode, nfile):
+    from pulseportraiture_amd import engine, pptoas
+    files = _scat_archives(nfile)
+    saved = (pptoas.load_data, pptoas._Stager, pptoas._worker_stream,
+             engine.device, engine.fit_batch)
+    pptoas.load_data = lambda fn, **kw: files[fn]
+    pptoas._Stager = _CPUStager
+    pptoas._worker_stream = lambda dev: None
+    engine.device = lambda *a, **k: -1       # torch.cuda.device(-1): no-op
+    engine.fit_batch = _fit_fake
+    try:
+        gt = _scat_gettoas(nfile)
+        gt.get_TOAs(quiet=True, fit_DM=True, fit_GM=(mode == "full"),
+                    fit_scat=True)
+        return _summary(gt)
+    finally:
+        (pptoas.load_data, pptoas._Stager, pptoas._worker_stream,
+         engine.device, engine.fit_batch) = saved
+
+
+def _scat_worker(rank, world, port, mode, nfile, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    sys.path.insert(0, os.path.dirname(__file__))
+    import test_dist_gloo as T
+    pdist.init("gloo")
+    q.put((rank, T._scat_run(mode, nfile)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,nfile", [("full", 3), ("scat", 3),
+                                        ("scat", 1)])
+def test_gettoas_scattering_fits_sharded_equal_serial(mode, nfile):
+    """full (fit_DM + fit_GM: sharded by sub-int in every archive) and scat
+    (3 archives: sharded by archive; 1 archive: by sub-int), with ragged
+    shards (5 sub-ints) and zapped channels: the 2-rank attributes, the
+    scattering TOA flags and the tau guesses each sub-int was fitted from
+    equal the serial run's."""
+    serial = _scat_run(mode, nfile)
+    assert len(serial["TOA_list"]) == 5 * nfile
+    assert "scat_time" in serial["TOA_list"][0][5]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scat_worker,
+                         args=(r, 2, port, mode, nfile, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        for k in serial:
+            if k != "fit_durations":            # wall-clock times
+                assert repr(got[r][k]) == repr(serial[k]), (r, k)

@@ -113,16 +113,34 @@ def _bench_rank(rank, world, port, args):
         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
 
 
-@pytest.mark.parametrize("fit", ["phase+DM", "align", "gettoas"])
+def _bench_one(args):
+    import json
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, os.path.join(
+        os.path.dirname(HERE), "bench.py")] + args, stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("fit", ["phase+DM", "full", "scat", "align",
+                                 "gettoas"])
 def test_bench_two_ranks_rehearsal(fit):
     """bench.py's N > 1 path (sharding, the result all-gather, max-over-ranks
     timing, rank-0 JSON) run as two processes on the box's one GPU over gloo,
-    as the driver's multi-GPU runs use it over RCCL (one rank per GPU)."""
+    as the driver's multi-GPU runs use it over RCCL (one rank per GPU).  The
+    fit modes' gathered result records are bit-identical to one rank fitting
+    all the sub-ints (results_sha256)."""
     import json
     port = _free_port()
-    args = ["--gpus", "2", "--dist-backend", "gloo", "--nsub", "48",
-            "--nchan", "64", "--nbin", "512", "--steps", "1", "--warmup",
-            "1", "--passes", "1", "--cpu-sample", "0", "--fit", fit]
+    nsub = 24 if fit in ("full", "scat") else 48
+    common = ["--nchan", "64", "--nbin", "512", "--steps", "1", "--warmup",
+              "1", "--passes", "1", "--cpu-sample", "0", "--fit", fit]
+    args = ["--gpus", "2", "--dist-backend", "gloo", "--nsub",
+            str(nsub)] + common
     if fit == "gettoas":
         # 6 archives of 8 sub-ints: archive-sharded GetTOAs (each rank
         # loads only its own three; the loader asserts it)
@@ -137,5 +155,9 @@ def test_bench_two_ranks_rehearsal(fit):
     assert not any(ln.startswith("{") for ln in outs[1].splitlines())
     if fit == "phase+DM":
         assert d["fits_converged_frac"] == 1.0
+    if fit in ("phase+DM", "full", "scat"):
+        one = _bench_one(["--nsub", str(2 * nsub)] + common)
+        assert one["n_gpus"] == 1
+        assert d["results_sha256"] == one["results_sha256"]
     if fit == "gettoas":
         assert d["toas"] == 48 and d["config"]["sharding"] == "archives"

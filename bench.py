@@ -140,8 +140,13 @@ def _oracle_chunk(args):
     from threadpoolctl import threadpool_limits
     with threadpool_limits(1):
         t0 = time.perf_counter()
-        _oracle_toas(O, data, model, freqs, P, DM0, flags)
-        return time.perf_counter() - t0
+        out = _oracle_toas(O, data, model, freqs, P, DM0, flags)
+        return time.perf_counter() - t0, {k: out[k] for k in _PARITY_KEYS}
+
+
+# the oracle outputs parity_vs_oracle reads
+_PARITY_KEYS = ("phis", "phi_errs", "DMs", "DM_errs", "nu_refs", "param_errs",
+                "red_chi2s", "GMs", "taus", "alphas")
 
 
 def _cpu_model():
@@ -204,13 +209,23 @@ def cpu_baseline(batch, nsample, nchan, nbin, workers, mode="phase+DM",
             pool.map(_noop,
                      range(workers), chunksize=1)   # every worker started
             t0 = time.perf_counter()
-            pool.map(_oracle_chunk, jobs, chunksize=1)
+            res = pool.map(_oracle_chunk, jobs, chunksize=1)
             wall = time.perf_counter() - t0
         out["all_core"] = dict(value=n_all / wall, workers=workers,
                                cores=workers,
                                sample="%d sub-ints, %d processes x 1 thread "
                                       "(the box's CPU share), %.1f s wall" %
                                       (n_all, workers, wall))
+        # the workers' fits (worker i fitted sub-ints i, i + workers, ...)
+        # in global order: the parity sample of the all-core run
+        allref = {}
+        for k in _PARITY_KEYS:
+            first = np.asarray(res[0][1][k])
+            a = np.zeros((n_all,) + first.shape[1:])
+            for i in range(workers):
+                a[i::workers] = np.asarray(res[i][1][k])
+            allref[k] = a
+        ref = dict(ref, all_core=allref, n_all=n_all)
     return out, ref
 
 
@@ -282,12 +297,23 @@ def bench_align(args):
     prof = ded.mean(dim=0).cpu().numpy()
     model0 = np.tile(prof, (nchan, 1))
     comm = dist.is_dist()
+    from pulseportraiture_amd import _lib
+    lib = _lib.load()
+    lctx = _lib.context(dev.index)
+    lib.ppf_set_profiling(lctx, 1)
+    acc_ev = []                     # HIP events around ppf_align_accum
 
-    def step(model_port):
+    def step(model_port, R=R, timed=True):
         out = torch.zeros((nchan, nbin), dtype=torch.float64, device=dev)
         wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
         ph, w = ppalign._fit_and_weights(R, model_port, True, nbin, dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), \
+            torch.cuda.Event(enable_timing=True)
+        e0.record()
         engine.align_accum(R.data[:, 0], ph, w, out, wsum, dev=dev)
+        e1.record()
+        if timed:
+            acc_ev.append((e0, e1))
         ppalign.raise_pending(R)
         if comm:
             dist.allreduce_sum_(out, wsum)
@@ -300,6 +326,7 @@ def bench_align(args):
     torch.cuda.synchronize(dev)
     dist.barrier()
     m = model0 if args.warmup == 0 else m
+    del acc_ev[:]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         m = step(m)
@@ -307,6 +334,49 @@ def bench_align(args):
     dist.barrier()
     dt = dist.max_over_ranks(time.perf_counter() - t0, dev)
     value = total * args.steps / dt
+    # ---- per-kernel times of the timed region (HIP events on the stream) ---
+    ncalls = args.steps                     # one ppf_fit_batch per iteration
+    khist = np.zeros((ncalls, 2))
+    kgot = lib.ppf_kernel_ms_history(lctx, ncalls, khist.ctypes.data)
+    kern_ms = khist[:kgot].sum(axis=0)
+    acc_ms = float(sum(a.elapsed_time(b) for a, b in acc_ev))
+    nharm = nbin // 2 + 1
+    nblkd = (nchan + 127) // 128
+    # ALGORITHMIC bytes per archive: k_xmom_g reads the
+    # f32 rows and the channel derivatives, writes 32 complex moments + 4
+    # scalars + the centre residual per channel (+ the model spectra once per
+    # launch); k_dsum_w reads the rows and writes the block guess profiles;
+    # k_align reads the rows and the channel phases / weights (+ writes the
+    # template and its weights once per launch)
+    xmom_unit = nchan * nbin * 4 + nchan * 16 + nchan * (32 * 16 + 4 * 8 + 8)
+    dsum_unit = nchan * nbin * 4 + nblkd * nbin * 8 + nblkd * 16
+    acc_unit = nchan * nbin * 4 + nchan * 16
+    L2N = (nbin // 4).bit_length()
+    kern = {
+        "xmom": dict(name="k_xmom_g<%d, 0, true, true>" % L2N, ms=kern_ms[0],
+                     unit=xmom_unit, bytes=ncalls * (count * xmom_unit +
+                                                     nchan * nharm * 16)),
+        "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
+                     bytes=ncalls * count * dsum_unit),
+        "accum": dict(name="k_align", ms=acc_ms, unit=acc_unit,
+                      bytes=ncalls * (count * acc_unit + nchan * nbin * 8 +
+                                      nchan * 8)),
+    }
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    dk = kern[dom]
+    achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
+    roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
+                unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                traffic=None, kernel=dk["name"],
+                algorithmic_bytes_per_launch=dk["bytes"] / ncalls,
+                algorithmic_bytes_per_unit=dk["unit"],
+                avg_launch_ms=round(dk["ms"] / ncalls, 4), launches=ncalls,
+                units_per_launch=count)
+    kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),
+                       avg_launch_ms=round(float(v["ms"]) / ncalls, 4),
+                       gbs=(None if not v["ms"] else
+                            round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
+               for k, v in kern.items()}
     fitstats = {}
     lr = R.__dict__.get("_dev_inputs", {}).get("last_results")
     if lr is not None:
@@ -330,11 +400,59 @@ def bench_align(args):
                                                           nbin),
                            nsub_per_gpu=args.nsub, nchan=nchan, nbin=nbin,
                            fit="align", parallelism="dp%d" % world),
-               roofline=None, cpu_baseline=None,
+               roofline=roof, kernels=kernels, cpu_baseline=None,
                template_peak=float(torch.as_tensor(m).abs().max()), **fitstats)
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"], out["parity"] = _align_cpu_baseline(
+            b, noise, model0, min(args.cpu_sample, count), step, R, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.barrier()
+
+
+def _align_cpu_baseline(b, noise, model0, nsamp, step, R, dev):
+    """The oracle's align_archives (ppalign.py:65-257 restated) for ONE
+    iteration over the first `nsamp` archives, one core, from the same
+    initial template; parity: the device iteration over the same archives
+    (its normalised template) against the oracle's."""
+    import torch
+    from types import SimpleNamespace
+    import oracle.ppfit_oracle as O
+    from threadpoolctl import threadpool_limits
+    from pulseportraiture_amd import synth
+    data = b["data"][:nsamp].double().cpu().numpy()
+    nchan, nbin = data.shape[1:]
+    arch = [SimpleNamespace(
+        subints=data[i][None, None], weights=np.ones((1, nchan)),
+        freqs=b["freqs"][None], Ps=b["P"][i:i + 1],
+        SNRs=np.ones((1, 1, nchan)), noise_stds=noise[i][None, None],
+        ok_isubs=[0], ok_ichans=[np.arange(nchan)], DM=synth.DM0, dmc=0,
+        nbin=nbin) for i in range(nsamp)]
+    mdl = SimpleNamespace(masks=np.ones((1, 1, nchan, nbin)),
+                          subints=model0[None, None], freqs=b["freqs"][None],
+                          ok_ichans=[np.arange(nchan)])
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        ref, _ = O.align_archives(arch, mdl, fit_dm=True, niter=1)
+        dt = time.perf_counter() - t0
+    Rs = SimpleNamespace(**{k: v[:nsamp] for k, v in R.__dict__.items()
+                            if not k.startswith("_") and k != "n"})
+    Rs.n = nsamp
+    got = step(model0, R=Rs, timed=False).cpu().numpy()
+    scale = float(np.abs(ref[0]).max())
+    dev_max = float(np.abs(got - ref[0]).max()) / scale
+    base = dict(value=nsamp / dt, unit="archive-iterations/s", cores=1,
+                kind="port",
+                sample="%d archives of %dch x %dbin, one oracle "
+                       "align_archives iteration (guess + phase/DM fit + "
+                       "rotate-and-sum per archive), %.1f s" %
+                       (nsamp, nchan, nbin, dt),
+                cpu_model=_cpu_model(), nproc=os.cpu_count())
+    parity = dict(n=nsamp, max_abs_diff_over_peak=dev_max,
+                  ok=bool(dev_max < 1e-6),
+                  against="oracle align_archives iteration on the "
+                          "cpu_baseline archives (same initial template)")
+    return base, parity
 
 
 class _Epoch(object):
@@ -932,7 +1050,8 @@ def main():
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         # scattering fits take ~10x longer on the CPU: a 24x smaller sample
         nsamp = min(args.cpu_sample if not scat_fit else
-                    max(1, args.cpu_sample // 24), count)
+                    (max(4, args.cpu_sample // 12) if nchan * nbin <= 1 << 20
+                     else 1), count)
         out["cpu_baseline"], oref = cpu_baseline(
             batch, nsamp, nchan, nbin, args.cpu_workers, mode=args.fit,
             flags=FIT["flags"], per_worker=4 if not scat_fit else 1)
@@ -940,6 +1059,12 @@ def main():
                                        1)
         out["parity"] = parity_vs_oracle(res_np[:nsamp], oref, batch["P"],
                                          FIT["flags"])
+        if "all_core" in oref:
+            # and the all-core run's sub-ints (C5: 16 sub-ints, where one
+            # single-core fit takes ~28 s)
+            na = oref["n_all"]
+            out["parity_all_core"] = parity_vs_oracle(
+                res_np[:na], oref["all_core"], batch["P"], FIT["flags"])
     else:
         out["cpu_baseline"] = None
     if rank == 0:

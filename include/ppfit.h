@@ -324,7 +324,8 @@ int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, c
  * the unpacking, baseline removal, pscrunch and per-profile statistics of
  * pplib.load_data, pplib.py:2749-2915, for fold-mode PSRFITS): raw SUBINT
  * DATA bytes as stored in the file (big-endian; elem 0 = int16, 1 = uint8,
- * 2 = float32), one block of sub_stride bytes per sub-int holding
+ * 2 = float32; 3 = native little-endian float32 rows, load_data's second
+ * statistics pass over dedispersed / tscrunched rows), one block of sub_stride bytes per sub-int holding
  * [npol][nchan][nbin] samples (at least the pols used: 1, or 2 with
  * pol_mode 1; scl / offs still index all npol), become float32 rows
  *   out[s][n][b] = sum_p (DATA * DAT_SCL + DAT_OFFS)   (float32 arithmetic)

@@ -741,7 +741,7 @@ int ppf_unpack_psrfits_batch(ppf_ctx *ctx, int32_t nsub, int32_t npol, int32_t n
                              int32_t *wstart, void *workspace, size_t workspace_bytes,
                              void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (nsub < 0 || npol < 1 || nchan < 1 || nbin < 2 || elem < 0 || elem > 2 || pol_mode < 0 ||
+    if (nsub < 0 || npol < 1 || nchan < 1 || nbin < 2 || elem < 0 || elem > 3 || pol_mode < 0 ||
         pol_mode > 1 || (pol_mode == 1 && npol < 2))
         return fail(ctx, PPF_EINVAL, "bad unpack arguments (npol=%d nchan=%d nbin=%d elem=%d "
                     "pol_mode=%d)", npol, nchan, nbin, elem, pol_mode);

@@ -6,7 +6,9 @@
 // per-profile baseline statistics and S/N.
 //
 //   k_unpack      WG = (sub-int, block of kUnpackChans channels), thread =
-//                 bin pairs: big-endian int16 / uint8 / float32 samples ->
+//                 bin pairs: big-endian int16 / uint8 / float32 samples (or
+//                 native float32 rows: load_data's statistics pass after
+//                 dedispersion / tscrunch, DAT_SCL = 1, DAT_OFFS = 0) ->
 //                 DATA * DAT_SCL + DAT_OFFS in float32 arithmetic (two
 //                 roundings, no fma: PSRCHIVE's loader) -> total intensity
 //                 (npol 1: itself; AA+BB / AABBCRCI: AA + BB; IQUV: I) ->
@@ -34,6 +36,7 @@ __device__ __forceinline__ float sample_f32(const uint8_t *p, int elem, int64_t 
         return (float)(int16_t)__builtin_bswap16(u);
     }
     if (elem == 1) return (float)p[i];
+    if (elem == 3) return reinterpret_cast<const float *>(p)[i];   // native rows
     const uint32_t u = __builtin_bswap32(reinterpret_cast<const uint32_t *>(p)[i]);
     return __uint_as_float(u);
 }

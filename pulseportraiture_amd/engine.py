@@ -464,6 +464,31 @@ def noise_rows(rows, frac=4, dev=None):
     return out.reshape(shape[:-1])
 
 
+def noise_len_supported(n):
+    """Row lengths ppf_noise_batch transforms (its LDS FFT): even, 32..8192,
+    n/2 = 2^a 3^b 5^c 7^d."""
+    if n % 2 or n < 32 or n > 8192:
+        return False
+    m = n // 2
+    for r in (2, 3, 5, 7):
+        while m % r == 0:
+            m //= r
+    return m == 1
+
+
+def noise_long(row, frac=4, dev=None):
+    """get_noise_PS of ONE row of any length (pplib.py:2334-2338): the mean
+    power of the top 1/frac of the rFFT, the transform by the device FFT
+    library (torch.fft -> rocFFT), float64."""
+    dev = device(dev)
+    x = to_dev(row, dev, torch.float64).reshape(-1)
+    n = x.numel()
+    F = torch.fft.rfft(x)
+    pows = (F.real * F.real + F.imag * F.imag) / n
+    kc = int((1 - frac ** -1) * pows.numel())
+    return float(torch.sqrt(pows[kc:].mean()))
+
+
 def unpack_psrfits(raw, elem, npol, nchan, nbin, scl, offs, wts=None,
                    pol_mode=0, rm_baseline=True, dev=None):
     """ppf_unpack_psrfits_batch: raw DATA bytes [nsub, >= npol nchan nbin

@@ -304,6 +304,21 @@ def polyco_freq(tab, imjd, frac):
     return f0 + df / 60.0
 
 
+class _PolycoRows(object):
+    """The POLYCO columns polyco_freq reads, copied out of the file map
+    (so the map can be closed on the loading thread)."""
+
+    def __init__(self, tab):
+        self._c = {k: np.array(tab.column(k)) for k in
+                   ("REF_MJD", "REF_F0", "NCOEF", "COEFF") if tab.has(k)}
+
+    def has(self, name):
+        return name in self._c
+
+    def column(self, name):
+        return self._c[name]
+
+
 def unpack_host(raw, dtype, scl, offs, npol, nchan, nbin):
     """NumPy restatement of the device unpack (tests): float32 value =
     DATA * DAT_SCL + DAT_OFFS (two float32 roundings, no fused
@@ -525,20 +540,34 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     (ppf_unpack_psrfits_batch), and get_noise_PS gives noise_stds (the
     reference's use_get_noise = True, pplib.py:74, 2841-2848).  The rows stay
     on the device (`subints.device_rows`); get_TOAs fits them without a
-    second upload.  Options that need PSRCHIVE's predictor or state machine
-    (dedisperse, tscrunch, fscrunch, other polarisation states) raise
+    second upload.
+
+    dedisperse / tscrunch follow load_data's order (pplib.py:2786-2793:
+    dedisperse, remove the baseline, tscrunch), on the device: every
+    channel rotated by the dispersion delay of the stored DM to the centre
+    frequency (OBSFREQ), per sub-int period, with the reference's
+    rotate_data constant (ppf_rotate_batch), the baseline then measured and
+    removed on the dedispersed rows; tscrunch = the DAT_WTS-weighted mean of
+    the sub-ints per channel (ppf_align_accum with zero phases; PSRCHIVE's
+    weighted Profile average), its weight the summed weights, its epoch the
+    middle of the span, its period the predictor's (POLYCO) there or the
+    duration-weighted mean PERIOD.  What PSRCHIVE itself would give (its
+    dispersion constant, epoch and period conventions) is unpinned here:
+    PSRCHIVE is absent and the reference holds no PSRFITS fixture.  A file
+    whose data are already dedispersed is not recognised (dmc = 0 on load);
+    dededisperse is a no-op.  fscrunch and other polarisation states raise
     NotImplementedError.
 
     defer=True returns a _Pending whose finish() gives the DataBunch: the
     read is done and the device work queued, but nothing waits for the
     device (get_TOAs' loader thread reads the next archive meanwhile)."""
-    if dedisperse or tscrunch or fscrunch:
-        raise NotImplementedError("load_data(dedisperse / tscrunch / fscrunch)"
-                                  " needs PSRCHIVE; the PSRFITS fast path "
-                                  "reads archives as stored")
+    if fscrunch:
+        raise NotImplementedError("load_data(fscrunch) needs PSRCHIVE; the "
+                                  "PSRFITS fast path keeps every channel")
     if state not in (None, "Intensity"):
         raise NotImplementedError("state=%r needs PSRCHIVE" % state)
-    pend = _Pending(filename, pscrunch, state, rm_baseline, quiet, dev)
+    pend = _Pending(filename, pscrunch, state, rm_baseline, quiet, dev,
+                    dedisperse=bool(dedisperse), tscrunch=bool(tscrunch))
     return pend if defer else pend.finish()
 
 
@@ -569,11 +598,13 @@ class _Pending(object):
     unpack / baseline / noise on this thread's copy stream; finish() waits
     for the device and builds the DataBunch."""
 
-    def __init__(self, filename, pscrunch, state, rm_baseline, quiet, dev):
+    def __init__(self, filename, pscrunch, state, rm_baseline, quiet, dev,
+                 dedisperse=False, tscrunch=False):
         import torch
         from . import engine
         from .timeline import span
         self.filename, self.quiet = filename, quiet
+        self.dedisperse, self.tscrunch = dedisperse, tscrunch
         with span("load.open"):
             f = self.f = PSRFITS(filename)
             nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
@@ -635,10 +666,16 @@ class _Pending(object):
                     up = torch.cuda.Event()
                     up.record(st)
                     slot[1] = up                    # the buffer is free after it
+                    # with dedisperse the baseline is removed after the
+                    # rotation (pplib.py:2786-2791)
                     out = engine.unpack_psrfits(
                         raw_d, elem, npol, nchan, nbin, aux_d[:nsc],
                         aux_d[nsc:2 * nsc], wts=aux_d[2 * nsc:],
-                        pol_mode=pol_mode, rm_baseline=rm_baseline, dev=dev)
+                        pol_mode=pol_mode,
+                        rm_baseline=rm_baseline and not dedisperse, dev=dev)
+                    if dedisperse or tscrunch:
+                        out = self._transform(out, aux_d[2 * nsc:],
+                                              rm_baseline, f, dev)
                     noise = engine.noise_rows(out["rows"], dev=dev)
                     # one download: stats [nsub, nchan, 3], total [nsub,
                     # nbin], noise [nsub, nchan] (all float64)
@@ -659,8 +696,72 @@ class _Pending(object):
                 if f.subint.has("TSUBINT") else np.zeros(nsub)
             self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
                 if f.subint.has("PAR_ANG") else np.zeros(nsub)
+            self.pred = _PolycoRows(f.polyco) if (
+                tscrunch and f.polyco is not None and f.polyco.nrows) \
+                else None
             del raw
             f.close()
+
+    def _tscrunched_epoch(self):
+        """(imjd [1], frac [1], P [1]) of the tscrunched integration: the
+        middle of [first start, last end] (sub-int epochs are centres), the
+        period from the POLYCO predictor at it when the file has one, else
+        the duration-weighted mean PERIOD."""
+        imjd, frac, dur = self.imjd, self.frac, self.tsub
+        rel = (imjd - imjd[0]) + frac
+        half = dur / 2.0 / 86400.0
+        mid = 0.5 * ((rel - half).min() + (rel + half).max())
+        day = np.floor(mid)
+        i1, f1 = np.array([imjd[0] + int(day)]), np.array([mid - day])
+        if self.pred is not None:
+            P = np.array([1.0 / polyco_freq(self.pred, int(i1[0]),
+                                            float(f1[0]))])
+        else:
+            w = dur if dur.sum() > 0 else np.ones_like(dur)
+            P = np.array([float(np.sum(self.Ps * w) / np.sum(w))])
+        return i1, f1, P
+
+    def _transform(self, out, wts, rm_baseline, f, dev):
+        """Dedispersion and / or tscrunch of the unpacked rows (on the copy
+        stream), then the statistics pass over the result (the native
+        float32 rows through ppf_unpack_psrfits_batch, elem 3)."""
+        import torch
+        from . import engine, pplib
+        nsub, nchan, nbin = f.nsub, f.nchan, f.nbin
+        rows = out["rows"]
+        ones = torch.ones((nsub, nchan), dtype=torch.float32, device=dev)
+        zeros = torch.zeros((nsub, nchan), dtype=torch.float32, device=dev)
+
+        def stats(rows, w, rm):
+            n = rows.shape[0]
+            return engine.unpack_psrfits(
+                rows.reshape(n, nchan * nbin).view(torch.uint8), 3, 1, nchan,
+                nbin, ones[:n], zeros[:n], wts=w, pol_mode=0, rm_baseline=rm,
+                dev=dev)
+        if self.dedisperse:
+            # rotate_data(rows, 0, DM, Ps, freqs, nu0) (pplib.py:2427-2515):
+            # the phases as it forms them
+            p, h = f.primary, f.subint.header
+            DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
+            nu0 = float(p.get("OBSFREQ", self.freqs.mean()))
+            D = pplib.Dconst * DM / (np.ones(nsub) * self.Ps)
+            ph = D[:, None] * (self.freqs ** -2.0 - nu0 ** -2.0)
+            rows = engine.rotate_rows(rows, ph, dev=dev).float()
+            out = stats(rows, wts, rm_baseline)
+            rows = out["rows"]
+        if self.tscrunch:
+            acc = torch.zeros((nchan, nbin), dtype=torch.float64, device=dev)
+            wsum = torch.zeros(nchan, dtype=torch.float64, device=dev)
+            engine.align_accum(rows, torch.zeros((nsub, nchan),
+                                                 dtype=torch.float64,
+                                                 device=dev),
+                               wts.reshape(nsub, nchan).double(), acc, wsum,
+                               dev=dev)
+            mean = acc / torch.where(wsum > 0, wsum,
+                                     torch.ones_like(wsum))[:, None]
+            out = stats(mean.float()[None].contiguous(),
+                        wsum.float()[None].contiguous(), False)
+        return out
 
     def finish(self):
         from . import pplib
@@ -675,15 +776,26 @@ class _Pending(object):
         from . import pplib
         f, filename, weights = self.f, self.filename, self.weights
         nsub, nchan, nbin = f.nsub, f.nchan, f.nbin
+        prof_norm = max(1.0, float(np.count_nonzero(weights)))
+        imjd, frac, Ps, freqs = self.imjd, self.frac, self.Ps, self.freqs
+        tsub, par = self.tsub, self.par
+        doppler = np.ones(nsub)
+        if self.tscrunch:
+            # one integration: summed weights, the middle of the span, the
+            # period there, the summed duration
+            imjd, frac, Ps = self._tscrunched_epoch()
+            weights = weights.sum(axis=0)[None]
+            freqs = freqs[:1]
+            par = np.array([par.mean()])
+            doppler = np.ones(1)
+            nsub = 1
         packed = self.packed_h.numpy()
         n1, n2 = nsub * nchan * 3, nsub * nbin
         stats = packed[:n1].reshape(nsub, nchan, 3)
         total = packed[n1:n1 + n2].reshape(nsub, nbin)
         noise = packed[n1 + n2:].reshape(nsub, nchan)
         p, h = f.primary, f.subint.header
-        epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(self.imjd,
-                                                                self.frac)]
-        freqs = self.freqs
+        epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(imjd, frac)]
         weights_norm = np.where(weights == 0.0, 0.0, 1.0)
         ok_isubs = np.compress(weights_norm.mean(axis=1), list(range(nsub)))
         chans = np.arange(nchan)
@@ -696,7 +808,6 @@ class _Pending(object):
         prof = total.sum(axis=0)
         prof_SNR, prof_noise = _window_snr(prof)
         telescope = str(p.get("TELESCOP", "")).strip()
-        tsub, par = self.tsub, self.par
         DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
         if not self.quiet:
             print("\nReading data from %s on source %s (PSRFITS fast "
@@ -704,20 +815,23 @@ class _Pending(object):
         data = pplib.DataBunch(
             arch=None, backend=str(p.get("BACKEND", "")).strip(),
             backend_delay=float(p.get("BE_DELAY", 0.0)),
-            bw=float(p.get("OBSBW", 0.0)), doppler_factors=np.ones(nsub),
+            bw=float(p.get("OBSBW", 0.0)), doppler_factors=doppler,
             doppler_known=False, DM=DM,
-            dmc=0, epochs=epochs, filename=filename, flux_prof=np.array([]),
+            dmc=int(self.dedisperse), epochs=epochs, filename=filename,
+            flux_prof=np.array([]),
             freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
             integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
             nchan=nchan, noise_stds=noise[:, None, :], npol=1, nsub=nsub,
-            nu0=float(p.get("OBSFREQ", freqs.mean())), ok_ichans=ok_ichans,
+            nu0=float(p.get("OBSFREQ", self.freqs.mean())),
+            ok_ichans=ok_ichans,
             ok_isubs=ok_isubs, parallactic_angles=par,
             phases=pplib.get_bin_centers(nbin),
-            prof=prof / max(1.0, weights_norm.sum()),
-            prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=self.Ps,
+            prof=prof / prof_norm,
+            prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=Ps,
             SNRs=stats[:, None, :, 2].copy(),
             source=str(p.get("SRC_NAME", "")).strip(),
             state="Intensity", subints=DeviceRows(self.rows, self.ev),
-            subtimes=list(tsub), telescope=telescope,
+            subtimes=[float(tsub.sum())] if self.tscrunch else list(tsub),
+            telescope=telescope,
             telescope_code=_telescope_code(telescope), weights=weights)
         return data

@@ -167,6 +167,12 @@ def narrowband():
     return Case({k: z[k] for k in z.files})
 
 
+def narrowband_opts():
+    """tests/golden/narrowband_opts.npz (make_golden_nb_opts.py)."""
+    z = _load("narrowband_opts.npz")
+    return Case({k: z[k] for k in z.files})
+
+
 def zap():
     """tests/golden/zap.npz (make_golden_zap.py) plus the reference's ragged
     get_channels_to_zap outputs unflattened to [call][file][sub] lists."""

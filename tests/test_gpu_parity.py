@@ -39,6 +39,15 @@ def test_noise_matches_reference(ppl):
             m["noise_out_%d" % nb], rtol=1e-12)
     with pytest.raises(NotImplementedError):     # nbin/2 = 3 x 167
         ppl.get_noise(np.ones((2, 1002)), chans=True)
+    # chans=False ravels the portrait (pplib.py:2334-2338): 64 x 2048 and an
+    # odd length go through the device FFT library (no LDS-size cap); the
+    # restatement is the reference's own NumPy arithmetic
+    for shape in ((64, 2048), (3, 1001), (1002,)):
+        x = np.random.default_rng(4).normal(size=shape)
+        F = np.fft.rfft(x.ravel())
+        p = np.real(F * np.conj(F)) / x.size
+        want = np.sqrt(np.mean(p[int((1 - 4 ** -1) * len(p)):]))
+        assert abs(ppl.get_noise(x) / want - 1) < 1e-12, shape
 
 
 def test_noise_fp32_input_equals_fp64(ppl):
@@ -672,6 +681,94 @@ def test_narrowband_toas_match_reference(monkeypatch, tmp_path, capsys):
     pplib.write_TOAs(gt.TOA_list)
     lines = capsys.readouterr().out.splitlines()
     ref = list(g["out_tim_lines"])
+    assert len(lines) == len(ref)
+    for a, b in zip(lines, ref):
+        ta, tb = a.split(), b.split()
+        assert len(ta) == len(tb)
+        for x, y in zip(ta, tb):
+            if x.endswith("example.gmodel"):     # -tmplt path differs
+                continue
+            assert _same_printed_number(x, y), (a, b)
+
+
+def _nb_bunch(name, sub, w, noise, snrs, epochs, g, par):
+    from pulseportraiture_amd.pplib import DataBunch, get_bin_centers
+    nsub = sub.shape[0]
+    nchan, nbin = int(g["nchan"]), int(g["nbin"])
+    wn = np.where(w == 0.0, 0.0, 1.0)
+    return DataBunch(
+        arch=None, backend="fake_be", backend_delay=1e-5, bw=800.0,
+        doppler_factors=np.ones(nsub), DM=float(g["DM0"]), dmc=0,
+        epochs=[_MJD(e) for e in epochs], filename=name,
+        flux_prof=np.array([]), freqs=np.tile(g["freqs"], (nsub, 1)),
+        frontend="fake_rx", integration_length=60.0 * 3, masks=None,
+        nbin=nbin, nchan=nchan, noise_stds=noise[:, None], npol=1, nsub=nsub,
+        nu0=1500.0, ok_ichans=[np.compress(wn[i], list(range(nchan)))
+                               for i in range(nsub)],
+        ok_isubs=np.arange(nsub), parallactic_angles=np.full(nsub, par),
+        phases=get_bin_centers(nbin), prof=None, prof_noise=1.0,
+        prof_SNR=100.0, Ps=np.ones(nsub) * float(g["P"]),
+        SNRs=snrs[:, None, :], source="J1234-5678", state="Intensity",
+        subints=sub.astype(np.float64)[:, None],
+        subtimes=[60.0 * (3 if nsub == 1 else 1)] * nsub, telescope="GBT",
+        telescope_code="1", weights=w)
+
+
+def test_narrowband_options_match_reference(monkeypatch, tmp_path, capsys):
+    """get_narrowband_TOAs' options against the reference's own runs
+    (tests/golden/narrowband_opts.npz): print_phase / print_flux raise what
+    the reference raises (it reads names that path never defines,
+    pptoas.py:1131-1137); tscrunch=True (the loader asked for tscrunched
+    archives) with print_parangle and extra flags gives the reference's
+    fits and .tim lines."""
+    import os
+    from pulseportraiture_amd import pptoas, pplib
+    g = G.narrowband_opts()
+    nf = int(g["nfile"])
+    files, ts = {}, {}
+    for f in range(nf):
+        name = "nb%d.fits" % f
+        files[name] = _nb_bunch(name, g["f%d_subints" % f],
+                                g["f%d_weights" % f], g["f%d_noise" % f],
+                                g["f%d_snrs" % f], g["f%d_epochs" % f], g, 0.0)
+        ts[name] = _nb_bunch(name, g["ts_f%d_subints" % f],
+                             g["ts_f%d_weights" % f], g["ts_f%d_noise" % f],
+                             g["ts_f%d_snrs" % f],
+                             [float(g["ts_f%d_epoch" % f])], g, 0.25)
+    seen = []
+
+    def load(fn, **kw):
+        seen.append(bool(kw.get("tscrunch")))
+        return ts[fn] if kw.get("tscrunch") else files[fn]
+    monkeypatch.setattr(pptoas, "load_data", load)
+    monkeypatch.setattr(pptoas, "_MJD", _MJD)
+    meta = tmp_path / "meta.txt"
+    meta.write_text("".join(n + "\n" for n in files))
+    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+    for opt in ("print_phase", "print_flux"):
+        gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+        with pytest.raises(Exception) as ei:
+            gt.get_narrowband_TOAs(quiet=True, **{opt: True})
+        assert "%s: %s" % (ei.type.__name__, ei.value) == \
+            str(g["exc_" + opt])
+    del seen[:]
+    gt = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    gt.get_narrowband_TOAs(quiet=True, tscrunch=True, print_parangle=True,
+                           addtnl_toa_flags={"pta": "TEST"})
+    assert seen and all(seen)
+    for f in range(nf):
+        used = g["ts_out_phi_errs"][f] > 0
+        dphi = np.abs(G.phase_diff(gt.phis[f], g["ts_out_phis"][f]))[used]
+        assert np.all(dphi < SIG * g["ts_out_phi_errs"][f][used]), dphi
+        for key in ("phi_errs", "scales", "scale_errs", "channel_snrs",
+                    "channel_red_chi2s"):
+            np.testing.assert_allclose(getattr(gt, key)[f],
+                                       g["ts_out_" + key][f], rtol=1e-6,
+                                       err_msg=key)
+    capsys.readouterr()
+    pplib.write_TOAs(gt.TOA_list)
+    lines = capsys.readouterr().out.splitlines()
+    ref = list(g["ts_out_tim_lines"])
     assert len(lines) == len(ref)
     for a, b in zip(lines, ref):
         ta, tb = a.split(), b.split()

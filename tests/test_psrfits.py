@@ -16,7 +16,8 @@ import pytest
 from pulseportraiture_amd import psrfits as PF
 
 
-def _archive(tmp, nsub=4, npol=2, nchan=32, nbin=256, seed=1, elem="I"):
+def _archive(tmp, nsub=4, npol=2, nchan=32, nbin=256, seed=1, elem="I",
+             wvals=False):
     rng = np.random.default_rng(seed)
     b = np.arange(nbin)
     prof = np.exp(-0.5 * ((b - 0.3 * nbin) / (0.02 * nbin)) ** 2)
@@ -25,6 +26,9 @@ def _archive(tmp, nsub=4, npol=2, nchan=32, nbin=256, seed=1, elem="I"):
     q, scl, offs = PF.quantize(rows)
     fr = np.tile(np.linspace(1100.0, 1900.0, nchan), (nsub, 1))
     wts = np.ones((nsub, nchan))
+    if wvals:
+        wts = np.round(rng.uniform(0.5, 2.0, (nsub, nchan)), 2)
+        wts[:, 7] = 0.0                                # zapped everywhere
     wts[1, 3] = 0.0
     fn = os.path.join(str(tmp), "a.fits")
     PF.write_psrfits(fn, q, scl, offs, fr, wts, np.full(nsub, 0.00289),
@@ -78,7 +82,7 @@ def test_mjd_arithmetic():
 
 def test_load_data_rejects_psrchive_only_options(tmp_path):
     fn = _archive(tmp_path)[0]
-    for kw in (dict(tscrunch=True), dict(dedisperse=True), dict(fscrunch=True)):
+    for kw in (dict(fscrunch=True), dict(state="Stokes")):
         with pytest.raises(NotImplementedError):
             PF.load_data(fn, pscrunch=True, **kw)
     with pytest.raises(NotImplementedError):
@@ -187,3 +191,128 @@ def test_gettoas_psrfits_equals_databunch_path(tmp_path, monkeypatch):
     # the fits converged on data of unit reduced chi^2
     rc = np.asarray(fast.red_chi2s[0])
     assert np.all((rc > 0.8) & (rc < 1.25)), rc
+
+
+def _baseline_removed(R, wts, frac=0.15):
+    """k_base_window + k_row_stats restated over float32 rows [nsub, nchan,
+    nbin]: (rows minus their window mean, float32; S/N; window starts)."""
+    nsub, nchan, nbin = R.shape
+    W = min(nbin - 1, max(1, int(np.rint(frac * nbin))))
+    out, snr, w0 = np.empty_like(R), np.empty((nsub, nchan)), []
+    for s in range(nsub):
+        tot = (wts[s][:, None] * R[s].astype(float)).sum(axis=0)
+        cs = np.concatenate([[0.0], np.cumsum(np.concatenate([tot, tot[:W]]))])
+        k = int(np.argmin(cs[W:W + nbin] - cs[:nbin]))
+        w0.append(k)
+        idx = (k + np.arange(W)) % nbin
+        mean = R[s][:, idx].astype(float).mean(axis=1)
+        sig = R[s][:, idx].astype(float).std(axis=1)
+        on = np.ones(nbin, bool)
+        on[idx] = False
+        snr[s] = (R[s][:, on].astype(float) - mean[:, None]).sum(axis=1) / \
+            (sig * np.sqrt(on.sum()))
+        out[s] = (R[s].astype(float) - mean[:, None]).astype(np.float32)
+    return out, snr, w0
+
+
+@pytest.mark.gpu
+def test_load_data_dedisperse_tscrunch(tmp_path):
+    """load_data(dedisperse, tscrunch) on the device against the DataBunch
+    rows transformed on the host side of the API: rotate_data (pplib.py:
+    2427-2515) by the stored DM to OBSFREQ per sub-int period, the baseline
+    measured after the rotation (pplib.py:2786-2791), then the
+    DAT_WTS-weighted mean over sub-ints (PSRCHIVE's weighted Profile
+    average; PSRCHIVE parity itself unpinned)."""
+    from pulseportraiture_amd import pplib
+    fn = _archive(tmp_path, wvals=True)[0]
+    f = PF.PSRFITS(fn)
+    wts = f.weights()                # DAT_WTS as stored (float32 values)
+    f.close()
+    base = PF.load_data(fn, pscrunch=True, rm_baseline=False, quiet=True)
+    U = np.asarray(base.subints)[:, 0]
+    nsub, nchan, nbin = U.shape
+    nu0 = base.nu0
+    R = pplib.rotate_data(U[:, None], 0.0, 12.5, base.Ps, base.freqs,
+                          nu0)[:, 0].astype(np.float32)
+    Rb, snr, _ = _baseline_removed(R, wts)
+    sp = 2 * np.spacing(np.float32(np.abs(Rb).max()))
+    # dedisperse
+    dd = PF.load_data(fn, pscrunch=True, rm_baseline=True, dedisperse=True,
+                      quiet=True)
+    assert dd.dmc == 1 and dd.nsub == nsub
+    np.testing.assert_allclose(np.asarray(dd.subints)[:, 0], Rb, rtol=0,
+                               atol=sp)
+    np.testing.assert_allclose(dd.SNRs[:, 0], snr, rtol=1e-6)
+    # tscrunch (no dedispersion, no baseline removal)
+    ts = PF.load_data(fn, pscrunch=True, rm_baseline=False, tscrunch=True,
+                      quiet=True)
+    wsum = wts.sum(axis=0)
+    mean = (wts[:, :, None] * U.astype(float)).sum(axis=0) / \
+        np.where(wsum > 0, wsum, 1.0)[:, None]
+    assert ts.nsub == 1 and ts.dmc == 0 and len(ts.epochs) == 1
+    np.testing.assert_allclose(np.asarray(ts.subints)[0, 0],
+                               mean.astype(np.float32), rtol=0,
+                               atol=4 * np.spacing(np.float32(
+                                   np.abs(mean).max())))
+    np.testing.assert_array_equal(ts.weights[0], wsum)
+    assert list(ts.ok_ichans[0]) == [c for c in range(nchan) if wsum[c]]
+    # the middle of the span: sub-int centres 5 + 10 i s, 10 s each
+    assert ts.epochs[0].intday() == 57000
+    assert abs(ts.epochs[0].fracday() - (3600.25 + 20.0) / 86400.0) < 1e-12
+    assert ts.subtimes == [40.0] and ts.Ps[0] == 0.00289
+    np.testing.assert_allclose(ts.noise_stds[0, 0], pplib.get_noise(
+        np.asarray(ts.subints)[0, 0].astype(float), chans=True), rtol=1e-9)
+    # both: the weighted mean of the dedispersed, baseline-removed rows
+    both = PF.load_data(fn, pscrunch=True, rm_baseline=True, dedisperse=True,
+                        tscrunch=True, quiet=True)
+    mb = (wts[:, :, None] * Rb.astype(float)).sum(axis=0) / \
+        np.where(wsum > 0, wsum, 1.0)[:, None]
+    np.testing.assert_allclose(np.asarray(both.subints)[0, 0],
+                               mb.astype(np.float32), rtol=0,
+                               atol=4 * np.spacing(np.float32(
+                                   np.abs(mb).max())))
+    assert both.dmc == 1 and both.nsub == 1
+
+
+@pytest.mark.gpu
+def test_gettoas_tscrunch_psrfits_equals_databunch_path(tmp_path,
+                                                        monkeypatch):
+    """get_TOAs(tscrunch=True) on a PSRFITS file (tscrunched on the device)
+    == get_TOAs on the same tscrunched rows and metadata as a host
+    DataBunch, bitwise."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import synth_np as SN
+    from pulseportraiture_amd import pptoas, pplib
+    nsub, nchan, nbin = 6, 64, 512
+    model, freqs = SN.template(nchan, nbin)
+    rng = np.random.default_rng(9)
+    P = 0.0028929
+    port = np.stack([SN.rotate(model, -(0.1 + 4148.808 * 10.0 *
+                                        (freqs ** -2 - 1500.0 ** -2) / P))
+                     for _ in range(nsub)])
+    rows = 15.0 * port[:, None] + rng.normal(0, 1.0, (nsub, 1, nchan, nbin))
+    q, scl, offs = PF.quantize(rows)
+    fn = str(tmp_path / "t.fits")
+    PF.write_psrfits(fn, q, scl, offs, np.tile(freqs, (nsub, 1)),
+                     np.ones((nsub, nchan)), np.full(nsub, P),
+                     5.0 + 10.0 * np.arange(nsub), np.full(nsub, 10.0),
+                     npol=1, pol_type="AA+BB", dm=10.0)
+    gm = str(tmp_path / "t.gmodel")
+    SN.write_gmodel(gm, *SN.read_gmodel())
+    meta = tmp_path / "meta.txt"
+    meta.write_text(fn + "\n")
+    fast = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    fast.get_TOAs(quiet=True, bary=False, tscrunch=True)
+    assert len(fast.TOA_list) == 1
+    d = pplib.load_data(fn, pscrunch=True, rm_baseline=False, tscrunch=True,
+                        quiet=True)
+    host = pplib.DataBunch(**{k: v for k, v in d.items()})
+    host["subints"] = np.asarray(d.subints).copy()
+    monkeypatch.setattr(pptoas, "load_data", lambda f_, **kw: host)
+    slow = pptoas.GetTOAs(str(meta), gm, quiet=True)
+    slow.get_TOAs(quiet=True, bary=False, tscrunch=True)
+    for key in ("phis", "phi_errs", "DMs", "DM_errs", "red_chi2s", "snrs"):
+        np.testing.assert_array_equal(np.asarray(getattr(fast, key)[0]),
+                                      np.asarray(getattr(slow, key)[0]),
+                                      err_msg=key)

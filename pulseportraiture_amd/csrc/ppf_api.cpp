@@ -708,7 +708,11 @@ int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
     ppf::NoiseArgs a{nbin, fft_log2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
-    if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise");
+    if (ppf::noise_wave_supported(a.log2N)) {
+        if ((e = ppf::launch_noise_wave(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise_w");
+    } else if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) {
+        return hip_fail(ctx, e, "k_noise");
+    }
     return PPF_OK;
 }
 

@@ -324,6 +324,9 @@ size_t tr_state_bytes();
 int pass_blocks(int nchan);
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
+// wave-per-row noise (k_noise_w) for N = nbin/2 = 128..1024
+bool noise_wave_supported(int log2N);
+hipError_t launch_noise_wave(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st);
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st);
 // per (model, channel): 1 + the last harmonic with |M_k|^2 > kCutRel max_k |M_k|^2

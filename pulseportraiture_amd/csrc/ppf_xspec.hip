@@ -155,6 +155,11 @@ __host__ __device__ constexpr int xspec_wpe() { return LOG2N == 10 ? 2 : 1; }
 // the fused guess runs at 1024 points only: below, its extra registers cost
 // a wave per SIMD or spill (those shapes take k_dsum)
 __host__ __device__ constexpr bool xspec_guess_fused(int log2N) { return log2N == 10; }
+// one post-pass over the transform (power sums and X together, X scaled at
+// the write-out); 0: the two-pass form (sums, then X scaled in the buffer)
+#ifndef PPF_XS_ONEPASS
+#define PPF_XS_ONEPASS 1
+#endif
 template <int LOG2N, int DT, bool GS>
 __global__ __launch_bounds__(64 * xsw<LOG2N>()) __attribute__((amdgpu_waves_per_eu(xspec_wpe<LOG2N>())))
 void k_xspec_w(XspecArgs a) {
@@ -164,6 +169,7 @@ void k_xspec_w(XspecArgs a) {
     constexpr int NP = N / 128;                       // (k, N-k) pairs per lane
     constexpr int SL = xspec_slw<LOG2N>();           // padded wave buffer + 2 side slots
     constexpr int XNYQ = SL - 2;                      // X_{N/2} of the row
+    constexpr int XIE2 = SL - 1;                      // the row's 1/errs_FT^2 (.x)
     // model pairs loaded ahead in pass 2: at 1024 points the 4-wave
     // workgroups leave VGPRs to spare (LDS caps them at two waves per SIMD:
     // 4 ahead, C3 27.1 -> 25.5 ms); at 512 points k_xspec_w runs four waves
@@ -226,7 +232,17 @@ void k_xspec_w(XspecArgs a) {
     // channel cbase + lane; the workgroup sum G[1..NL) after the twiddles
     constexpr int NL = 64 * guess_npl(LOG2N);
     bool gon = false;
-    double g_w = 0.0, g_dg = 0.0, g_w2e2 = 0.0;
+    // the row's weight and dedispersion phase come from wave-uniform loads
+    // (guess_weights, freqs) and two uniform scalars (Dg, nu_ref^-2, moved
+    // to SGPRs): no VGPRs held across the round loop for them
+    double g_Dg = 0.0, g_nrm2 = 0.0, g_w2e2 = 0.0;
+    auto g_wn = [&](int nn) {
+        return a.guess_weights[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
+    };
+    auto g_dgn = [&](int nn) {
+        const double f = a.freqs[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
+        return g_Dg * (1.0 / (f * f) - g_nrm2);
+    };
     double2 *gacc = lds + kXSW * SL + (PPF_TW_LDS ? tw_slots<LOG2N>() : 0);
     if constexpr (GS) {
         gon = a.gflag[s] != 0;                         // uniform
@@ -246,12 +262,8 @@ void k_xspec_w(XspecArgs a) {
                 const double nf = a.nu_fits[(int64_t)s * 3];
                 if (nf == nf) nu_ref_m2 = 1.0 / (nf * nf);
             }
-            const double Dg = kDconst * a.guess_DM[s] / a.P[s];
-            if (cbase + lane < cend) {
-                const double f = fr[cbase + lane];
-                g_w = a.guess_weights[(int64_t)s * a.nchan + cbase + lane];
-                g_dg = Dg * (1.0 / (f * f) - nu_ref_m2);
-            }
+            g_Dg = readlane_d(kDconst * a.guess_DM[s] / a.P[s], 0);
+            g_nrm2 = readlane_d(nu_ref_m2, 0);
             __syncthreads();
         }
     }
@@ -283,11 +295,106 @@ void k_xspec_w(XspecArgs a) {
             // FFT is done, so their wait no longer holds up anything): each
             // pass-2 iteration otherwise waited for its own two L2 loads
             double2 Mq[MD > 0 ? MD : 1][2];
+            auto preload_m = [&]() {
 #pragma unroll
-            for (int i = 0; i < MD; ++i) {
-                Mq[i][0] = Mrow[lane + 64 * i];
-                Mq[i][1] = Mrow[N - lane - 64 * i];
+                for (int i = 0; i < MD; ++i) {
+                    Mq[i][0] = Mrow[lane + 64 * i];
+                    Mq[i][1] = Mrow[N - lane - 64 * i];
+                }
+            };
+#if PPF_XS_ONEPASS
+            // ONE post-pass over the transform: each pair's D_k feeds the
+            // power sums (noise, Sd) and leaves the UNSCALED D_k conj(M_k) in
+            // the buffer; the row's 1/errs_FT^2 is known once the sums are
+            // complete, and the write-out applies it (the same product in
+            // the same order, so X is bit-identical to scaling it here).
+            // The Nyquist bin leaves pad(N/2) before pair 0 overwrites it.
+            double2 Dm = cmk(0.0, 0.0);
+            if (lane == 0) {
+                const double2 zm = buf[wfft::pad<LOG2N>(N / 2)];
+                Dm = cmk(zm.x, -zm.y);
             }
+            // guess phasor of this row: El = w e^{2 pi i k dphi} at k = lane
+            // + 64 i by recurrence (step e^{2 pi i 64 dphi}: lane 1's phasor
+            // squared six times)
+            double2 El = cmk(0.0, 0.0), Est = El;
+            if (GS && gon) {
+                const double dg = g_dgn(n);
+                const double2 E1 = cexp2pi((double)lane * dg);
+                El = cscale(E1, g_wn(n));
+                Est = cmk(readlane_d(E1.x, 1), readlane_d(E1.y, 1));
+#pragma unroll
+                for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
+            }
+            preload_m();
+            double pn = 0.0, pd = 0.0;
+            {
+                double2 w = w_seed;
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+                    const int klo = lane + 64 * i, khi = N - klo;
+                    double2 Dlo, Dhi;
+                    rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+                    w = cmul(w, w_step);
+                    const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                    if (klo >= a.kc) pn += p0;
+                    if (khi >= a.kc) pn += p1;
+                    if (klo >= 1) pd += p0;
+                    pd += p1;
+                    // (fused guess: X stops below NL, past it only the sums)
+                    if (!(GS && gon && 64 * i >= NL)) {
+                        double2 Mlo, Mhi;
+                        if constexpr (MD > 0) {
+                            Mlo = Mq[i % MD][0];
+                            Mhi = Mq[i % MD][1];
+                            if (i + MD < NP) {
+                                Mq[i % MD][0] = Mrow[klo + 64 * MD];
+                                Mq[i % MD][1] = Mrow[khi - 64 * MD];
+                            }
+                        } else {
+                            Mlo = Mrow[klo];
+                            Mhi = Mrow[khi];
+                        }
+                        buf[wfft::pad<LOG2N>(klo)] = (klo == 0) ? cmk(0.0, 0.0) : cmulc(Dlo, Mlo);
+                        if (GS && gon) {
+                            // X_{N-k} is past the cutoff: its slot takes the
+                            // row's guess term of harmonic k (k = 0: dropped)
+                            if (klo != 0) buf[wfft::pad<LOG2N>(khi)] = cmul(Dlo, El);
+                            El = cmul(El, Est);
+                        } else {
+                            buf[klo == 0 ? wfft::pad<LOG2N>(N / 2) : wfft::pad<LOG2N>(khi)] =
+                                cmulc(Dhi, Mhi);
+                        }
+                    }
+                    SCHED_CUT();
+                }
+            }
+            if (lane == 0) {
+                const double p = cabs2(Dm);
+                if (N / 2 >= a.kc) pn += p;
+                pd += p;
+            }
+            pn = wave_sum(pn);
+            pd = wave_sum(pd);
+            double errs_FT;
+            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+            if (GS && gon) {
+                const double wn = g_wn(n);
+                g_w2e2 += wn * wn * errs_FT * errs_FT;
+            }
+            if (lane == 0) {
+                buf[XNYQ] = cmulc(Dm, Mrow[N / 2]);
+                reinterpret_cast<double *>(buf + XIE2)[0] = inv_e2;   // for the write-out
+                double *chan = a.chan + crow * 4;
+                chan[0] = errs_FT;
+                chan[1] = inv_e2;
+                chan[2] = pd * inv_e2;                                  // Sd_n
+                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+            }
+#else
+            preload_m();
             // pass 1: power sums (noise, Sd); pass 2 recomputes D for X
             double pn = 0.0, pd = 0.0;
             {
@@ -327,7 +434,7 @@ void k_xspec_w(XspecArgs a) {
             double2 El = cmk(0.0, 0.0), Est = El;
             if (GS && gon) {
                 const int r = n - cbase;
-                const double wn = readlane_d(g_w, r), dg = readlane_d(g_dg, r);
+                const double wn = g_wn(n), dg = g_dgn(n);
                 const double2 E1 = cexp2pi((double)lane * dg);
                 El = cscale(E1, wn);
                 Est = cmk(readlane_d(E1.x, 1), readlane_d(E1.y, 1));
@@ -386,6 +493,7 @@ void k_xspec_w(XspecArgs a) {
                 chan[2] = pd * inv_e2;                                  // Sd_n
                 chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
             }
+#endif
         }
         __syncthreads();
         // write-out: thread t -> channel c = t % 8 of the round, harmonics
@@ -396,10 +504,17 @@ void k_xspec_w(XspecArgs a) {
             if (nc < cend) {
                 const bool ok = !mask || mask[nc];
                 const double2 *b = lds + c * SL;
+#if PPF_XS_ONEPASS
+                const double ie2 = ok ? reinterpret_cast<const double *>(b + XIE2)[0] : 0.0;
+#endif
                 for (int k = threadIdx.x / kXSW; k < kw; k += 64) {
                     const int slot = k == N ? wfft::pad<LOG2N>(N / 2)
                                             : (k == N / 2 ? XNYQ : wfft::pad<LOG2N>(k));
+#if PPF_XS_ONEPASS
+                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[slot], ie2) : cmk(0.0, 0.0);
+#else
                     Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);
+#endif
                 }
             }
         }
@@ -424,7 +539,8 @@ void k_xspec_w(XspecArgs a) {
             // holds the block's weights in its lanes), and sum w^2 errs_FT^2
             // per wave, added in wave order (buffer slot 0 is free after the
             // last round's barrier)
-            const double wsum = wave_sum(mlane ? g_w : 0.0), cnt = wave_sum(mlane ? 1.0 : 0.0);
+            const double gwl = mlane ? a.guess_weights[(int64_t)s * a.nchan + cbase + lane] : 0.0;
+            const double wsum = wave_sum(gwl), cnt = wave_sum(mlane ? 1.0 : 0.0);
             if (lane == 0) reinterpret_cast<double *>(buf)[0] = g_w2e2;
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -886,6 +1002,88 @@ hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st) {
         case 19: launch_w<9, 1>(a, st); break;
         case 20: launch_w<10, 0>(a, st); break;
         case 21: launch_w<10, 1>(a, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// k_noise_w: get_noise_PS per row (pplib.py:2312-2332) with one row per wave:
+// the register radix FFT of k_xspec_w (next row in flight during the
+// transform), the real post-pass, and the mean power of harmonics >= kc.
+// Rows are dealt to the waves round-robin (4 waves per workgroup, as many
+// workgroups as keep every CU's LDS busy); the block kernel k_noise (one
+// 256-thread workgroup per row, a barrier per FFT stage) remains for the
+// other lengths.
+// ===========================================================================
+constexpr int kNoiseW = 4;
+template <int LOG2N, int DT>
+__global__ __launch_bounds__(64 * kNoiseW) void k_noise_w(NoiseArgs a, int64_t nrows) {
+    using P = wfft::Plan<LOG2N>;
+    constexpr int N = P::N, R = P::R, NP = N / 128;
+    constexpr int SL = wfft::buf_slots<LOG2N>();
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *buf = lds + wave * SL;
+    double2 *tw = lds + kNoiseW * SL;
+    for (int i = threadIdx.x; i < tw_slots<LOG2N>(); i += 64 * kNoiseW) tw[i] = a.T[i];
+    __syncthreads();
+    const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    const RowT *rows = reinterpret_cast<const RowT *>(a.in);
+    const int64_t nw = (int64_t)gridDim.x * kNoiseW;
+    int64_t row = (int64_t)blockIdx.x * kNoiseW + wave;
+    RowT zr[R];
+    auto fetch = [&](int64_t rr) {
+        const RowT *src = rows + rr * N;
+#pragma unroll
+        for (int q = 0; q < R; ++q) zr[q] = src[lane + 64 * q];
+    };
+    if (row < nrows) fetch(row);
+    for (; row < nrows; row += nw) {
+        double2 x[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+        if (row + nw < nrows) fetch(row + nw);
+        wfft::fft_row<LOG2N>(x, buf, tw, lane);
+        double pn = 0.0;
+        double2 w = w_seed;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int klo = lane + 64 * i, khi = N - klo;
+            double2 Dlo, Dhi;
+            rfft_pair<LOG2N>(buf, klo, w, Dlo, Dhi);
+            w = cmul(w, w_step);
+            if (klo >= a.kc) pn += cabs2(Dlo);
+            if (khi >= a.kc) pn += cabs2(Dhi);
+        }
+        if (lane == 0 && N / 2 >= a.kc) pn += cabs2(buf[wfft::pad<LOG2N>(N / 2)]);
+        pn = wave_sum(pn);
+        if (lane == 0) a.out[row] = sqrt(pn / (double)a.nbin / (double)(N + 1 - a.kc));
+    }
+}
+
+template <int LOG2N, int DT>
+static void launch_nw(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
+    const size_t lds = ((size_t)kNoiseW * wfft::buf_slots<LOG2N>() + tw_slots<LOG2N>()) * sizeof(double2);
+    // two to four workgroups per CU by LDS; a few rows per wave
+    const int64_t want = (nrows + kNoiseW - 1) / kNoiseW;
+    const unsigned grid = (unsigned)std::min<int64_t>(want, 256 * 16);
+    hipLaunchKernelGGL((k_noise_w<LOG2N, DT>), dim3(grid), dim3(64 * kNoiseW), lds, st, a, nrows);
+}
+
+bool noise_wave_supported(int log2N) { return log2N >= 7 && log2N <= 10; }
+
+hipError_t launch_noise_wave(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
+    switch (a.log2N * 2 + a.dtype) {
+        case 14: launch_nw<7, 0>(a, nrows, st); break;
+        case 15: launch_nw<7, 1>(a, nrows, st); break;
+        case 16: launch_nw<8, 0>(a, nrows, st); break;
+        case 17: launch_nw<8, 1>(a, nrows, st); break;
+        case 18: launch_nw<9, 0>(a, nrows, st); break;
+        case 19: launch_nw<9, 1>(a, nrows, st); break;
+        case 20: launch_nw<10, 0>(a, nrows, st); break;
+        case 21: launch_nw<10, 1>(a, nrows, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

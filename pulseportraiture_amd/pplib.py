@@ -14,6 +14,8 @@ import time
 
 import pickle
 
+import math
+
 import numpy as np
 
 from . import _lib, engine
@@ -56,12 +58,14 @@ class MJD(object):
     sub-nanosecond resolution.  MJD(days) or MJD(intday, fracday)."""
 
     def __init__(self, intday=0.0, fracday=None):
+        # math.floor: the same integers as np.floor, without the NumPy
+        # scalar round trip (GetTOAs makes two of these per TOA)
         if fracday is None:
             d = float(intday)
-            i = np.floor(d)
-            intday, fracday = int(i), d - i
+            i = math.floor(d)
+            intday, fracday = i, d - i
         i, f = int(intday), float(fracday)
-        k = int(np.floor(f))
+        k = math.floor(f)
         self._i, self._f = i + k, f - k
 
     def __add__(self, other):

@@ -313,9 +313,17 @@ class GetTOAs(object):
         in ONE ppf_gauss_portrait_batch launch (k_gauss_port)."""
         if self.is_FITS_model:
             raise NotImplementedError("FITS (archive) templates need PSRCHIVE")
+        # within one get_TOAs call the template file is read once and an
+        # archive whose portraits (frequency sets, TAU) equal an earlier
+        # archive's reuses that archive's device portraits: the same
+        # deterministic k_gauss_port output the reference rebuilds per
+        # archive
+        mc = self.__dict__.setdefault("_mcache", {})
         try:
+            if "model" not in mc:
+                mc["model"] = read_model(self.modelfile, quiet=True)
             (self.model_name, code, nu_ref, self.ngauss, gparams, _mff, alpha,
-             _mfa) = read_model(self.modelfile, quiet=True)
+             _mfa) = mc["model"]
         except (UnboundLocalError, UnicodeDecodeError):
             # a make_spline_model template (pptoas.py:416-419): one device
             # portrait per distinct frequency set, unscattered
@@ -325,24 +333,34 @@ class GetTOAs(object):
              self.alpha) = code, nu_ref, gparams, alpha
         nbin = len(d.phases)
         cache, prms, freqs, index = {}, [], [], []
+        g1 = gparams[1]
         for isub in ok_isubs:
-            p = np.copy(gparams)
-            if fit_scat:
-                p[1] = 0.0                 # unscattered template (pptoas.py:408-417)
-            elif p[1] != 0.0:
-                p[1] *= nbin / d.Ps[isub]  # read_model's TAU [s] -> [bin]
-            key = (d.freqs[isub].tobytes(), float(p[1]))
+            # TAU: 0 for the unscattered template of a scattering fit
+            # (pptoas.py:408-417), else read_model's [s] -> [bin]
+            t1 = 0.0 if fit_scat else (g1 * (nbin / d.Ps[isub])
+                                       if g1 != 0.0 else g1)
+            key = (d.freqs[isub].tobytes(), float(t1))
             if key not in cache:
                 cache[key] = len(prms)
+                p = np.copy(gparams)
+                p[1] = t1
                 prms.append(p)
                 freqs.append(np.asarray(d.freqs[isub], dtype=float))
             index.append(cache[key])
         if not prms:
             return np.zeros((0, len(d.freqs[0]), nbin)), \
                 np.zeros(0, dtype=np.int32)
-        models = engine.gauss_portraits(
-            code, np.stack(prms), 0.0 if fit_scat else alpha,
-            np.stack(freqs), nu_ref, nbin)
+        ck = (bool(fit_scat), nbin, tuple(cache))
+        models = mc.get(ck)
+        if models is None:
+            models = engine.gauss_portraits(
+                code, np.stack(prms), 0.0 if fit_scat else alpha,
+                np.stack(freqs), nu_ref, nbin)
+            if len(mc) > 8:
+                mc.clear()
+                mc["model"] = (self.model_name, code, nu_ref, self.ngauss,
+                               gparams, _mff, alpha, _mfa)
+            mc[ck] = models
         return (models.cpu().numpy() if host else models,
                 np.array(index, dtype=np.int32))
 
@@ -417,6 +435,7 @@ class GetTOAs(object):
         self.tscrunch = tscrunch
         self.add_instrumental_response = add_instrumental_response
         self._ff = [None]   # fit_flags carried across sub-ints (pptoas.py:519-529)
+        self._mcache = {}   # template portraits of this call (_models)
         # With several ranks and at least as many archives as ranks, each
         # rank loads and fits only its own contiguous block of archives
         # (pptoas.py:258) and the per-archive results are
@@ -971,6 +990,20 @@ class GetTOAs(object):
                   ("nch", nchan)]
         chbw = abs(d.bw) / nchan
         TOAs, TOA_errs = out["TOAs"], out["TOA_errs"]
+        print_flux = ctx["print_flux"]
+        if print_flux:
+            mmean, model_index = out["mmean"], job["model_index"]
+            pf, pfe = out["profile_fluxes"], out["profile_flux_errs"]
+            scl, scle = r["scales"], r["scale_errs"]
+            for j, isub in enumerate(ok_isubs):
+                ok = okb[j]
+                smm = mmean[model_index[j]][ok]
+                pf[isub, ok] = smm * scl[j][ok]
+                pfe[isub, ok] = abs(smm) * scle[j][ok]
+                out["fluxes"][isub], out["flux_errs"][isub] = weighted_mean(
+                    pf[isub, ok], pfe[isub, ok])
+                out["flux_freqs"][isub], _ = weighted_mean(F[j][ok],
+                                                           pfe[isub, ok])
         for j, isub in enumerate(ok_isubs):
             P = d.Ps[isub]
             phi = params[j, 0]
@@ -1012,6 +1045,10 @@ class GetTOAs(object):
             if ctx["print_phase"]:
                 toa_flags["phs"] = phi
                 toa_flags["phs_err"] = perrs[j, 0]
+            if print_flux:
+                toa_flags["flux"] = out["fluxes"][isub]
+                toa_flags["flux_err"] = out["flux_errs"][isub]
+                toa_flags["flux_ref_freq"] = out["flux_freqs"][isub]
             if ctx["print_parangle"]:
                 toa_flags["par_angle"] = d.parallactic_angles[isub]
             for k, v in ctx["addtnl_toa_flags"].items():
@@ -1036,8 +1073,15 @@ class GetTOAs(object):
         MJDs, DM0 = job["MJDs"], job["DM0"]
         ok_isubs, nok = job["ok_isubs"], job["nok"]
         models, model_index = job["models"], job["model_index"]
-        if ctx["print_flux"] and isinstance(models, torch.Tensor):
-            models = models.cpu().numpy()
+        mmean = None
+        if ctx["print_flux"]:
+            # the flux needs only each model row's mean: the scattered
+            # model's mean is the unscattered one's (the scattering kernel's
+            # zeroth harmonic is 1, pplib.py:4245-4260), so the reference's
+            # per-sub-int rfft / irfft of the model (pptoas.py:628-636)
+            # reduces to the row means, taken once per archive on the device
+            mmean = models.mean(dim=-1).cpu().numpy() if isinstance(
+                models, torch.Tensor) else np.asarray(models).mean(axis=-1)
         mask, flags_b = job["mask"], job["flags_b"]
         fit_duration = job["fit_duration"]
         batch_duration = r["batch_duration"]
@@ -1062,7 +1106,7 @@ class GetTOAs(object):
         nfevals = np.zeros(nsub, dtype="int")
         rcs = np.zeros(nsub, dtype="int")
         # ---- per-sub-integration bookkeeping (pptoas.py:567-711) -----
-        uniform = (FAST_HOST and not print_flux and nok > 0 and
+        uniform = (FAST_HOST and nok > 0 and
                    bool((flags_b == flags_b[0]).all()) and
                    int(np.count_nonzero(flags_b[0])) == self.nfit and
                    bool(mask.any(axis=1).all()))
@@ -1073,7 +1117,10 @@ class GetTOAs(object):
                 tau_errs=tau_errs, alphas=alphas, alpha_errs=alpha_errs,
                 scales=scales, scale_errs=scale_errs, snrs=snrs,
                 channel_snrs=channel_snrs, red_chi2s=red_chi2s,
-                covariances=covariances, nfevals=nfevals, rcs=rcs))
+                covariances=covariances, nfevals=nfevals, rcs=rcs,
+                profile_fluxes=profile_fluxes,
+                profile_flux_errs=profile_flux_errs, fluxes=fluxes,
+                flux_errs=flux_errs, flux_freqs=flux_freqs, mmean=mmean))
         for j, isub in enumerate([] if uniform else ok_isubs):
             fit_flags_j = [int(v) for v in flags_b[j]]
             ok = mask[j].astype(bool)
@@ -1103,17 +1150,7 @@ class GetTOAs(object):
                 df = 1.0
             freqsx = d.freqs[isub, ok]
             if print_flux:
-                modelx = models[model_index[j]][ok]
-                if results.tau != 0.0:
-                    tau = 10 ** results.tau if self.log10_tau else \
-                        results.tau
-                    scat_model = np.fft.irfft(scattering_portrait_FT(
-                        scattering_times(tau, results.alpha, freqsx,
-                                         results.nu_tau), nbin) *
-                        np.fft.rfft(modelx, axis=1), axis=1)
-                else:
-                    scat_model = np.copy(modelx)
-                smm = scat_model.mean(axis=1)
+                smm = mmean[model_index[j]][ok]
                 profile_fluxes[isub, ok] = smm * results.scales
                 profile_flux_errs[isub, ok] = abs(smm) * results.scale_errs
                 flux, flux_err = weighted_mean(profile_fluxes[isub, ok],
@@ -1290,6 +1327,7 @@ class GetTOAs(object):
             raise NotImplementedError("instrumental response (SURVEY.md row "
                                       "19) is not on the accelerated path")
         print("You are using an experimental functionality of pptoas!")
+        self._mcache = {}   # template portraits of this call (_models)
         self.nfit = 1
         self.fit_phi = True
         self.fit_tau = fit_scat

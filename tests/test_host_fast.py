@@ -60,21 +60,22 @@ def _table(rng, nok, nchan):
                 covariance=rng.normal(size=(nok, 5, 5)), batch_duration=0.37)
 
 
-def _ctx(nu_refs, bary, fit_scat, print_phase):
+def _ctx(nu_refs, bary, fit_scat, print_phase, print_flux=False):
     return dict(quiet=True, tscrunch=False, fit_scat=fit_scat,
                 method="trust-ncg", bounds=[None], by_archive=False,
                 nu_fit_tuple=None, nu_ref_tuple=nu_refs, bary=bary,
-                print_phase=print_phase, print_flux=False,
+                print_phase=print_phase, print_flux=print_flux,
                 print_parangle=True, addtnl_toa_flags={"pta": "X"})
 
 
 def _run(fast, flags, bary, log10_tau, scat_guess, nu_refs, print_phase,
-         ok_common=True):
+         ok_common=True, print_flux=False):
     rng = np.random.default_rng(17)
     nsub, nchan, nbin = 9, 24, 256
     d = _archive(rng, nsub, nchan, nbin, ok_common)
     g = _gt(flags, bary, log10_tau, scat_guess)
-    ctx = _ctx(nu_refs, bary, bool(flags[3]), print_phase)
+    ctx = _ctx(nu_refs, bary, bool(flags[3]), print_phase, print_flux)
+    models = np.random.default_rng(5).normal(2.0, 1.0, (2, nchan, 8))
     ok_isubs = list(d.ok_isubs)
     nu_fits_a = list(np.zeros([nsub, 3]))
     nu_refs_a = list(np.zeros([nsub, 3]))
@@ -90,7 +91,8 @@ def _run(fast, flags, bary, log10_tau, scat_guess, nu_refs, print_phase,
         job = dict(d=d, datafile="a.fits", nsub=nsub, nchan=nchan, nbin=nbin,
                    obs=None, nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a,
                    MJDs=np.zeros(nsub), DM0=10.0, ok_isubs=ok_isubs,
-                   nok=len(ok_isubs), models=None, model_index=None,
+                   nok=len(ok_isubs), models=models,
+                   model_index=np.arange(len(ok_isubs)) % 2,
                    mask=mask, flags_b=flags_b, fit_duration=0.0)
         g._book_archive(job, _table(rng, len(ok_isubs), nchan), ctx, 0.0)
     finally:
@@ -116,22 +118,27 @@ def _same(a, b):
 
 
 CASES = [
-    ([1, 1, 0, 0, 0], True, False, None, None, False),
+    ([1, 1, 0, 0, 0], True, False, None, None, False, True),
     ([1, 1, 0, 0, 0], False, False, None, (1400.0, 1400.0, 1400.0), True),
     ([1, 1, 1, 0, 0], True, False, None, None, True),
     ([1, 0, 0, 0, 0], True, False, None, None, False),
     ([1, 1, 0, 1, 1], True, True, (1e-4, 1500.0, -4.0), None, False),
     ([1, 1, 0, 1, 1], True, False, None, (1500.0, 1500.0, 1500.0), False),
-    ([1, 1, 0, 1, 0], False, True, None, None, True),
+    ([1, 1, 0, 1, 0], False, True, None, None, True, True),
 ]
 
 
 @pytest.mark.parametrize("case", CASES)
 def test_uniform_paths_equal_loops(case):
-    flags, bary, log10_tau, sg, nu_refs, pp = case
-    used, gf, nf_f, fast = _run(True, flags, bary, log10_tau, sg, nu_refs, pp)
+    flags, bary, log10_tau, sg, nu_refs, pp = case[:6]
+    pf = case[6] if len(case) > 6 else False
+    used, gf, nf_f, fast = _run(True, flags, bary, log10_tau, sg, nu_refs, pp,
+                                print_flux=pf)
     assert used
-    _, gs, nf_s, slow = _run(False, flags, bary, log10_tau, sg, nu_refs, pp)
+    _, gs, nf_s, slow = _run(False, flags, bary, log10_tau, sg, nu_refs, pp,
+                             print_flux=pf)
+    if pf:
+        assert np.all(np.asarray(fast.fluxes[0]) != 0.0)
     _same(list(gf), list(gs))
     _same(nf_f, nf_s)
     for a in pptoas._ATTRS:
@@ -153,3 +160,19 @@ def test_ragged_channels_take_the_loop():
     used, *_ = _run(True, [1, 1, 0, 0, 0], True, False, None, None, False,
                     ok_common=False)
     assert not used
+
+
+def test_flux_is_the_scattered_model_mean():
+    """print_flux takes each model row's mean: the scattered model's mean
+    (the reference's rfft / irfft round trip, pptoas.py:628-636) is the same
+    number up to rounding."""
+    from pulseportraiture_amd.pplib import (scattering_portrait_FT,
+                                            scattering_times)
+    rng = np.random.default_rng(2)
+    model = rng.normal(3.0, 1.0, (16, 256))
+    freqs = np.linspace(1100.0, 1900.0, 16)
+    scat = np.fft.irfft(scattering_portrait_FT(scattering_times(
+        0.03, -4.0, freqs, 1500.0), 256) * np.fft.rfft(model, axis=1),
+        axis=1)
+    np.testing.assert_allclose(scat.mean(axis=1), model.mean(axis=1),
+                               rtol=1e-14)

@@ -474,11 +474,15 @@ class GetTOAs(object):
         # is prepared (a PSRFITS archive's file read, upload and device
         # unpack: psrfits.load_data, whose reads and copies release the
         # GIL); the reference's first load_data call, made ahead of time,
-        # with the same arguments.  PPF_LOAD_DEPTH loads more archives ahead
-        # on as many threads: measured slower (16-bit PSRFITS, 32 archives:
-        # depth 1 6.1-6.2k, 2 5.1-5.6k, 3 4.7-5.3k TOAs/s in one call; the
-        # file reads and pinned copies share the host's memory bandwidth)
+        # with the same arguments.  PPF_LOAD_DEPTH loads more archives at
+        # once on as many threads: measured slower (16-bit PSRFITS, 32
+        # archives: depth 1 6.1-6.2k, 2 5.1-5.6k, 3 4.7-5.3k TOAs/s in one
+        # call; the file reads and pinned copies share the host's memory
+        # bandwidth).  PPF_LOAD_AHEAD archives are queued ahead on those
+        # threads (a PSRFITS load returns once its upload and unpack are
+        # queued, so the one loader thread keeps reading)
         depth = max(1, int(os.environ.get("PPF_LOAD_DEPTH", "1")))
+        ahead_n = max(depth, int(os.environ.get("PPF_LOAD_AHEAD", "2")))
         loader = ThreadPoolExecutor(max_workers=depth)
         mine = list(mine)
         loads = {}
@@ -502,7 +506,7 @@ class GetTOAs(object):
         err = None
         try:
             for pos, iarch in enumerate(mine):
-                for ahead in range(depth + 1):
+                for ahead in range(ahead_n + 1):
                     if pos + ahead < len(mine) and mine[pos + ahead] not in loads:
                         nxt = mine[pos + ahead]
                         loads[nxt] = loader.submit(_load, datafiles[nxt])

@@ -436,6 +436,7 @@ class GetTOAs(object):
         self.add_instrumental_response = add_instrumental_response
         self._ff = [None]   # fit_flags carried across sub-ints (pptoas.py:519-529)
         self._mcache = {}   # template portraits of this call (_models)
+        self._fit_ws = {}   # the fit worker's workspace (_fit_share)
         # With several ranks and at least as many archives as ranks, each
         # rank loads and fits only its own contiguous block of archives
         # (pptoas.py:258) and the per-archive results are
@@ -905,7 +906,8 @@ class GetTOAs(object):
                 _dist.raise_if_any_failed(err, dev if nccl else None)
                 table = _dist.allgather_rows(table if nccl else table.cpu(),
                                              nok, job["world"])
-            r = _unpack(table.cpu().numpy(), nchan)
+            with span("fit.d2h"):
+                r = _unpack(table.cpu().numpy(), nchan)
             _sp.__exit__(None, None, None)
         job["staged"].release()
         r["batch_duration"] = time.time() - t_fit
@@ -917,6 +919,9 @@ class GetTOAs(object):
         if not count:
             return torch.zeros((0, _table_width(nchan)), dtype=torch.float64,
                                device=dev)
+        _sp = span("fit.call")
+        _sp.__enter__()
+        ws = self.__dict__.setdefault("_fit_ws", {})
         res = engine.fit_batch(
             data_t, job["models"], d.freqs[isubs], d.Ps[isubs],
             job["init"][sl], job["flags_b"][sl], nu_fits=job["nu_fit_b"][sl],
@@ -928,7 +933,13 @@ class GetTOAs(object):
             guess_DM=np.full(count, job["DM_stored"]), guess_Ns=100,
             guess_tau=job["guess_tau"][sl] if ctx["fit_scat"] else None,
             bounds=_box(job["bounds"], 5) if ctx["method"] == "TNC" else None,
-            dev=dev)
+            dev=dev, workspace=ws.get(dev), max_workspace=ws.get("max"))
+        # the workspace is reused by the next archive's call on this (the
+        # worker's) stream; the budget is the free HBM at the first call
+        ws[dev] = res.get("workspace")
+        if "max" not in ws and torch.cuda.is_available():
+            ws["max"] = torch.cuda.mem_get_info(dev)[0] // 2
+        _sp.__exit__(None, None, None)
         return _pack(res)
 
     def _book_uniform(self, job, r, ctx, fit_duration, out):

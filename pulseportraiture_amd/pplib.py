@@ -68,6 +68,13 @@ class MJD(object):
         k = math.floor(f)
         self._i, self._f = i + k, f - k
 
+    @classmethod
+    def _make(cls, i, f):
+        """An MJD from an integer day and a fraction already in [0, 1)."""
+        m = cls.__new__(cls)
+        m._i, m._f = i, f
+        return m
+
     def __add__(self, other):
         if isinstance(other, MJD):
             return MJD(self._i + other._i, self._f + other._f)

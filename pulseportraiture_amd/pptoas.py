@@ -64,6 +64,12 @@ def _MJD(days):
     return _PSRCHIVE[0](days)
 
 
+def _MJD_is_plain():
+    """True when TOA epochs are pplib.MJD (no PSRCHIVE bindings)."""
+    _MJD(0.0)
+    return _PSRCHIVE[0] is _pplib.MJD
+
+
 def _rank_world():
     """(rank, world) when torch.distributed runs more than one rank."""
     if _dist.is_dist():
@@ -987,17 +993,25 @@ class GetTOAs(object):
             perrs[:, 4]
         out["nfevals"][rows] = Rt[:, I["nfeval"]].astype(int)
         out["rcs"][rows] = st & 0xff
-        out["scales"][rows] = np.where(okb, r["scales"], 0.0)
-        out["scale_errs"][rows] = np.where(okb, r["scale_errs"], 0.0)
-        out["channel_snrs"][rows] = np.where(okb, r["channel_snrs"], 0.0)
+        # every channel usable (the common archive): plain copies; a
+        # contiguous run of sub-ints: slices instead of gathers
+        allok = bool(okb.all())
+        rs = slice(int(rows[0]), int(rows[-1]) + 1) \
+            if int(rows[-1]) - int(rows[0]) + 1 == nok else rows
+        for key in ("scales", "scale_errs", "channel_snrs"):
+            out[key][rs] = r[key] if allok else np.where(okb, r[key], 0.0)
         out["snrs"][rows] = Rt[:, I["snr"]]
         out["red_chi2s"][rows] = Rt[:, I["red_chi2"]]
         nfit = self.nfit
-        out["covariances"][rows] = r["covariance"][:, :nfit, :nfit]
-        F = np.asarray(d.freqs)[rows]
-        nchx = okb.sum(axis=1)
-        fmax = np.where(okb, F, -np.inf).max(axis=1)
-        fmin = np.where(okb, F, np.inf).min(axis=1)
+        out["covariances"][rs] = r["covariance"][:, :nfit, :nfit]
+        F = np.asarray(d.freqs)[rs]
+        if allok:
+            nchx = np.full(nok, nchan)
+            fmax, fmin = F.max(axis=1), F.min(axis=1)
+        else:
+            nchx = okb.sum(axis=1)
+            fmax = np.where(okb, F, -np.inf).max(axis=1)
+            fmin = np.where(okb, F, np.inf).min(axis=1)
         snr_c, gof_c = Rt[:, I["snr"]], Rt[:, I["red_chi2"]]
         cov01 = ctx["nu_ref_tuple"] is not None and all(ff[:2])
         common = [("be", d.backend), ("fe", d.frontend),
@@ -1019,59 +1033,89 @@ class GetTOAs(object):
                     pf[isub, ok], pfe[isub, ok])
                 out["flux_freqs"][isub], _ = weighted_mean(F[j][ok],
                                                            pfe[isub, ok])
-        for j, isub in enumerate(ok_isubs):
-            P = d.Ps[isub]
-            phi = params[j, 0]
-            toa = d.epochs[isub] + _MJD((phi * P + d.backend_delay) /
-                                        (3600 * 24.))
-            toa_err = perrs[j, 0] * P * 1e6
-            df = d.doppler_factors[isub] if self.bary else 1.0
-            nu_refs_a[isub] = [nuo[j, 0], nuo[j, 1], nuo[j, 2]]
-            TOAs[isub], TOA_errs[isub] = toa, toa_err
-            toa_flags = {}
-            if ff[2]:
-                toa_flags["gm"] = GMv[j]
-                toa_flags["gm_err"] = perrs[j, 2]
-            if ff[3]:
-                tau, tau_err = params[j, 3], perrs[j, 3]
-                if self.log10_tau:
-                    toa_flags["scat_time"] = 10 ** tau * P / df * 1e6
-                    toa_flags["log10_scat_time"] = tau + np.log10(P / df)
-                    toa_flags["log10_scat_time_err"] = tau_err
-                else:
-                    toa_flags["scat_time"] = tau * P / df * 1e6
-                    toa_flags["scat_time_err"] = tau_err * P / df * 1e6
-                toa_flags["scat_ref_freq"] = nuo[j, 2] * df
-                toa_flags["scat_ind"] = params[j, 4]
-            if ff[4]:
-                toa_flags["scat_ind_err"] = perrs[j, 4]
-            toa_flags.update(common)
-            toa_flags["nchx"] = int(nchx[j])
-            toa_flags["bw"] = fmax[j] - fmin[j]
-            toa_flags["chbw"] = chbw
-            toa_flags["subint"] = isub
-            toa_flags["tobs"] = d.subtimes[isub]
-            toa_flags["fratio"] = fmax[j] / fmin[j]
-            toa_flags["tmplt"] = self.modelfile
-            toa_flags["snr"] = snr_c[j]
-            if cov01:
-                toa_flags["phi_DM_cov"] = r["covariance"][j, 0, 1]
-            toa_flags["gof"] = gof_c[j]
-            if ctx["print_phase"]:
-                toa_flags["phs"] = phi
-                toa_flags["phs_err"] = perrs[j, 0]
-            if print_flux:
-                toa_flags["flux"] = out["fluxes"][isub]
-                toa_flags["flux_err"] = out["flux_errs"][isub]
-                toa_flags["flux_ref_freq"] = out["flux_freqs"][isub]
-            if ctx["print_parangle"]:
-                toa_flags["par_angle"] = d.parallactic_angles[isub]
-            for k, v in ctx["addtnl_toa_flags"].items():
-                toa_flags[k] = v
-            self.TOA_list.append(TOA(
-                datafile, nuo[j, 0], toa, toa_err, d.telescope,
-                d.telescope_code, DMv[j] if ff[1] else None,
-                perrs[j, 1] if ff[1] else None, toa_flags))
+        # the TOA epochs, in whole arrays: epoch + MJD((phi P + backend
+        # delay) / 86400), the same additions and floors pplib.MJD makes
+        # one TOA at a time (pptoas.py:578-580)
+        Ps_r = np.asarray(d.Ps)[rows]
+        dd = (params[:, 0] * Ps_r + d.backend_delay) / (3600 * 24.)
+        toa_err = perrs[:, 0] * Ps_r * 1e6
+        eps = [d.epochs[i] for i in ok_isubs]
+        if _MJD_is_plain() and all(type(e) is _pplib.MJD for e in eps):
+            mi = np.floor(dd)
+            F = np.array([e._f for e in eps]) + (dd - mi)
+            K = np.floor(F)
+            I = np.array([e._i for e in eps], dtype=np.int64) + \
+                mi.astype(np.int64) + K.astype(np.int64)
+            toas = [_pplib.MJD._make(i, f) for i, f in zip(I.tolist(),
+                                                          (F - K).tolist())]
+        else:
+            toas = [e + _MJD(x) for e, x in zip(eps, dd)]
+        # the flag columns (one value per TOA, in the reference's key order)
+        keys, cols = [], []
+
+        def col(k, v):
+            keys.append(k)
+            cols.append(v)
+        Pl, errl = list(Ps_r), list(toa_err)
+        if self.bary:
+            dfl = list(np.asarray(d.doppler_factors)[rows])
+        else:
+            dfl = [1.0] * nok
+        if ff[2]:
+            col("gm", list(GMv))
+            col("gm_err", list(perrs[:, 2]))
+        if ff[3]:
+            taus_l, terr_l = list(params[:, 3]), list(perrs[:, 3])
+            if self.log10_tau:
+                col("scat_time", [10 ** t * P / df * 1e6 for t, P, df in
+                                  zip(taus_l, Pl, dfl)])
+                col("log10_scat_time", [t + np.log10(P / df) for t, P, df in
+                                        zip(taus_l, Pl, dfl)])
+                col("log10_scat_time_err", terr_l)
+            else:
+                col("scat_time", [t * P / df * 1e6 for t, P, df in
+                                  zip(taus_l, Pl, dfl)])
+                col("scat_time_err", [e * P / df * 1e6 for e, P, df in
+                                      zip(terr_l, Pl, dfl)])
+            col("scat_ref_freq", [v * df for v, df in zip(list(nuo[:, 2]),
+                                                          dfl)])
+            col("scat_ind", list(params[:, 4]))
+        if ff[4]:
+            col("scat_ind_err", list(perrs[:, 4]))
+        for k, v in common:
+            col(k, [v] * nok)
+        col("nchx", nchx.tolist())
+        col("bw", list(fmax - fmin))
+        col("chbw", [chbw] * nok)
+        col("subint", list(ok_isubs))
+        col("tobs", [d.subtimes[i] for i in ok_isubs])
+        col("fratio", list(fmax / fmin))
+        col("tmplt", [self.modelfile] * nok)
+        col("snr", list(snr_c))
+        if cov01:
+            col("phi_DM_cov", list(r["covariance"][:, 0, 1]))
+        col("gof", list(gof_c))
+        if ctx["print_phase"]:
+            col("phs", list(params[:, 0]))
+            col("phs_err", list(perrs[:, 0]))
+        if print_flux:
+            col("flux", [out["fluxes"][i] for i in ok_isubs])
+            col("flux_err", [out["flux_errs"][i] for i in ok_isubs])
+            col("flux_ref_freq", [out["flux_freqs"][i] for i in ok_isubs])
+        if ctx["print_parangle"]:
+            col("par_angle", [d.parallactic_angles[i] for i in ok_isubs])
+        for k, v in ctx["addtnl_toa_flags"].items():
+            col(k, [v] * nok)
+        nul = [list(v) for v in nuo]
+        DMl = list(DMv) if ff[1] else [None] * nok
+        DMel = list(perrs[:, 1]) if ff[1] else [None] * nok
+        tel, code = d.telescope, d.telescope_code
+        for j, (isub, vals) in enumerate(zip(ok_isubs, zip(*cols))):
+            nu_refs_a[isub] = nul[j]
+            TOAs[isub], TOA_errs[isub] = toas[j], errl[j]
+            self.TOA_list.append(TOA(datafile, nul[j][0], toas[j], errl[j],
+                                     tel, code, DMl[j], DMel[j],
+                                     dict(zip(keys, vals))))
         return fit_duration
 
     def _book_archive(self, job, r, ctx, start):

@@ -30,7 +30,9 @@ def _gt(fit_flags, bary, log10_tau, scat_guess):
 def _archive(rng, nsub, nchan, nbin, ok_common=True):
     freqs = np.linspace(1100.0, 1900.0, nchan)
     chans = np.arange(nchan)
-    if ok_common:
+    if ok_common == "all":
+        ok = [chans] * nsub
+    elif ok_common:
         ok = [chans[chans % 7 != 3]] * nsub
     else:
         ok = [chans[(chans + i) % 5 != 0] for i in range(nsub)]
@@ -129,14 +131,15 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_uniform_paths_equal_loops(case):
+@pytest.mark.parametrize("chans", [True, "all"])
+def test_uniform_paths_equal_loops(case, chans):
     flags, bary, log10_tau, sg, nu_refs, pp = case[:6]
     pf = case[6] if len(case) > 6 else False
     used, gf, nf_f, fast = _run(True, flags, bary, log10_tau, sg, nu_refs, pp,
-                                print_flux=pf)
+                                ok_common=chans, print_flux=pf)
     assert used
     _, gs, nf_s, slow = _run(False, flags, bary, log10_tau, sg, nu_refs, pp,
-                             print_flux=pf)
+                             ok_common=chans, print_flux=pf)
     if pf:
         assert np.all(np.asarray(fast.fluxes[0]) != 0.0)
     _same(list(gf), list(gs))

@@ -603,24 +603,25 @@ def bench_gettoas(args):
     if args.timeline and rank == 0:
         spans = timeline.dump()
         summ = {}
-        for name, th, a, b in spans:
-            e = summ.setdefault(name, dict(count=0, total_ms=0.0, threads=[]))
+        for name, th, a, b, c in spans:
+            e = summ.setdefault(name, dict(count=0, total_ms=0.0, cpu_ms=0.0,
+                                           threads=[]))
             e["count"] += 1
             e["total_ms"] += (b - a) * 1e3
+            e["cpu_ms"] += c * 1e3
             if th not in e["threads"]:
                 e["threads"].append(th)
-        busy = {}
-        for name, th, a, b in spans:
-            if "." not in name or name.startswith("main."):
-                busy[th] = busy.get(th, 0.0) + (b - a) * 1e3
         with open(args.timeline, "w") as fh:
             json.dump(dict(step_ms=(te - ts) * 1e3, ntoa=nfile * per,
                            stages={k: dict(v, mean_ms=v["total_ms"] /
+                                           v["count"],
+                                           mean_cpu_ms=v["cpu_ms"] /
                                            v["count"])
                                    for k, v in sorted(summ.items())},
                            spans=[(n, th, round((a - ts) * 1e3, 3),
-                                   round((b - ts) * 1e3, 3))
-                                  for n, th, a, b in spans]), fh, indent=1)
+                                   round((b - ts) * 1e3, 3),
+                                   round(c * 1e3, 3))
+                                  for n, th, a, b, c in spans]), fh, indent=1)
     ntoa = nfile * per
     out = dict(metric="GetTOAs end-to-end sub-int TOAs/sec (phase+DM, "
                       "%dch×%dbin, host archives, PCIe + bookkeeping "

@@ -269,7 +269,7 @@ class PSRFITS(object):
                         raise IOError("short read of %s row %d" %
                                       (self.filename, r))
                     done += k
-        nw = min(8, self.nsub)
+        nw = min(_READ_THREADS, self.nsub)
         cuts = [self.nsub * i // nw for i in range(nw + 1)]
         futs = [_reader_pool().submit(rows, cuts[i], cuts[i + 1])
                 for i in range(nw)]
@@ -278,12 +278,14 @@ class PSRFITS(object):
 
 
 _POOL = []
+# threads of the positioned DATA reads (env PPF_READ_THREADS, default 8)
+_READ_THREADS = max(1, int(os.environ.get("PPF_READ_THREADS", "8")))
 
 
 def _reader_pool():
     if not _POOL:
         from concurrent.futures import ThreadPoolExecutor
-        _POOL.append(ThreadPoolExecutor(max_workers=8))
+        _POOL.append(ThreadPoolExecutor(max_workers=_READ_THREADS))
     return _POOL[0]
 
 
@@ -592,6 +594,28 @@ def _pinned_buffer(dev, nbytes):
     return buf, slot
 
 
+# page-locked buffers for the statistics download (stats, total profiles,
+# noise), taken by a load and given back once finish() has copied them out
+_PACKED = []
+
+
+def _packed_take(n):
+    import torch
+    with _PINNED_LOCK:
+        for i, b in enumerate(_PACKED):
+            if b.numel() >= n:
+                return _PACKED.pop(i)[:n]
+    return torch.empty(max(n, 1 << 16), dtype=torch.float64,
+                       pin_memory=True)[:n]
+
+
+def _packed_give(buf):
+    base = buf._base if buf._base is not None else buf
+    with _PINNED_LOCK:
+        if len(_PACKED) < 8:
+            _PACKED.append(base)
+
+
 class _Pending(object):
     """load_data's two halves: __init__ parses the file, reads the DATA
     bytes into a page-locked buffer and queues the upload and the device
@@ -682,8 +706,7 @@ class _Pending(object):
                     packed = torch.cat([out["stats"].reshape(-1),
                                         out["total"].reshape(-1),
                                         noise.reshape(-1)])
-                    self.packed_h = torch.empty(packed.shape, dtype=packed.dtype,
-                                                pin_memory=True)
+                    self.packed_h = _packed_take(packed.numel())
                     self.packed_h.copy_(packed, non_blocking=True)
                     self.ev = torch.cuda.Event()
                     self.ev.record(st)
@@ -764,13 +787,15 @@ class _Pending(object):
         return out
 
     def finish(self):
-        from . import pplib
         from .timeline import span
         with span("load.wait"):
             self.ev.synchronize()
         self._keep = None
         with span("load.meta"):
-            return self._bunch()
+            data = self._bunch()
+        _packed_give(self.packed_h)
+        self.packed_h = None
+        return data
 
     def _bunch(self):
         from . import pplib
@@ -789,7 +814,7 @@ class _Pending(object):
             par = np.array([par.mean()])
             doppler = np.ones(1)
             nsub = 1
-        packed = self.packed_h.numpy()
+        packed = self.packed_h.numpy()[:nsub * (nchan * 4 + nbin)].copy()
         n1, n2 = nsub * nchan * 3, nsub * nbin
         stats = packed[:n1].reshape(nsub, nchan, 3)
         total = packed[n1:n1 + n2].reshape(nsub, nbin)

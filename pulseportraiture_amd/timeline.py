@@ -1,8 +1,10 @@
 """Host timeline of the GetTOAs data plane (off unless PPF_TIMELINE=1).
 
 `span(name)` brackets one stage on the calling thread; `dump()` returns the
-recorded (name, thread, t0, t1) tuples (perf_counter seconds) and clears
-them.  tools/gettoas_timeline.py turns them into the per-stage breakdown
+recorded (name, thread, t0, t1, cpu) tuples (perf_counter seconds; cpu = the
+thread's CPU seconds inside the span, time.thread_time) and clears them.
+Wall time minus CPU time is waiting: for the device, for I/O, or for the
+GIL held by another thread.  tools/gettoas_timeline.py turns them into the per-stage breakdown
 committed under profiles/."""
 import os
 import threading
@@ -20,12 +22,15 @@ def span(name):
         yield
         return
     t0 = time.perf_counter()
+    c0 = time.thread_time()
     try:
         yield
     finally:
         t1 = time.perf_counter()
+        c1 = time.thread_time()
         with _lock:
-            _spans.append((name, threading.current_thread().name, t0, t1))
+            _spans.append((name, threading.current_thread().name, t0, t1,
+                           c1 - c0))
 
 
 def dump():

@@ -443,6 +443,10 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
 // the row loop.  The four waves' sums are added in wave order through LDS
 // (deterministic) and the block's partial profile is written once.
 // ===========================================================================
+// rows in flight per wave (1: the one being summed has a successor loading)
+#ifndef PPF_DSUM_DEPTH
+#define PPF_DSUM_DEPTH 2
+#endif
 template <int DT, int LOG2NB>
 // (capped at four waves per SIMD -- 128 VGPRs, nine spills -- it measured
 // 8.2 vs 7.1 ms per 10,000 C2 sub-ints)
@@ -499,6 +503,60 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = 0.0;
     double wsum = 0.0, wcnt = 0.0;
+#if PPF_DSUM_DEPTH >= 2
+    // two rows in flight per wave: the row being summed comes from one
+    // register buffer while the next two are loading (the second buffer and
+    // the refill of the first)
+    auto next_usable = [&](int m) {
+        m += kWaves;
+        while (m < c1 && !usable(m)) m += kWaves;
+        return m;
+    };
+    auto load = [&](VecT (&p)[NL], int m) {
+        // unconditional (a valid row when past the block): keeps p in VGPRs
+        const VecT *src = rows + (int64_t)(m < c1 ? m : c1 - 1) * (NB / VW);
+#pragma unroll
+        for (int i = 0; i < NL; ++i) p[i] = src[lane + 64 * i];
+    };
+    auto row = [&](VecT (&p)[NL], int m, int m2) {
+        wave_lds_sync();                      // the previous row's reads are issued
+#pragma unroll
+        for (int i = 0; i < NL; ++i) reinterpret_cast<VecT *>(xs)[lane + 64 * i] = p[i];
+        load(p, m2);
+        const int r = m - c0;
+        const double w = readlane_d(r < 64 ? t_w[0] : t_w[1], r & 63),
+                     f0 = readlane_d(r < 64 ? t_f[0] : t_f[1], r & 63);
+        const double tau = Dg * (1.0 / (f0 * f0) - nu_mean_m2);
+        const double fl = floor(tau), f = tau - fl;
+        const int i0 = (int)(fl - (double)NB * floor(fl / (double)NB));   // mod nbin
+        const double wa = w * (1.0 - f), wb = w * f;
+        wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int ia = (lane + 64 * j + i0) & (NB - 1);
+            acc[j] = fma(wa, (double)xs[ia], fma(wb, (double)xs[(ia + 1) & (NB - 1)], acc[j]));
+        }
+        wsum += w;
+        wcnt += 1.0;
+    };
+    int n = c0 + wave;
+    while (n < c1 && !usable(n)) n += kWaves;
+    int n1 = next_usable(n);
+    VecT pa[NL], pb[NL];
+    load(pa, n);
+    load(pb, n1);
+    while (n < c1) {
+        int n2 = next_usable(n1);
+        row(pa, n, n2);                       // pa: n -> n2
+        n = n1;
+        n1 = n2;
+        if (n >= c1) break;
+        n2 = next_usable(n1);
+        row(pb, n, n2);                       // pb: n -> the row after n1
+        n = n1;
+        n1 = n2;
+    }
+#else
     int n = c0 + wave;
     while (n < c1 && !usable(n)) n += kWaves;
     VecT pre[NL];
@@ -537,6 +595,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
         wcnt += 1.0;
         n = nn;
     }
+#endif
     // fixed-order sum of the four waves' profiles (LDS reused as NB doubles)
     __syncthreads();
     double *part = dlds;

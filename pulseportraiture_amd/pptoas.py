@@ -11,6 +11,7 @@ corrections, TOA flags, DeltaDM).  Archive I/O stays on PSRCHIVE via
 Reference: /root/reference/pptoas.py (file:line cited per block).
 """
 import contextlib
+import gc
 import os
 import threading
 import time
@@ -511,6 +512,12 @@ class GetTOAs(object):
                                  **({"defer": True} if _is_fits(f) else {}))
         pending = None
         err = None
+        # the cyclic garbage collector is paused for the loop (restored
+        # after): get_TOAs allocates a few objects per TOA that form no
+        # cycles, and a full collection over a large TOA list is a
+        # millisecond pause in whichever stage it lands
+        gc_on = gc.isenabled()
+        gc.disable()
         try:
             for pos, iarch in enumerate(mine):
                 for ahead in range(ahead_n + 1):
@@ -539,6 +546,8 @@ class GetTOAs(object):
                 raise
             err = exc
         finally:
+            if gc_on:
+                gc.enable()
             pool.shutdown(wait=True)
             for fu in loads.values():
                 fu.cancel()

@@ -278,6 +278,7 @@ class PSRFITS(object):
 
 
 _POOL = []
+_UPLOAD_CHUNK = int(os.environ.get("PPF_UPLOAD_CHUNK_MB", "0"))
 # threads of the positioned DATA reads (env PPF_READ_THREADS, default 8)
 _READ_THREADS = max(1, int(os.environ.get("PPF_READ_THREADS", "8")))
 
@@ -686,7 +687,14 @@ class _Pending(object):
                 aux_d = dbuf[nraw:nraw + naux].view(torch.float32)
                 with torch.cuda.stream(st):
                     aux_d.copy_(aux, non_blocking=True)
-                    raw_d.copy_(host, non_blocking=True)
+                    # in row chunks (env PPF_UPLOAD_CHUNK_MB, 0 = one copy):
+                    # a small copy queued meanwhile on another stream (the
+                    # fit worker's inputs) need not wait for the whole archive
+                    step = max(1, (_UPLOAD_CHUNK << 20) // max(nbytes, 1)) \
+                        if _UPLOAD_CHUNK > 0 else nsub
+                    for r0 in range(0, nsub, step):
+                        raw_d[r0:r0 + step].copy_(host[r0:r0 + step],
+                                                  non_blocking=True)
                     up = torch.cuda.Event()
                     up.record(st)
                     slot[1] = up                    # the buffer is free after it

@@ -931,7 +931,7 @@ def main():
     if momx_used:
         #  k_moments (first launch: every sub-int): read X below the cutoff
         #   and dphi, write 32 complex moments + the centre residual
-        kern["xmom"] = dict(name="k_moments", ms=kern_ms[0],
+        kern["moments"] = dict(name="k_moments", ms=kern_ms[0],
                             unit=xh * 16 + nchan * 16 + nchan * (32 * 16 + 8),
                             bytes=steps_subints * (xh * 16 + nchan * 16 +
                                                    nchan * (32 * 16 + 8)))
@@ -981,6 +981,19 @@ def main():
                         valu_active_per_wave=fk.get("valu_active_per_wave"),
                         clock_ghz=fk.get("clock_ghz"),
                         source=os.path.relpath(fpath, ROOT))
+            # VALU issue floor of one launch: 4 cycles per f64 and 2 per
+            # other wave64 VALU instruction (MI355X: 16 f64 / 32 f32 lanes
+            # per SIMD per clock) over the 1024 SIMDs at the clock the chip
+            # held; the launch's measured time over it
+            if fk.get("valu_all_per_unit") is not None and fk.get("clock_ghz"):
+                v64 = fk["valu_f64_per_unit"]
+                cyc = 4.0 * v64 + 2.0 * (fk["valu_all_per_unit"] - v64)
+                floor_ms = units_launch * cyc / (1024 * fk["clock_ghz"] * 1e9) * 1e3
+                fp64["issue_floor_ms"] = round(floor_ms, 4)
+                fp64["issue_floor_frac"] = round(floor_ms / (dk["ms"] / nlaunch), 4)
+                roof["issue_floor_ms"] = fp64["issue_floor_ms"]
+                roof["issue_floor_frac"] = fp64["issue_floor_frac"]
+                roof["valu_active_per_wave"] = fk.get("valu_active_per_wave")
     names = ["model_rfft", "xspec", "guess", "solve"]
     stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
     kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),

@@ -27,7 +27,8 @@ import os
 
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
            "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
-           "tr_mom": ("k_tr_mom", ""), "postfit": ("k_postfit", "")}
+           "tr_mom": ("k_tr_mom", ""), "postfit": ("k_postfit", ""),
+           "moments": ("k_moments", "")}
 
 
 def main():
@@ -41,7 +42,7 @@ def main():
     bench = json.loads(line)
     cfg = bench["config"]
     calls = bench["steps"] + bench["warmup"]
-    per_launch = min(cfg["chunk"], cfg["nsub_per_gpu"])
+    per_launch = min(cfg.get("chunk", cfg["nsub_per_gpu"]), cfg["nsub_per_gpu"])
     cnt = collections.defaultdict(lambda: collections.defaultdict(float))
     grbm_rows = collections.defaultdict(int)
     files = sorted(glob.glob(os.path.join(a.prof_dir, "*", "*counter_collection.csv")))

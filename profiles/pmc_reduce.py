@@ -16,6 +16,9 @@ the bench fit mode (phase+DM, full, scat) and kernel:
   pass  -- the streaming trust-region evaluation k_pass<true>; unit = one
            evaluation of one sub-integration (the run's launches process
            nsub x mean_passes_per_fit evaluations per call)
+  moments -- k_moments (moments from the stored cross spectrum): every
+           launch, re-centring launches included, per sub-integration of a
+           launch (so a lower bound per first-pass sub-integration)
 """
 import argparse
 import collections
@@ -25,7 +28,8 @@ import json
 import os
 
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
-           "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", "")}
+           "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
+           "moments": ("k_moments", ""), "noise": ("k_noise_w<", "")}
 
 
 def load(d):
@@ -49,7 +53,7 @@ def main():
     cfg = bench["config"]
     mode = cfg["fit"]
     calls = bench["steps"] + bench["warmup"]
-    per_launch = min(cfg["chunk"], cfg["nsub_per_gpu"])
+    per_launch = min(cfg.get("chunk", cfg["nsub_per_gpu"]), cfg["nsub_per_gpu"])
     fr = load(os.path.join(a.prof_dir, "fetch"))
     wr = load(os.path.join(a.prof_dir, "write"))
     KiB = 1024.0

@@ -443,9 +443,11 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
 // the row loop.  The four waves' sums are added in wave order through LDS
 // (deterministic) and the block's partial profile is written once.
 // ===========================================================================
-// rows in flight per wave (1: the one being summed has a successor loading)
+// rows in flight per wave (1: the one being summed has a successor loading;
+// 2 measured slower: C5 k_dsum_w 9.25 vs 8.39 ms per 500 sub-ints, the
+// extra VGPRs cost occupancy)
 #ifndef PPF_DSUM_DEPTH
-#define PPF_DSUM_DEPTH 2
+#define PPF_DSUM_DEPTH 1
 #endif
 template <int DT, int LOG2NB>
 // (capped at four waves per SIMD -- 128 VGPRs, nine spills -- it measured

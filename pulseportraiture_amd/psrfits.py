@@ -278,9 +278,23 @@ class PSRFITS(object):
 
 
 _POOL = []
-_UPLOAD_CHUNK = int(os.environ.get("PPF_UPLOAD_CHUNK_MB", "0"))
+# archive uploads in chunks of this many MiB (env PPF_UPLOAD_CHUNK_MB; 0 =
+# one copy): GetTOAs from 16-bit PSRFITS 13.7k vs 13.0k TOAs/s at 16
+_UPLOAD_CHUNK = int(os.environ.get("PPF_UPLOAD_CHUNK_MB", "16"))
 # threads of the positioned DATA reads (env PPF_READ_THREADS, default 8)
 _READ_THREADS = max(1, int(os.environ.get("PPF_READ_THREADS", "8")))
+
+
+_MASTER = []
+
+
+def _read_master():
+    """The thread that runs one archive's read_data_into at a time (which
+    fans out to _reader_pool), so a loader can parse the next file meanwhile."""
+    if not _MASTER:
+        from concurrent.futures import ThreadPoolExecutor
+        _MASTER.append(ThreadPoolExecutor(max_workers=1))
+    return _MASTER[0]
 
 
 def _reader_pool():
@@ -534,7 +548,7 @@ _TLS = threading.local()
 def load_data(filename, state=None, dedisperse=False, dededisperse=False,
               tscrunch=False, pscrunch=False, fscrunch=False, rm_baseline=True,
               flux_prof=False, refresh_arch=True, return_arch=True, quiet=False,
-              dev=None, defer=False):
+              dev=None, defer=False, lazy=False):
     """pplib.load_data (pplib.py:2749-2915) for fold-mode PSRFITS without
     PSRCHIVE.  The DATA bytes are read from the file into a page-locked
     buffer and uploaded; the device unpacks them, sums the polarisations
@@ -563,7 +577,11 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
 
     defer=True returns a _Pending whose finish() gives the DataBunch: the
     read is done and the device work queued, but nothing waits for the
-    device (get_TOAs' loader thread reads the next archive meanwhile)."""
+    device (get_TOAs' loader thread reads the next archive meanwhile).
+    lazy=True (with defer) returns as soon as the file is parsed and its
+    DATA read has started on a reader thread; the upload and device work
+    are queued by queue() (get_TOAs' loader calls it for archive i while
+    archive i+1 is being read) or else by finish()."""
     if fscrunch:
         raise NotImplementedError("load_data(fscrunch) needs PSRCHIVE; the "
                                   "PSRFITS fast path keeps every channel")
@@ -571,6 +589,8 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
         raise NotImplementedError("state=%r needs PSRCHIVE" % state)
     pend = _Pending(filename, pscrunch, state, rm_baseline, quiet, dev,
                     dedisperse=bool(dedisperse), tscrunch=bool(tscrunch))
+    if not (defer and lazy):
+        pend.queue()
     return pend if defer else pend.finish()
 
 
@@ -666,12 +686,7 @@ class _Pending(object):
         nraw = -(-nsub * nbytes // 256) * 256
         nsc = nsub * npol * nchan
         naux = 4 * (2 * nsc + nsub * nchan)
-        if not hasattr(_TLS, "streams"):
-            _TLS.streams = {}
         with torch.cuda.device(dev):
-            st = _TLS.streams.get(dev.index)
-            if st is None:
-                st = _TLS.streams[dev.index] = torch.cuda.Stream(dev)
             buf, slot = _pinned_buffer(dev, nraw + naux)
             host = buf[:nsub * nbytes].view(nsub, nbytes)
             aux = buf[nraw:nraw + naux].view(torch.float32)
@@ -679,15 +694,60 @@ class _Pending(object):
             a[:nsc] = scl.reshape(-1)
             a[nsc:2 * nsc] = offs.reshape(-1)
             a[2 * nsc:] = self.weights.reshape(-1)
-            with span("load.read"):
-                f.read_data_into(nbytes, host.numpy())
+        # the rest of the metadata while the file is open
+        self.tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
+            if f.subint.has("TSUBINT") else np.zeros(nsub)
+        self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
+            if f.subint.has("PAR_ANG") else np.zeros(nsub)
+        self.pred = _PolycoRows(f.polyco) if (
+            tscrunch and f.polyco is not None and f.polyco.nrows) else None
+        del raw
+        # the DATA read runs on the reader threads from here; queue() waits
+        # for it and starts the upload
+        self._rfut = _read_master().submit(f.read_data_into, nbytes,
+                                           host.numpy())
+        self._q = dict(dev=dev, buf=buf, slot=slot, host=host, aux=aux,
+                       nraw=nraw, naux=naux, nsc=nsc, nbytes=nbytes,
+                       elem=elem, pol_mode=pol_mode, rm_baseline=rm_baseline)
+        self._qlock = threading.Lock()
+        self._queued = False
+
+    def queue(self):
+        """Wait for the DATA read, then queue the upload, the device unpack,
+        baseline, statistics and noise and the statistics download on this
+        thread's copy stream (once; later calls return at once)."""
+        import torch
+        from . import engine
+        from .timeline import span
+        with self._qlock:
+            if self._queued:
+                return
+            self._queued = True
+            self._queue(torch, engine, span)
+
+    def _queue(self, torch, engine, span):
+        q, f = self._q, self.f
+        nsub, npol, nchan, nbin = f.nsub, f.npol, f.nchan, f.nbin
+        dev, slot, host, aux = q["dev"], q["slot"], q["host"], q["aux"]
+        nraw, naux, nsc, nbytes = q["nraw"], q["naux"], q["nsc"], q["nbytes"]
+        elem, pol_mode, rm_baseline = q["elem"], q["pol_mode"], \
+            q["rm_baseline"]
+        dedisperse, tscrunch = self.dedisperse, self.tscrunch
+        if not hasattr(_TLS, "streams"):
+            _TLS.streams = {}
+        with span("load.read"):
+            self._rfut.result()
+        with torch.cuda.device(dev):
+            st = _TLS.streams.get(dev.index)
+            if st is None:
+                st = _TLS.streams[dev.index] = torch.cuda.Stream(dev)
             with span("load.queue"):
                 dbuf = torch.empty(nraw + naux, dtype=torch.uint8, device=dev)
                 raw_d = dbuf[:nsub * nbytes].view(nsub, nbytes)
                 aux_d = dbuf[nraw:nraw + naux].view(torch.float32)
                 with torch.cuda.stream(st):
                     aux_d.copy_(aux, non_blocking=True)
-                    # in row chunks (env PPF_UPLOAD_CHUNK_MB, 0 = one copy):
+                    # in row chunks (PPF_UPLOAD_CHUNK_MB):
                     # a small copy queued meanwhile on another stream (the
                     # fit worker's inputs) need not wait for the whole archive
                     step = max(1, (_UPLOAD_CHUNK << 20) // max(nbytes, 1)) \
@@ -720,17 +780,9 @@ class _Pending(object):
                     self.ev.record(st)
             self.rows = out["rows"]
             self._keep = (dbuf, packed)
-        # the rest of the metadata, and the unmap (milliseconds for a large
-        # file), on this (loading) thread too
+        self._q = None
+        # the unmap (milliseconds for a large file) on this thread too
         with span("load.close"):
-            self.tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
-                if f.subint.has("TSUBINT") else np.zeros(nsub)
-            self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
-                if f.subint.has("PAR_ANG") else np.zeros(nsub)
-            self.pred = _PolycoRows(f.polyco) if (
-                tscrunch and f.polyco is not None and f.polyco.nrows) \
-                else None
-            del raw
             f.close()
 
     def _tscrunched_epoch(self):
@@ -796,6 +848,7 @@ class _Pending(object):
 
     def finish(self):
         from .timeline import span
+        self.queue()
         with span("load.wait"):
             self.ev.synchronize()
         self._keep = None

@@ -416,9 +416,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
     g.g_sum = S.g_sum; g.g_tau = S.g_tau; g.g_alpha = S.g_alpha;
     const double nuDM2 = pow(g.nu_DM, -2.0), nuGM4 = pow(g.nu_GM, -4.0);
 
-    double acc[21];
-#pragma unroll
-    for (int i = 0; i < 21; ++i) acc[i] = 0.0;
     // Newton warm start: only every S.sub-th group of 64 channels (a wave).
     // With a stride of four groups or more a workgroup holds at most one such
     // group, its first; then all four waves take that group's 64 channels and
@@ -553,6 +550,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
             }
         }
     }
+    // (the 21 sums come to life only after the harmonic loop)
+    double acc[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) acc[i] = 0.0;
     if (use_n && (!split || wave == 0)) {
         double my[10];
         my[0] = a0; my[1] = -kTwoPi * a1; my[2] = -kTwoPi * kTwoPi * a2;

@@ -65,10 +65,16 @@ def _MJD(days):
     return _PSRCHIVE[0](days)
 
 
+_MJD_ORIG = _MJD
+
+
 def _MJD_is_plain():
-    """True when TOA epochs are pplib.MJD (no PSRCHIVE bindings)."""
+    """True when TOA epochs are pplib.MJD: no PSRCHIVE bindings and _MJD
+    not replaced (tests substitute their own epoch type)."""
+    if _MJD is not _MJD_ORIG:
+        return False
     _MJD(0.0)
-    return _PSRCHIVE[0] is _pplib.MJD
+    return bool(_PSRCHIVE) and _PSRCHIVE[0] is _pplib.MJD
 
 
 def _rank_world():

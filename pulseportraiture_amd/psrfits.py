@@ -711,6 +711,7 @@ class _Pending(object):
                        elem=elem, pol_mode=pol_mode, rm_baseline=rm_baseline)
         self._qlock = threading.Lock()
         self._queued = False
+        self._m = self._meta()
 
     def queue(self):
         """Wait for the DATA read, then queue the upload, the device unpack,
@@ -858,7 +859,9 @@ class _Pending(object):
         self.packed_h = None
         return data
 
-    def _bunch(self):
+    def _meta(self):
+        """The DataBunch fields that need only the file (built on the loading
+        thread while the DATA read runs)."""
         from . import pplib
         f, filename, weights = self.f, self.filename, self.weights
         nsub, nchan, nbin = f.nsub, f.nchan, f.nbin
@@ -875,11 +878,6 @@ class _Pending(object):
             par = np.array([par.mean()])
             doppler = np.ones(1)
             nsub = 1
-        packed = self.packed_h.numpy()[:nsub * (nchan * 4 + nbin)].copy()
-        n1, n2 = nsub * nchan * 3, nsub * nbin
-        stats = packed[:n1].reshape(nsub, nchan, 3)
-        total = packed[n1:n1 + n2].reshape(nsub, nbin)
-        noise = packed[n1 + n2:].reshape(nsub, nchan)
         p, h = f.primary, f.subint.header
         epochs = [pplib.MJD(int(i), float(x)) for i, x in zip(imjd, frac)]
         weights_norm = np.where(weights == 0.0, 0.0, 1.0)
@@ -890,34 +888,45 @@ class _Pending(object):
             ok_ichans = [chans] * nsub
         else:
             ok_ichans = [chans[okc[isub]] for isub in range(nsub)]
-        masks = _Masks(weights_norm, nbin)
-        prof = total.sum(axis=0)
-        prof_SNR, prof_noise = _window_snr(prof)
         telescope = str(p.get("TELESCOP", "")).strip()
-        DM = float(h.get("DM", p.get("CHAN_DM", 0.0)))
-        if not self.quiet:
-            print("\nReading data from %s on source %s (PSRFITS fast "
-                  "path)..." % (filename, p.get("SRC_NAME", "")))
-        data = pplib.DataBunch(
+        return dict(
+            _nsub=nsub, _prof_norm=prof_norm,
             arch=None, backend=str(p.get("BACKEND", "")).strip(),
             backend_delay=float(p.get("BE_DELAY", 0.0)),
             bw=float(p.get("OBSBW", 0.0)), doppler_factors=doppler,
-            doppler_known=False, DM=DM,
+            doppler_known=False, DM=float(h.get("DM", p.get("CHAN_DM", 0.0))),
             dmc=int(self.dedisperse), epochs=epochs, filename=filename,
             flux_prof=np.array([]),
             freqs=freqs, frontend=str(p.get("FRONTEND", "")).strip(),
-            integration_length=float(tsub.sum()), masks=masks, nbin=nbin,
-            nchan=nchan, noise_stds=noise[:, None, :], npol=1, nsub=nsub,
+            integration_length=float(tsub.sum()),
+            masks=_Masks(weights_norm, nbin), nbin=nbin, nchan=nchan,
+            npol=1, nsub=nsub,
             nu0=float(p.get("OBSFREQ", self.freqs.mean())),
-            ok_ichans=ok_ichans,
-            ok_isubs=ok_isubs, parallactic_angles=par,
-            phases=pplib.get_bin_centers(nbin),
-            prof=prof / prof_norm,
-            prof_noise=prof_noise, prof_SNR=prof_SNR, Ps=Ps,
-            SNRs=stats[:, None, :, 2].copy(),
-            source=str(p.get("SRC_NAME", "")).strip(),
-            state="Intensity", subints=DeviceRows(self.rows, self.ev),
+            ok_ichans=ok_ichans, ok_isubs=ok_isubs, parallactic_angles=par,
+            phases=pplib.get_bin_centers(nbin), Ps=Ps,
+            source=str(p.get("SRC_NAME", "")).strip(), state="Intensity",
             subtimes=[float(tsub.sum())] if self.tscrunch else list(tsub),
-            telescope=telescope,
-            telescope_code=_telescope_code(telescope), weights=weights)
-        return data
+            telescope=telescope, telescope_code=_telescope_code(telescope),
+            weights=weights)
+
+    def _bunch(self):
+        from . import pplib
+        m = dict(self._m)
+        nsub, prof_norm = m.pop("_nsub"), m.pop("_prof_norm")
+        nchan, nbin = m["nchan"], m["nbin"]
+        packed = self.packed_h.numpy()
+        n1, n2 = nsub * nchan * 3, nsub * nbin
+        stats = packed[:n1].reshape(nsub, nchan, 3)
+        total = packed[n1:n1 + n2].reshape(nsub, nbin)
+        # (copies: the page-locked buffer goes back to its pool)
+        noise = packed[n1 + n2:n1 + n2 + nsub * nchan].reshape(nsub, nchan)
+        prof = total.sum(axis=0)
+        prof_SNR, prof_noise = _window_snr(prof)
+        if not self.quiet:
+            print("\nReading data from %s on source %s (PSRFITS fast "
+                  "path)..." % (self.filename, m["source"]))
+        return pplib.DataBunch(
+            noise_stds=noise[:, None, :].copy(), prof=prof / prof_norm,
+            prof_noise=prof_noise, prof_SNR=prof_SNR,
+            SNRs=stats[:, None, :, 2].copy(),
+            subints=DeviceRows(self.rows, self.ev), **m)

@@ -179,3 +179,16 @@ def test_flux_is_the_scattered_model_mean():
         axis=1)
     np.testing.assert_allclose(scat.mean(axis=1), model.mean(axis=1),
                                rtol=1e-14)
+
+
+def test_substituted_epoch_type_takes_the_object_path(monkeypatch):
+    """With pptoas._MJD replaced (PSRCHIVE's MJD, or a test's own type) the
+    TOA epochs are built one object at a time; the same values here."""
+    used, _, _, fast = _run(True, [1, 1, 0, 0, 0], True, False, None, None,
+                            False, ok_common="all")
+    monkeypatch.setattr(pptoas, "_MJD", lambda days: pplib.MJD(days))
+    assert not pptoas._MJD_is_plain()
+    _, _, _, obj = _run(True, [1, 1, 0, 0, 0], True, False, None, None,
+                        False, ok_common="all")
+    assert [repr(t.MJD) for t in fast.TOA_list] == \
+        [repr(t.MJD) for t in obj.TOA_list]

@@ -365,9 +365,17 @@ def bench_align(args):
     dom = max(kern, key=lambda k: kern[k]["ms"])
     dk = kern[dom]
     achieved = dk["bytes"] / (dk["ms"] / 1e3) / 1e9
+    # HBM traffic per launch from the PMC passes of the same command
+    # (profiles/pmc_reduce.py, mode "align")
+    traffic = None
+    if os.path.exists(args.pmc):
+        pk = json.load(open(args.pmc)).get("modes", {}).get(
+            "align", {}).get("kernels", {}).get(dom)
+        if pk:
+            traffic = round(pk["hbm_bytes"] * count)
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
                 unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                traffic=None, kernel=dk["name"],
+                traffic=traffic, kernel=dk["name"],
                 algorithmic_bytes_per_launch=dk["bytes"] / ncalls,
                 algorithmic_bytes_per_unit=dk["unit"],
                 avg_launch_ms=round(dk["ms"] / ncalls, 4), launches=ncalls,
@@ -912,7 +920,19 @@ def main():
     # or with the guess at nbin 2048 unless the fused pass is forced
     momx_used = not scat_fit and (args.mom_x == "x" or (
         args.mom_x == "auto" and nbin == 2048))
-    if scat_fit or momx_used:
+    # the wave-FFT kernels take power-of-two nbin in [256, 2048]; other
+    # lengths (the mixed-radix 1000, 1536, ...) run the block-FFT spectrum
+    # pass, which writes every harmonic of X, and k_moments
+    wave = (nbin & (nbin - 1)) == 0 and 256 <= nbin <= 2048
+    if not wave and not scat_fit:
+        xfull = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
+        kern["xspec"] = dict(name="k_xspec (block FFT)", ms=stage_ms[1],
+                             unit=xfull, bytes=steps_subints * xfull +
+                             ncalls * nchan * nharm * 16)
+        mu = xh * 16 + nchan * 16 + nchan * (32 * 16 + 8)
+        kern["moments"] = dict(name="k_moments", ms=kern_ms[0], unit=mu,
+                               bytes=steps_subints * mu)
+    elif scat_fit or momx_used:
         kern["xspec"] = dict(name="k_xspec_w<%d, 0>" % L2N, ms=stage_ms[1],
                              unit=xspec_unit,
                              bytes=steps_subints * xspec_unit +
@@ -928,14 +948,15 @@ def main():
         kern["pass"] = dict(name="k_pass<true>", ms=pass_ms, unit=pass_unit,
                             launches=int(pass_launches),
                             bytes=evals * pass_unit + pass_launches * xh * 8)
-    if momx_used:
+    if momx_used and wave:
         #  k_moments (first launch: every sub-int): read X below the cutoff
-        #   and dphi, write 32 complex moments + the centre residual
-        kern["moments"] = dict(name="k_moments", ms=kern_ms[0],
-                            unit=xh * 16 + nchan * 16 + nchan * (32 * 16 + 8),
-                            bytes=steps_subints * (xh * 16 + nchan * 16 +
-                                                   nchan * (32 * 16 + 8)))
-    elif not scat_fit:
+        #   and dphi, write 16 complex moments about each channel band's
+        #   centre (mom16, the X-moment path), the centre residual and the
+        #   band centre
+        mu = xh * 16 + nchan * 16 + nchan * (16 * 16 + 8 + 8)
+        kern["moments"] = dict(name="k_moments", ms=kern_ms[0], unit=mu,
+                               bytes=steps_subints * mu)
+    elif not scat_fit and wave:
         kern["xmom"] = dict(name="k_xmom_g<%d, 0, true, true>" % L2N,
                             ms=kern_ms[0], unit=xmom_unit,
                             bytes=steps_subints * xmom_unit +
@@ -1026,7 +1047,9 @@ def main():
                            harmonic_cutoff=not args.no_hcut,
                            solver=args.solver, mom_x=args.mom_x,
                            moments="cross spectrum (k_xspec_w + k_moments)"
-                           if momx_used else "fused pass (k_xmom_g)",
+                           if momx_used and wave else (
+                               "fused pass (k_xmom_g)" if wave else
+                               "cross spectrum (block FFT + k_moments)"),
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),

@@ -505,26 +505,21 @@ class GetTOAs(object):
         # device is per host thread, and a new thread starts on GPU 0
         ldev = engine.device() if torch.cuda.is_available() else None
 
-        prev = [None]
-
         def _load(f):
             # defer + lazy: a PSRFITS file is parsed and its DATA read
-            # started here; the previous archive's upload and device work are
-            # queued while this read runs (psrfits._Pending.queue), and
-            # _prep_archive's finish() queues whatever is still pending
+            # started here; the read thread queues its upload and device
+            # work when the read completes (psrfits._Pending), while this
+            # thread goes on to parse the next file; _prep_archive's finish()
+            # waits for them
             with (torch.cuda.device(ldev) if ldev is not None else
                   contextlib.nullcontext()):
-                d = load_data(f, dedisperse=False, dededisperse=False,
-                              tscrunch=tscrunch, pscrunch=True,
-                              fscrunch=False, rm_baseline=rm_baseline,
-                              flux_prof=False, refresh_arch=False,
-                              return_arch=False, quiet=quiet,
-                              **({"defer": True, "lazy": True}
-                                 if _is_fits(f) else {}))
-                if prev[0] is not None:
-                    prev[0].queue()
-                prev[0] = d if hasattr(d, "queue") else None
-                return d
+                return load_data(f, dedisperse=False, dededisperse=False,
+                                 tscrunch=tscrunch, pscrunch=True,
+                                 fscrunch=False, rm_baseline=rm_baseline,
+                                 flux_prof=False, refresh_arch=False,
+                                 return_arch=False, quiet=quiet,
+                                 **({"defer": True, "lazy": True}
+                                    if _is_fits(f) else {}))
         pending = None
         err = None
         # the cyclic garbage collector is paused for the loop (restored

@@ -579,9 +579,9 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
     read is done and the device work queued, but nothing waits for the
     device (get_TOAs' loader thread reads the next archive meanwhile).
     lazy=True (with defer) returns as soon as the file is parsed and its
-    DATA read has started on a reader thread; the upload and device work
-    are queued by queue() (get_TOAs' loader calls it for archive i while
-    archive i+1 is being read) or else by finish()."""
+    DATA read has started on the read thread, which queues the upload and
+    device work itself when the read completes (queue() / finish() wait for
+    that); without it load_data returns once they are queued."""
     if fscrunch:
         raise NotImplementedError("load_data(fscrunch) needs PSRCHIVE; the "
                                   "PSRFITS fast path keeps every channel")
@@ -598,6 +598,24 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
 # only once the upload that read it has completed (its event)
 _PINNED = {}
 _PINNED_LOCK = threading.Lock()
+
+
+class _UploadTicket(object):
+    """The last user of a pinned slot: synchronize() returns once that
+    load has queued its upload (queue()) and the upload has completed."""
+
+    def __init__(self):
+        self._done = threading.Event()
+        self.ev = None
+
+    def set(self, ev):
+        self.ev = ev
+        self._done.set()
+
+    def synchronize(self):
+        self._done.wait()
+        if self.ev is not None:
+            self.ev.synchronize()
 
 
 def _pinned_buffer(dev, nbytes):
@@ -688,6 +706,8 @@ class _Pending(object):
         naux = 4 * (2 * nsc + nsub * nchan)
         with torch.cuda.device(dev):
             buf, slot = _pinned_buffer(dev, nraw + naux)
+            # the next user of this slot waits for this load's upload
+            self._ticket = slot[1] = _UploadTicket()
             host = buf[:nsub * nbytes].view(nsub, nbytes)
             aux = buf[nraw:nraw + naux].view(torch.float32)
             a = aux.numpy()
@@ -702,21 +722,33 @@ class _Pending(object):
         self.pred = _PolycoRows(f.polyco) if (
             tscrunch and f.polyco is not None and f.polyco.nrows) else None
         del raw
-        # the DATA read runs on the reader threads from here; queue() waits
-        # for it and starts the upload
-        self._rfut = _read_master().submit(f.read_data_into, nbytes,
-                                           host.numpy())
         self._q = dict(dev=dev, buf=buf, slot=slot, host=host, aux=aux,
                        nraw=nraw, naux=naux, nsc=nsc, nbytes=nbytes,
                        elem=elem, pol_mode=pol_mode, rm_baseline=rm_baseline)
         self._qlock = threading.Lock()
         self._queued = False
+        # the DATA read runs on the reader threads from here, and the upload
+        # and device work are queued as soon as it completes (on the read
+        # thread, in read order); queue() / finish() wait for that
+        self._rfut = _read_master().submit(self._read_then_queue, nbytes,
+                                           host.numpy())
         self._m = self._meta()
 
+    def _read_then_queue(self, nbytes, dst):
+        try:
+            self.f.read_data_into(nbytes, dst)
+        except BaseException:
+            self._ticket.set(None)
+            raise
+        self._queue_now()
+
     def queue(self):
-        """Wait for the DATA read, then queue the upload, the device unpack,
-        baseline, statistics and noise and the statistics download on this
-        thread's copy stream (once; later calls return at once)."""
+        """Return once the DATA read is done and the upload, the device
+        unpack, baseline, statistics and noise and the statistics download
+        are queued (by the read thread, on its copy stream)."""
+        self._rfut.result()
+
+    def _queue_now(self):
         import torch
         from . import engine
         from .timeline import span
@@ -724,7 +756,11 @@ class _Pending(object):
             if self._queued:
                 return
             self._queued = True
-            self._queue(torch, engine, span)
+            try:
+                self._queue(torch, engine, span)
+            finally:
+                if not self._ticket._done.is_set():
+                    self._ticket.set(None)
 
     def _queue(self, torch, engine, span):
         q, f = self._q, self.f
@@ -736,8 +772,6 @@ class _Pending(object):
         dedisperse, tscrunch = self.dedisperse, self.tscrunch
         if not hasattr(_TLS, "streams"):
             _TLS.streams = {}
-        with span("load.read"):
-            self._rfut.result()
         with torch.cuda.device(dev):
             st = _TLS.streams.get(dev.index)
             if st is None:
@@ -758,7 +792,7 @@ class _Pending(object):
                                                   non_blocking=True)
                     up = torch.cuda.Event()
                     up.record(st)
-                    slot[1] = up                    # the buffer is free after it
+                    self._ticket.set(up)            # the buffer is free after it
                     # with dedisperse the baseline is removed after the
                     # rotation (pplib.py:2786-2791)
                     out = engine.unpack_psrfits(
@@ -849,7 +883,8 @@ class _Pending(object):
 
     def finish(self):
         from .timeline import span
-        self.queue()
+        with span("load.read"):
+            self._rfut.result()             # read and queued (or raised)
         with span("load.wait"):
             self.ev.synchronize()
         self._keep = None

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-4 evidence run: the GPU parity suite, then every bench line with its
+# CPU baseline and parity sample (C2 headline, single-call latency, C3 and C5
+# with >= 5 timed steps, C4 ppalign, GetTOAs from 16-bit PSRFITS and from
+# float32 archives, phase+DM at the mixed-radix nbin 1000 and 1536).
+# usage: tools/evid_r4.sh TAG [tests|notests]
+tag=${1:-a}
+mode=${2:-tests}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+st=gpurun_out/evid_${tag}_status.txt
+if [ "$mode" = tests ]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests_$tag.log 2>&1
+  rc=$?; echo "tests rc=$rc $(tail -1 gpurun_out/gpu_tests_$tag.log)" >> $st
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+fi
+run() {
+  name=$1; lim=$2; shift 2
+  timeout -k 10 $lim python bench.py "$@" > gpurun_out/bench_${name}_$tag.log 2>&1
+  rc=$?
+  echo "$name rc=$rc $(python tools/show.py gpurun_out/bench_${name}_$tag.log | head -1)" >> $st
+  [ $rc -eq 0 ] || exit $rc
+}
+run c2 300
+run single 200 --fit single --cpu-sample 1
+run c3 300 --fit full --nsub 10000 --steps 5 --warmup 1
+run c5 300 --fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 5 --warmup 1
+run c4 300 --fit align --nsub 1000 --nchan 256 --nbin 1024 --steps 5 --warmup 2
+run gettoaspsrfits 300 --fit gettoas --psrfits --steps 3 --warmup 1
+run gettoas 300 --fit gettoas --steps 3 --warmup 1
+run c2nb1000 300 --nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
+run c2nb1536 300 --nbin 1536 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
+echo end >> $st

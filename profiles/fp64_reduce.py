@@ -28,7 +28,7 @@ import os
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
            "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
            "tr_mom": ("k_tr_mom", ""), "postfit": ("k_postfit", ""),
-           "moments": ("k_moments", "")}
+           "moments": ("k_moments", ""), "accum": ("k_align", "")}
 
 
 def main():

@@ -29,7 +29,7 @@ import os
 
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
            "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
-           "moments": ("k_moments", ""), "noise": ("k_noise_w<", "")}
+           "moments": ("k_moments", ""), "accum": ("k_align", ""), "noise": ("k_noise_w<", "")}
 
 
 def load(d):

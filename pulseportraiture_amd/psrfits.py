@@ -735,8 +735,10 @@ class _Pending(object):
         self._m = self._meta()
 
     def _read_then_queue(self, nbytes, dst):
+        from .timeline import span
         try:
-            self.f.read_data_into(nbytes, dst)
+            with span("load.data"):
+                self.f.read_data_into(nbytes, dst)
         except BaseException:
             self._ticket.set(None)
             raise

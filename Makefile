@@ -3,12 +3,12 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := pulseportraiture_amd/csrc
 OUT := pulseportraiture_amd/lib/libppfit.so
-SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_xspec.hip $(CSRC)/ppf_solve.hip $(CSRC)/ppf_psrfits.hip $(CSRC)/ppf_api.cpp
+SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_xspec.hip $(CSRC)/ppf_solve.hip $(CSRC)/ppf_psrfits.hip $(CSRC)/ppf_api.cpp $(CSRC)/ppf_io.cpp
 HDRS := $(CSRC)/ppf_device.hpp $(CSRC)/ppf_state.hpp $(CSRC)/ppf_wfft.hpp $(CSRC)/ppf_internal.hpp include/ppfit.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed \
             -ffp-contract=fast -munsafe-fp-atomics
 
-OBJS := $(CSRC)/ppf_kernels.o $(CSRC)/ppf_xspec.o $(CSRC)/ppf_solve.o $(CSRC)/ppf_psrfits.o $(CSRC)/ppf_api.o
+OBJS := $(CSRC)/ppf_kernels.o $(CSRC)/ppf_xspec.o $(CSRC)/ppf_solve.o $(CSRC)/ppf_psrfits.o $(CSRC)/ppf_api.o $(CSRC)/ppf_io.o
 
 all: $(OUT)
 
@@ -27,9 +27,13 @@ $(CSRC)/ppf_psrfits.o: $(CSRC)/ppf_psrfits.hip $(HDRS)
 $(CSRC)/ppf_api.o: $(CSRC)/ppf_api.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+# host-only: the native DATA reader (no device code)
+$(CSRC)/ppf_io.o: $(CSRC)/ppf_io.cpp include/ppfit.h
+	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -pthread -c $< -o $@
+
 $(OUT): $(OBJS)
 	@mkdir -p $(dir $(OUT))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -o $@ $(OBJS)
 
 clean:
 	rm -f $(OBJS) $(OUT)

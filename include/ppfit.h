@@ -43,7 +43,8 @@ enum ppf_error {
     PPF_EINVAL = -1,   /* bad argument / shape */
     PPF_EHIP = -2,     /* HIP runtime error */
     PPF_ENOMEM = -3,   /* workspace too small */
-    PPF_EUNSUP = -4    /* unsupported configuration (e.g. nbin) */
+    PPF_EUNSUP = -4,   /* unsupported configuration (e.g. nbin) */
+    PPF_EIO = -5       /* file read failed or came up short */
 };
 
 enum ppf_dtype { PPF_F32 = 0, PPF_F64 = 1 };
@@ -345,6 +346,27 @@ int ppf_unpack_psrfits_batch(ppf_ctx *ctx, int32_t nsub, int32_t npol, int32_t n
                              int32_t rm_baseline, float *out, double *stats, double *total,
                              int32_t *wstart, void *workspace, size_t workspace_bytes,
                              void *stream);
+
+/* nbytes from page-locked host memory src (a pinned buffer: hipHostMalloc /
+ * torch pin_memory) to device memory dst, read by a kernel over PCIe on
+ * stream instead of by a copy engine.  GetTOAs stages each archive's fit
+ * inputs (engine._stage_host: the per-sub-int arrays of the reference's
+ * fit_portrait_full calls, pptoas.py:530-533) this way, so they never wait
+ * behind the archive uploads the copy engines are busy with.  Both pointers
+ * 16-byte aligned; src must stay untouched until the stream has passed the
+ * copy. */
+int ppf_copy_from_pinned(ppf_ctx *ctx, void *dst, const void *src, int64_t nbytes, void *stream);
+
+/* Positioned reads of the PSRFITS DATA column into host memory (the file
+ * side of the fast path above; psrfits.PSRFITS.read_data_into): for each of
+ * nrows rows, nbytes bytes at file offset offset + r * row_stride go to
+ * dst + r * dst_stride.  The rows are cut into pieces of at most 4 MiB that
+ * nthreads threads (1..64) take in turn with pread(2); the call returns when
+ * every piece is in (dst is typically a page-locked upload buffer).  No
+ * device and no context: PPF_OK, PPF_EINVAL (bad arguments) or PPF_EIO (a
+ * read failed or hit end of file). */
+int ppf_read_rows(int32_t fd, int64_t offset, int64_t row_stride, int64_t nbytes,
+                  int64_t nrows, void *dst, int64_t dst_stride, int32_t nthreads);
 
 /* Gaussian-component model portraits: pplib.gen_gaussian_portrait
  * (pplib.py:886-963, join_ichans = []) as called by pplib.read_model

@@ -120,6 +120,11 @@ SIGNATURES = {
                                                 _vp, _vp, _vp, _i32, _i32,
                                                 _vp, _vp, _vp, _vp, _vp,
                                                 ctypes.c_size_t, _vp]),
+    "ppf_copy_from_pinned": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64,
+                                            _vp]),
+    "ppf_read_rows": (ctypes.c_int, [_i32, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_int64, _vp,
+                                     ctypes.c_int64, _i32]),
     "ppf_poly_real_roots_host": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_tr_subproblem_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                               ctypes.c_double, _vp]),

@@ -771,6 +771,24 @@ int ppf_unpack_psrfits_batch(ppf_ctx *ctx, int32_t nsub, int32_t npol, int32_t n
     return PPF_OK;
 }
 
+int ppf_copy_from_pinned(ppf_ctx *ctx, void *dst, const void *src, int64_t nbytes, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nbytes < 0 || (nbytes > 0 && (!dst || !src)))
+        return fail(ctx, PPF_EINVAL, "bad copy arguments");
+    if (((uintptr_t)dst | (uintptr_t)src) % 16)
+        return fail(ctx, PPF_EINVAL, "copy buffers must be 16-byte aligned");
+    if (nbytes == 0) return PPF_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    void *src_dev = nullptr;
+    if ((e = hipHostGetDevicePointer(&src_dev, const_cast<void *>(src), 0)) != hipSuccess || !src_dev)
+        return hip_fail(ctx, e != hipSuccess ? e : hipErrorInvalidValue,
+                        "hipHostGetDevicePointer (src must be page-locked host memory)");
+    if ((e = ppf::launch_copy_host(src_dev, dst, nbytes, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(ctx, e, "k_copy_host");
+    return PPF_OK;
+}
+
 int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_dtype,
                           const void *data, const double *model, const int32_t *model_index,
                           const double *noise, int32_t Ns, double lo, double hi, double *out,

@@ -250,6 +250,7 @@ struct UnpackArgs {
     double *stats;               // [nsub][nchan][3]: off mean, off sigma, S/N
 };
 hipError_t launch_unpack(const UnpackArgs &a, hipStream_t st);
+hipError_t launch_copy_host(const void *src_dev, void *dst, int64_t nbytes, hipStream_t st);
 size_t unpack_partials(int nsub, int nchan, int nbin);
 
 // pplib.gen_gaussian_portrait (pplib.py:886-963) per (portrait, channel) row

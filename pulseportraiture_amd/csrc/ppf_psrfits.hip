@@ -158,6 +158,40 @@ hipError_t launch_unpack(const UnpackArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Device-side copy out of page-locked host memory (zero-copy reads over
+// PCIe by the CUs): the fit inputs' staging buffer reaches HBM without a
+// copy-engine transfer, so it never queues behind an archive upload.
+__global__ __launch_bounds__(256) void k_copy_host(const uint4 *__restrict__ src,
+                                                   uint4 *__restrict__ dst, int64_t n16) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(64) void k_copy_host_tail(const uint8_t *__restrict__ src,
+                                                       uint8_t *__restrict__ dst, int64_t n) {
+    const int64_t i = threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+hipError_t launch_copy_host(const void *src_dev, void *dst, int64_t nbytes, hipStream_t st) {
+    const int64_t n16 = nbytes / 16, tail = nbytes - n16 * 16;
+    if (n16 > 0) {
+        const int64_t want = (n16 + 255) / 256;
+        const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+        hipLaunchKernelGGL(k_copy_host, dim3(grid), dim3(256), 0, st, (const uint4 *)src_dev,
+                           (uint4 *)dst, n16);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (tail > 0) {
+        hipLaunchKernelGGL(k_copy_host_tail, dim3(1), dim3(64), 0, st,
+                           (const uint8_t *)src_dev + n16 * 16, (uint8_t *)dst + n16 * 16, tail);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
 size_t unpack_partials(int nsub, int nchan, int nbin) {
     return (size_t)nsub * ((nchan + kUnpackChans - 1) / kUnpackChans) * nbin;
 }

@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .timeline import span
 
 DEVICE_TYPE = "cuda"   # torch's name for HIP devices on ROCm
 
@@ -69,6 +70,9 @@ def _pinned(tag, nbytes):
 
 
 _STAGE = threading.local()
+# fit inputs staged by ppf_copy_from_pinned's kernel (1) or a copy-engine
+# transfer (0); env PPF_STAGE_KERNEL
+_STAGE_KERNEL = os.environ.get("PPF_STAGE_KERNEL", "1") != "0"
 _NPD = {torch.float64: np.float64, torch.float32: np.float32,
         torch.int32: np.int32, torch.uint8: np.uint8}
 
@@ -99,7 +103,15 @@ def _stage_host(items, dev):
     for a, off in zip(arrs, offs):
         hb[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
     d = torch.empty(total, dtype=torch.uint8, device=dev)
-    d.copy_(slot[0][:total], non_blocking=True)
+    if _STAGE_KERNEL:
+        # read by a kernel over PCIe: no copy-engine transfer, so it never
+        # queues behind an archive upload (ppf_copy_from_pinned)
+        ctx = _lib.context(dev.index)
+        _lib.check(_lib.load().ppf_copy_from_pinned(
+            ctx, _p(d), ctypes.c_void_p(slot[0].data_ptr()), total,
+            _stream(dev)), ctx)
+    else:
+        d.copy_(slot[0][:total], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     slot[1] = ev
@@ -243,8 +255,9 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     host = [(k, x, dt) for k, x, dt in specs
             if x is not None and not isinstance(x, torch.Tensor)]
     if host:
-        up = dict(zip([k for k, _, _ in host], _stage_host(
-            [(x, dt) for _, x, dt in host], dev)))
+        with span("fit.stage"):
+            up = dict(zip([k for k, _, _ in host], _stage_host(
+                [(x, dt) for _, x, dt in host], dev)))
         freqs, P, init = up.get("freqs", freqs), up.get("P", P), \
             up.get("init", init)
         fit_flags, nu_fits = up.get("flags", fit_flags), \
@@ -417,7 +430,9 @@ def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace):
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     d.workspace, d.workspace_bytes = _p(workspace), workspace.numel()
     ctx = _lib.context(dev.index)
-    _lib.check(lib.ppf_fit_batch(ctx, ctypes.byref(d), _stream(dev)), ctx)
+    with span("fit.lib"):
+        rc = lib.ppf_fit_batch(ctx, ctypes.byref(d), _stream(dev))
+    _lib.check(rc, ctx)
     # keep inputs alive until the stream has consumed them
     keep = (cfg["model"],) + tuple(v for v in per_sub.values()
                                    if v is not None)

@@ -13,6 +13,7 @@ Reference: /root/reference/pptoas.py (file:line cited per block).
 import contextlib
 import gc
 import os
+import sys
 import threading
 import time
 import warnings
@@ -38,6 +39,7 @@ rm_baseline = bool(_pplib.F0_fact)  # pptoas.py:36-39
 # sub-ints share channels, frequencies and fit flags (bit-identical to the
 # per-sub-int loops, which remain the general path; False forces those)
 FAST_HOST = True
+_SWITCH_MS = float(os.environ.get("PPF_SWITCH_INTERVAL_MS", "0") or 0)
 
 
 def _is_fits(filename):
@@ -528,6 +530,11 @@ class GetTOAs(object):
         # millisecond pause in whichever stage it lands
         gc_on = gc.isenabled()
         gc.disable()
+        # the interpreter's thread switch interval for the loop (env
+        # PPF_SWITCH_INTERVAL_MS; unset: left as it is)
+        sw0 = sys.getswitchinterval()
+        if _SWITCH_MS:
+            sys.setswitchinterval(_SWITCH_MS * 1e-3)
         try:
             for pos, iarch in enumerate(mine):
                 for ahead in range(ahead_n + 1):
@@ -558,6 +565,7 @@ class GetTOAs(object):
         finally:
             if gc_on:
                 gc.enable()
+            sys.setswitchinterval(sw0)
             pool.shutdown(wait=True)
             for fu in loads.values():
                 fu.cancel()

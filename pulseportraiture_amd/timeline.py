@@ -4,8 +4,8 @@
 recorded (name, thread, t0, t1, cpu) tuples (perf_counter seconds; cpu = the
 thread's CPU seconds inside the span, time.thread_time) and clears them.
 Wall time minus CPU time is waiting: for the device, for I/O, or for the
-GIL held by another thread.  tools/gettoas_timeline.py turns them into the per-stage breakdown
-committed under profiles/."""
+GIL held by another thread.  `bench.py --fit gettoas --timeline FILE`
+writes them with the per-stage breakdown (profiles/r04/gettoas_*timeline*)."""
 import os
 import threading
 import time

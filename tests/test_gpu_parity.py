@@ -1060,3 +1060,48 @@ def test_stager_pinned_and_pageable_sources_upload_the_same_rows():
             np.testing.assert_array_equal(t.cpu().numpy(), a)
     finally:
         st.close()
+
+
+@pytest.mark.gpu
+def test_copy_from_pinned_and_stage_host():
+    """ppf_copy_from_pinned (the fit inputs' kernel copy out of page-locked
+    memory, 16-B body + byte tail) moves every byte; engine._stage_host
+    returns the same arrays through it as through a copy-engine transfer;
+    a pageable source is refused."""
+    import ctypes
+    import torch
+    from pulseportraiture_amd import _lib, engine
+    dev = engine.device()
+    lib, ctx = _lib.load(), _lib.context(dev.index)
+    rng = np.random.default_rng(9)
+    for n in (16, 48, 1000, 4096 + 7, (3 << 20) + 13):
+        h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        h.numpy()[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        d = torch.full((n + 64,), 0x5A, dtype=torch.uint8, device=dev)
+        s = torch.cuda.current_stream(dev)
+        assert lib.ppf_copy_from_pinned(
+            ctx, ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(h.data_ptr()),
+            n, ctypes.c_void_p(s.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        np.testing.assert_array_equal(got[:n], h.numpy())
+        assert (got[n:] == 0x5A).all()
+    pageable = np.zeros(64, dtype=np.uint8)
+    d = torch.empty(64, dtype=torch.uint8, device=dev)
+    assert lib.ppf_copy_from_pinned(
+        ctx, ctypes.c_void_p(d.data_ptr()), pageable.ctypes.data, 64,
+        ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)) != 0
+    items = [(rng.standard_normal((7, 33)), torch.float64),
+             (rng.integers(0, 2, (7, 33)).astype(np.uint8), torch.uint8),
+             (np.arange(7, dtype=np.int32), torch.int32),
+             (rng.standard_normal(5).astype(np.float32), torch.float32)]
+    outs = {}
+    for kern in (True, False):
+        engine._STAGE_KERNEL = kern
+        try:
+            outs[kern] = [t.cpu().numpy() for t in engine._stage_host(items, dev)]
+        finally:
+            engine._STAGE_KERNEL = True
+    for (a, _), k, c in zip(items, outs[True], outs[False]):
+        np.testing.assert_array_equal(k, a)
+        np.testing.assert_array_equal(c, a)

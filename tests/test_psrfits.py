@@ -60,6 +60,45 @@ def test_fits_round_trip(tmp_path):
     f.close()
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_read_data_into_native_reader(tmp_path, threads, monkeypatch):
+    """ppf_read_rows (native positioned reads, no device) returns the DATA
+    bytes of every row, at any thread count, into a strided buffer, and
+    fails loudly on a truncated file or a bad destination."""
+    fn, q, scl, offs, fr, wts = _archive(tmp_path, nsub=5, npol=2, nchan=16,
+                                         nbin=128)
+    monkeypatch.setattr(PF, "_READ_THREADS", threads)
+    f = PF.PSRFITS(fn)
+    raw, dt = f.data_bytes()
+    nbytes = 1 * 16 * 128 * 2                 # pol 0 only: the first block
+    dst = np.full((5, nbytes + 64), 0xAB, dtype=np.uint8)
+    f.read_data_into(nbytes, dst)
+    np.testing.assert_array_equal(dst[:, :nbytes], np.asarray(raw)[:, :nbytes])
+    assert (dst[:, nbytes:] == 0xAB).all()
+    full = raw.shape[1]
+    dst2 = np.zeros((5, full), dtype=np.uint8)
+    f.read_data_into(full, dst2)
+    np.testing.assert_array_equal(dst2, np.asarray(raw))
+    with pytest.raises(ValueError):
+        f.read_data_into(nbytes, np.zeros((4, nbytes), dtype=np.uint8))
+    f.close()
+    # a file cut inside the last row's DATA: the read comes up short
+    f = PF.PSRFITS(fn)
+    t = f.subint
+    cut = t._off + 4 * t.rowbytes + t.columns["DATA"][0] + 100
+    f.close()
+    with open(fn, "r+b") as fh:
+        fh.truncate(cut)
+    with open(fn, "rb") as fh:
+        from pulseportraiture_amd import _lib
+        rc = _lib.load().ppf_read_rows(
+            fh.fileno(), t._off + t.columns["DATA"][0], t.rowbytes, nbytes,
+            5, dst.ctypes.data, dst.strides[0], threads)
+        assert rc == -5                                   # PPF_EIO
+        assert _lib.load().ppf_read_rows(fh.fileno(), 0, 10, 20, 1,
+                                         dst.ctypes.data, 64, 1) == -1
+
+
 def test_unpack_host_restatement(tmp_path):
     fn, q, scl, offs, fr, wts = _archive(tmp_path)
     f = PF.PSRFITS(fn)

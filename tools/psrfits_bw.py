@@ -39,7 +39,6 @@ def main():
 
     for nt in (1, 2, 4, 8, 12, 16):
         psrfits._READ_THREADS = nt
-        psrfits._POOL.clear()
         ts = []
         for r in range(reps):
             t0 = time.perf_counter()
@@ -50,7 +49,6 @@ def main():
             nt, 1e3 * ts[len(ts) // 2], gbs(ts[len(ts) // 2]), gbs(ts[0])),
             flush=True)
     psrfits._READ_THREADS = 8
-    psrfits._POOL.clear()
     st = torch.cuda.Stream(dev)
     for chunk in (0, 16, 4):
         ts = []
@@ -75,7 +73,6 @@ def main():
     # both at once: upload slot 0 while reading file 1 into slot 1
     for nt in (4, 8, 16):
         psrfits._READ_THREADS = nt
-        psrfits._POOL.clear()
         tr, tu, tw = [], [], []
         for r in range(reps):
             torch.cuda.synchronize()

@@ -781,9 +781,11 @@ int ppf_copy_from_pinned(ppf_ctx *ctx, void *dst, const void *src, int64_t nbyte
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     void *src_dev = nullptr;
-    if ((e = hipHostGetDevicePointer(&src_dev, const_cast<void *>(src), 0)) != hipSuccess || !src_dev)
+    if ((e = hipHostGetDevicePointer(&src_dev, const_cast<void *>(src), 0)) != hipSuccess || !src_dev) {
+        (void)hipGetLastError();   // not sticky: the next launch must not see it
         return hip_fail(ctx, e != hipSuccess ? e : hipErrorInvalidValue,
                         "hipHostGetDevicePointer (src must be page-locked host memory)");
+    }
     if ((e = ppf::launch_copy_host(src_dev, dst, nbytes, (hipStream_t)stream)) != hipSuccess)
         return hip_fail(ctx, e, "k_copy_host");
     return PPF_OK;

@@ -328,15 +328,18 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
                solver=_solver(solver),
                mom_x=MOM_X if mom_x is None else bool(mom_x))
     lib = _lib.load()
-    need = _workspace_bytes(lib, per_sub, 0, nsub, n_x, cfg)
+    d0 = _desc(per_sub, 0, nsub, n_x, cfg)
+    need = _desc_workspace_bytes(lib, d0)
     if max_workspace is None and (need <= (64 << 20) or nsub == 1):
         # small batches (the single-call APIs) skip the free-memory query
-        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
+        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace,
+                          d0, need)
     if max_workspace is None:
         free, _ = torch.cuda.mem_get_info(dev)
         max_workspace = free // 2
     if need <= max_workspace:
-        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace)
+        return _fit_slice(lib, dev, per_sub, 0, nsub, n_x, cfg, workspace,
+                          d0, need)
     # chunks of equal size whose workspace fits the budget
     per = max(1, int(nsub * max_workspace // max(need, 1)))
     while per > 1 and _workspace_bytes(lib, per_sub, 0, per, per, cfg) > \
@@ -401,7 +404,10 @@ def _desc(per_sub, c0, c1, n_x, cfg):
 
 
 def _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg):
-    d = _desc(per_sub, c0, c1, n_x, cfg)
+    return _desc_workspace_bytes(lib, _desc(per_sub, c0, c1, n_x, cfg))
+
+
+def _desc_workspace_bytes(lib, d):
     nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
@@ -411,20 +417,32 @@ def _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg):
     return nbytes
 
 
-def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace):
-    f64 = torch.float64
+def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace, d=None,
+               nbytes=None):
+    """ppf_fit_batch over sub-ints [c0, c1) (d / nbytes: their descriptor
+    and workspace size when the caller has them).  The outputs are views of
+    ONE zeroed float64 buffer ("_flat": results | scales | scale_errs |
+    channel_snrs | covariance), which a caller may download in one copy."""
     nsub = c1 - c0
     nchan = per_sub["data"].shape[1]
-    results = torch.zeros((nsub, _lib.RESULT_DOUBLES), dtype=f64, device=dev)
-    scales = torch.zeros((nsub, nchan), dtype=f64, device=dev)
-    scale_errs = torch.zeros_like(scales)
-    channel_snrs = torch.zeros_like(scales)
-    cov = torch.zeros((nsub, 5, 5), dtype=f64, device=dev)
-    d = _desc(per_sub, c0, c1, n_x, cfg)
+    R = _lib.RESULT_DOUBLES
+    sizes = (nsub * R, nsub * nchan, nsub * nchan, nsub * nchan, nsub * 25)
+    flat = torch.zeros(sum(sizes), dtype=torch.float64, device=dev)
+    views, o = [], 0
+    for n in sizes:
+        views.append(flat[o:o + n])
+        o += n
+    results = views[0].view(nsub, R)
+    scales, scale_errs, channel_snrs = (v.view(nsub, nchan)
+                                        for v in views[1:4])
+    cov = views[4].view(nsub, 5, 5)
+    if d is None:
+        d = _desc(per_sub, c0, c1, n_x, cfg)
+    if nbytes is None:
+        nbytes = _desc_workspace_bytes(lib, d)
     d.results, d.scales, d.scale_errs = _p(results), _p(scales), \
         _p(scale_errs)
     d.channel_snrs, d.covariance = _p(channel_snrs), _p(cov)
-    nbytes = _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg)
     if workspace is None or workspace.numel() < nbytes or \
             workspace.device != dev:
         workspace = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -438,7 +456,7 @@ def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace):
                                    if v is not None)
     return dict(results=results, scales=scales, scale_errs=scale_errs,
                 channel_snrs=channel_snrs, covariance=cov,
-                workspace=workspace, _keep=keep)
+                workspace=workspace, _keep=keep, _flat=flat)
 
 
 def rotate_rows(rows, phases, dev=None):

@@ -259,6 +259,19 @@ def _pack(res):
                      dim=1)
 
 
+def _unflat(res, host):
+    """engine.fit_batch's outputs as host arrays, cut from the download of
+    their one device buffer (res["_flat"])."""
+    out, o = {}, 0
+    for k in ("results", "scales", "scale_errs", "channel_snrs",
+              "covariance"):
+        shape = tuple(res[k].shape)
+        n = int(np.prod(shape))
+        out[k] = host[o:o + n].reshape(shape)
+        o += n
+    return out
+
+
 def _unpack(t, nchan):
     R = _lib.RESULT_DOUBLES
     return dict(results=t[:, :R], scales=t[:, R:R + nchan],
@@ -495,10 +508,12 @@ class GetTOAs(object):
         # archives: depth 1 6.1-6.2k, 2 5.1-5.6k, 3 4.7-5.3k TOAs/s in one
         # call; the file reads and pinned copies share the host's memory
         # bandwidth).  PPF_LOAD_AHEAD archives are queued ahead on those
-        # threads (a PSRFITS load returns once its upload and unpack are
-        # queued, so the one loader thread keeps reading)
+        # threads (a PSRFITS load parses the file and hands the read to the
+        # reader threads, so the one loader thread keeps going): 3 ahead
+        # with psrfits' 4 pinned slots 17.5-18.1k vs 2 ahead / 3 slots
+        # 15.6-17.1k TOAs/s (A/B in one call, tools/g21.sh)
         depth = max(1, int(os.environ.get("PPF_LOAD_DEPTH", "1")))
-        ahead_n = max(depth, int(os.environ.get("PPF_LOAD_AHEAD", "2")))
+        ahead_n = max(depth, int(os.environ.get("PPF_LOAD_AHEAD", "3")))
         loader = ThreadPoolExecutor(max_workers=depth)
         mine = list(mine)
         loads = {}
@@ -937,10 +952,15 @@ class GetTOAs(object):
             if job["world"] > 1:
                 # a failed rank must not leave the others in the all-gather
                 _dist.raise_if_any_failed(err, dev if nccl else None)
+                table = _pack(table) if isinstance(table, dict) else table
                 table = _dist.allgather_rows(table if nccl else table.cpu(),
                                              nok, job["world"])
             with span("fit.d2h"):
-                r = _unpack(table.cpu().numpy(), nchan)
+                if isinstance(table, dict):
+                    # one rank: the outputs' single buffer in one copy
+                    r = _unflat(table, table["_flat"].cpu().numpy())
+                else:
+                    r = _unpack(table.cpu().numpy(), nchan)
             _sp.__exit__(None, None, None)
         job["staged"].release()
         r["batch_duration"] = time.time() - t_fit
@@ -973,7 +993,7 @@ class GetTOAs(object):
         if "max" not in ws and torch.cuda.is_available():
             ws["max"] = torch.cuda.mem_get_info(dev)[0] // 2
         _sp.__exit__(None, None, None)
-        return _pack(res)
+        return res if "_flat" in res else _pack(res)
 
     def _book_uniform(self, job, r, ctx, fit_duration, out):
         """_book_archive's per-sub-int loop for an archive fitted with one

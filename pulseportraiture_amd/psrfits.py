@@ -609,9 +609,9 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
 # only once the upload that read it has completed (its event)
 _PINNED = {}
 _PINNED_LOCK = threading.Lock()
-# page-locked DATA buffers per device (env PPF_PINNED_SLOTS, default 3): a
+# page-locked DATA buffers per device (env PPF_PINNED_SLOTS, default 4): a
 # read may run this many archives minus one ahead of the oldest upload
-_PIN_SLOTS = max(2, int(os.environ.get("PPF_PINNED_SLOTS", "3")))
+_PIN_SLOTS = max(2, int(os.environ.get("PPF_PINNED_SLOTS", "4")))
 
 
 class _UploadTicket(object):

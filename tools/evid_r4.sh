@@ -26,7 +26,7 @@ run single 200 --fit single --cpu-sample 1
 run c3 300 --fit full --nsub 10000 --steps 5 --warmup 1
 run c5 300 --fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 5 --warmup 1
 run c4 300 --fit align --nsub 1000 --nchan 256 --nbin 1024 --steps 5 --warmup 2
-run gettoaspsrfits 300 --fit gettoas --psrfits --steps 3 --warmup 1
+run gettoaspsrfits 300 --fit gettoas --psrfits --steps 4 --warmup 1 --timeline gpurun_out/gettoas_psrfits_timeline_$tag.json
 run gettoas 300 --fit gettoas --steps 3 --warmup 1
 run c2nb1000 300 --nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
 run c2nb1536 300 --nbin 1536 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8

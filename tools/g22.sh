@@ -1,7 +1,7 @@
 # GetTOAs loader: kernel-staged fit inputs (PPF_STAGE_KERNEL 1 / 0), loads
 # ahead 3 with 4 pinned slots (candidate defaults), A/B in ONE call
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_psrfits.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "psrfits or copy_from_pinned or stager or get_toas or gettoas" > gpurun_out/g22_pytest.log 2>&1 || exit 2
+timeout -k 10 300 python -u -m pytest tests/test_psrfits.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "psrfits or copy_from_pinned or stager or get_toas or gettoas or fit_batch or full" > gpurun_out/g22_pytest.log 2>&1 || exit 2
 for rep in 1 2 3; do
 for v in k1 k0; do
   case $v in

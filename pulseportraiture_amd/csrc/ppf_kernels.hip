@@ -684,8 +684,21 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double2 *Mm = a.Mft + (int64_t)mi * a.nchan * nharm;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const int lane = tid & 63;
+    // the mean model has no harmonic above the largest channel cutoff
+    // (k_model_cut): the FFTFIT sums stop there
+    double kmx[1] = {1.0};
+    if (a.KC)
+        for (int n = tid; n < a.nchan; n += kBlock)
+            kmx[0] = fmax(kmx[0], (double)a.KC[(int64_t)mi * a.nchan + n]);
+    else
+        kmx[0] = (double)nharm;
+    block_max<1>(kmx, red);
+    // fused: the noise comes from the channels (below), so only the
+    // harmonics the FFTFIT sums read (k < kmx) are formed; otherwise every
+    // harmonic, for the power above kc
+    const int kloop = fused ? (int)kmx[0] : nharm;
     // uniform trip count: the mask ballots below need every lane active
-    for (int k0 = 0; k0 <= N; k0 += kBlock) {
+    for (int k0 = 0; k0 < kloop; k0 += kBlock) {
         const int k = k0 + tid;
         const bool kv = k <= N;
         // mean model profile of the usable channels: the batch sum minus the
@@ -703,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
                 }
             }
         }
-        if (!kv) continue;
+        if (!kv || k >= kloop) continue;
         double2 R = cscale(fused ? fused_bin(k) : rfft_bin(z, N, a.T2, k), 1.0 / wsum);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
@@ -719,15 +732,6 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
     // fused: the profile's expected noise, sqrt(sum w^2 errs_FT^2) / W
     const double err = fused ? sqrt(sh[2]) / wsum : sig * sqrt((double)a.nbin / 2.0);
-    // the mean model has no harmonic above the largest channel cutoff
-    // (k_model_cut): the FFTFIT sums stop there
-    double kmx[1] = {1.0};
-    if (a.KC)
-        for (int n = tid; n < a.nchan; n += kBlock)
-            kmx[0] = fmax(kmx[0], (double)a.KC[(int64_t)mi * a.nchan + n]);
-    else
-        kmx[0] = (double)nharm;
-    block_max<1>(kmx, red);
     const double phase = brute_fmin(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
                                     nullptr);
     // nu_mean of the usable channels (block reduction: 16384-channel

@@ -991,7 +991,16 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // MFMA f64 16x16x4: A = Y (16 channels x 4 harmonics; one wave = 16
 // channels), B = u^m (4 harmonics x 16 moments), two B tiles (m < 16, m >=
 // 16) and separate real / imaginary A.  The harmonic sum is the MFMA K loop.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_moments(SolveArgs a) {
+#ifndef PPF_MOM_WPE
+#define PPF_MOM_WPE 3
+#endif
+// (measured, C2 per 10k sub-ints, same call: KU = 8 6.12 vs 5.76 ms; the
+// loop unrolled by two over two buffers, so that no batch waits for loads it
+// has just issued, 5.77 at KU = 4 and 5.91 at KU = 2: no latency to hide)
+#ifndef PPF_MOM_KU
+#define PPF_MOM_KU 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_MOM_WPE))) void k_moments(SolveArgs a) {
     const int nblk = (a.nchan + kMomChans - 1) / kMomChans;
     const int s = blockIdx.x / nblk, blk = blockIdx.x % nblk;
     const TRState &S = a.state[s];
@@ -1034,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     double2 E = cmk(1.0, 0.0);
     // batches of 4 K-steps (16 harmonics), software-pipelined: the next
     // batch's loads are in flight while this one's MFMAs run
-    constexpr int KU = 4;
+    constexpr int KU = PPF_MOM_KU;
     double2 xa[KU], xb[KU];
     auto ld = [&](double2 (&xv)[KU], int kb) {
 #pragma unroll

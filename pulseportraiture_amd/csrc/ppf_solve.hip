@@ -524,7 +524,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
         };
         ldg(kb0, xa, pa);
         // (no early exit: a trailing group may sum zeros, which keeps one
-        // straight-line body and its load/wait schedule)
+        // straight-line body and its load/wait schedule.  Whole iterations
+        // below kb1 without the end-of-row selects, 8.6 % fewer VALU
+        // instructions per harmonic, measured no faster: C3 1.315-1.375 vs
+        // 1.353-1.399 ms, C5 2.47-2.48 vs 2.45-2.49 ms per launch in one call)
         for (int kb = kb0; kb < kb1; kb += 2 * KB) {
             ldg(kb + KB, xb, pb);
             sum_group(kb, xa, pa);

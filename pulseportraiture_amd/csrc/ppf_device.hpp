@@ -363,7 +363,7 @@ __device__ void mr_stage(double2 *buf, int N, int L, const double2 *__restrict__
 
 // Any supported N (fft_len_supported); every thread of the block calls it.
 __device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, bool inverse);
-__device__ __noinline__ void lds_fft_mixed(double2 *buf, int N, const double2 *__restrict__ T,
+__device__ __forceinline__ void lds_fft_mixed(double2 *buf, int N, const double2 *__restrict__ T,
                                            bool inverse) {
     int r[32];
     const int ns = fft_radices(N, r);
@@ -379,10 +379,18 @@ __device__ __noinline__ void lds_fft_mixed(double2 *buf, int N, const double2 *_
         L *= r[s];
     }
 }
+// MX = false: N is a power of two (the caller's launcher checked) and the
+// kernel carries none of the mixed-radix code, whose registers would
+// otherwise set its VGPR budget: with the stages inlined a block-FFT kernel
+// needs ~190 VGPRs (two waves per SIMD), with them behind a call 248 VGPRs +
+// 32 AGPRs and scratch (one wave), against ~100 without (round 4: k_guess at
+// C4 0.60 vs 0.30 ms per launch).  Launchers instantiate MX = true only for
+// nbin / 2 not a power of two.
+template <bool MX = true>
 __device__ __forceinline__ void lds_fft_n(double2 *buf, int N, const double2 *__restrict__ T,
                                           bool inverse) {
-    if (is_pow2(N)) lds_fft(buf, __builtin_ctz((unsigned)N), T, inverse);
-    else lds_fft_mixed(buf, N, T, inverse);
+    if (!MX || is_pow2(N)) lds_fft(buf, __builtin_ctz((unsigned)N), T, inverse);
+    else if constexpr (MX) lds_fft_mixed(buf, N, T, inverse);
 }
 
 // Compile-time-size variant of lds_fft (exact register footprint, unrolled

@@ -54,13 +54,14 @@ __global__ void k_twiddles(int N, double2 *T, double2 *T2) {
 // ===========================================================================
 // rfft of fp64 rows -> full half spectrum [row][N+1] (model portraits)
 // ===========================================================================
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_rfft_rows(RfftArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
     double2 *o = a.out + row * (int64_t)(N + 1);
     for (int k = threadIdx.x; k <= N; k += kBlock) o[k] = rfft_bin(lds, N, a.T2, k);
 }
@@ -629,6 +630,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
 // ===========================================================================
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // lds: z[N] (packed profile, FFT in place) | xm[N+1] | sh[Ns+8]
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -671,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     }
     __syncthreads();
     const double wsum = sh[0], cnt = sh[1];
-    if (!fused) lds_fft_n(z, a.nbin >> 1, a.T, false);
+    if (!fused) lds_fft_n<MX>(z, a.nbin >> 1, a.T, false);
     // R_k of the fused partials (k < NL; 0 above: past every channel's cutoff)
     auto fused_bin = [&](int k) {
         double2 r = cmk(0.0, 0.0);
@@ -762,14 +764,14 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
 // ===========================================================================
 // k_rotate: out = irfft(rfft(in) * exp(2 pi i k phase_row))
 // ===========================================================================
-template <int KMAX>
+template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
     // harmonics handled by this thread: k = tid + 256 i, k < N (pre-pass pairs k, N-k)
@@ -793,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     double2 *o = reinterpret_cast<double2 *>(a.out) + row * (int64_t)N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
@@ -802,6 +804,7 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
 // ===========================================================================
 // k_noise: get_noise_PS per row
 // ===========================================================================
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 2];
@@ -809,7 +812,7 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
     double acc[1] = {0.0};
     for (int k = threadIdx.x + a.kc; k <= N; k += kBlock) acc[0] += cabs2(rfft_bin(lds, N, a.T2, k));
     block_sum<1>(acc, red);
@@ -819,6 +822,7 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
 // ===========================================================================
 // k_phase_shift: pplib.fit_phase_shift per profile
 // ===========================================================================
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];   // [N] fft | [N+1] xm | sh
     __shared__ double red[kWaves * 4];
@@ -830,7 +834,7 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     const int mi = a.model_index ? a.model_index[prof] : 0;
     load_row(fbuf, a.model, 1, mi, a.nbin);
     __syncthreads();
-    lds_fft_n(fbuf, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(fbuf, a.nbin >> 1, a.T, false);
     double pp[1] = {0.0};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
         double2 M = rfft_bin(fbuf, N, a.T2, k);
@@ -840,7 +844,7 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     __syncthreads();
     load_row(fbuf, a.data, a.dtype, prof, a.nbin);
     __syncthreads();
-    lds_fft_n(fbuf, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(fbuf, a.nbin >> 1, a.T, false);
     double acc[3] = {0.0, 0.0, pp[0]};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
         double2 D = rfft_bin(fbuf, N, a.T2, k);
@@ -900,6 +904,7 @@ __device__ __forceinline__ double u01(uint64_t h) {   // (0, 1]
     return ((double)(h >> 11) + 1.0) * (1.0 / 9007199254740992.0);
 }
 
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
@@ -915,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
         lds[k] = irfft_prebin(X1, X2, a.T2[k]);
     }
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     const int64_t row = (int64_t)s * a.nchan + n;
     for (int j = threadIdx.x; j < N; j += kBlock) {
@@ -983,7 +988,7 @@ __device__ __forceinline__ double2 scat_recip(double b) {
     return cmk(r / d, -1.0 / d);
 }
 
-template <int KMAX>
+template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -1038,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
         // taus = (tau / nbin) * (freqs / nu_ref)**alpha; B_k = 1 / (1 + 2 pi i k tau_n)
         const double tn = tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]);
         __syncthreads();
-        lds_fft_n(lds, a.nbin >> 1, a.T, false);
+        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
         double2 Xk[KMAX], Xn[KMAX];
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
@@ -1062,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
             if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
         }
         __syncthreads();
-        lds_fft_n(lds, a.nbin >> 1, a.T, true);
+        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
         const double sc = 1.0 / (double)N;
         double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
         for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
@@ -1089,13 +1094,22 @@ static inline int log2i(int n) {
     return l;
 }
 
+// launch KER<A, MX> with MX = mx (the mixed-radix FFT compiled in only when
+// nbin / 2 is not a power of two; lds_fft_n)
+#define MXL(mx, KER, A, ...)                                          \
+    do {                                                              \
+        if (mx) hipLaunchKernelGGL((KER<A, true>), __VA_ARGS__);      \
+        else hipLaunchKernelGGL((KER<A, false>), __VA_ARGS__);        \
+    } while (0)
+
 hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st) {
     hipLaunchKernelGGL(k_twiddles, dim3((N + 255) / 256), dim3(256), 0, st, N, T, T2);
     return hipGetLastError();
 }
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    hipLaunchKernelGGL(k_rfft_rows, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_rfft_rows<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    else hipLaunchKernelGGL(k_rfft_rows<true>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 template <int L2>
@@ -1173,18 +1187,20 @@ hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
 
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
     size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
-    hipLaunchKernelGGL(k_guess, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
+    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_guess<false>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
+    else hipLaunchKernelGGL(k_guess<true>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nport * a.nchan)), b(kBlock);
+    const bool mx = !is_pow2(a.nbin / 2);
     switch (kmax_pow2(a.nbin / 2)) {
-        case 1: hipLaunchKernelGGL(k_gauss_port<1>, g, b, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_gauss_port<2>, g, b, lds, st, a); break;
-        case 4: hipLaunchKernelGGL(k_gauss_port<4>, g, b, lds, st, a); break;
-        case 8: hipLaunchKernelGGL(k_gauss_port<8>, g, b, lds, st, a); break;
-        case 16: hipLaunchKernelGGL(k_gauss_port<16>, g, b, lds, st, a); break;
+        case 1: MXL(mx, k_gauss_port, 1, g, b, lds, st, a); break;
+        case 2: MXL(mx, k_gauss_port, 2, g, b, lds, st, a); break;
+        case 4: MXL(mx, k_gauss_port, 4, g, b, lds, st, a); break;
+        case 8: MXL(mx, k_gauss_port, 8, g, b, lds, st, a); break;
+        case 16: MXL(mx, k_gauss_port, 16, g, b, lds, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1192,12 +1208,13 @@ hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
+    const bool mx = !is_pow2(a.nbin / 2);
     switch (kmax_pow2(a.nbin / 2)) {
-        case 1: hipLaunchKernelGGL(k_rotate<1>, g, b, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_rotate<2>, g, b, lds, st, a); break;
-        case 4: hipLaunchKernelGGL(k_rotate<4>, g, b, lds, st, a); break;
-        case 8: hipLaunchKernelGGL(k_rotate<8>, g, b, lds, st, a); break;
-        case 16: hipLaunchKernelGGL(k_rotate<16>, g, b, lds, st, a); break;
+        case 1: MXL(mx, k_rotate, 1, g, b, lds, st, a); break;
+        case 2: MXL(mx, k_rotate, 2, g, b, lds, st, a); break;
+        case 4: MXL(mx, k_rotate, 4, g, b, lds, st, a); break;
+        case 8: MXL(mx, k_rotate, 8, g, b, lds, st, a); break;
+        case 16: MXL(mx, k_rotate, 16, g, b, lds, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1216,7 +1233,7 @@ int align_groups(int nsub, int nchan) {
     return g < 1 ? 1 : g;
 }
 
-template <int KMAX>
+template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
@@ -1235,7 +1252,7 @@ __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
         wtot += w;
         load_row(lds, a.in, a.dtype, row, a.nbin);
         __syncthreads();
-        lds_fft_n(lds, a.nbin >> 1, a.T, false);
+        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
             const int k = threadIdx.x + i * kBlock;
@@ -1262,7 +1279,7 @@ __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
     if (threadIdx.x == 0) a.wpart[(int64_t)g * a.nchan + n] = wtot;
 }
 
-template <int KMAX>
+template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1, n = blockIdx.x;
@@ -1288,7 +1305,7 @@ __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
     double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)n * N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cadd(o[j], cscale(lds[j], sc));
@@ -1309,17 +1326,18 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
         hipError_t e = launch_align_part_w(a, st);
         if (e != hipSuccess) return e;
     }
+    const bool mx = !is_pow2(a.nbin / 2);
     switch (kmax_pow2(a.nbin / 2)) {
-        case 1: if (!wave) hipLaunchKernelGGL(k_align_part<1>, gp, b, lds, st, a);
-                hipLaunchKernelGGL(k_align_fin<1>, gf, b, lds, st, a); break;
-        case 2: if (!wave) hipLaunchKernelGGL(k_align_part<2>, gp, b, lds, st, a);
-                hipLaunchKernelGGL(k_align_fin<2>, gf, b, lds, st, a); break;
-        case 4: if (!wave) hipLaunchKernelGGL(k_align_part<4>, gp, b, lds, st, a);
-                hipLaunchKernelGGL(k_align_fin<4>, gf, b, lds, st, a); break;
-        case 8: if (!wave) hipLaunchKernelGGL(k_align_part<8>, gp, b, lds, st, a);
-                hipLaunchKernelGGL(k_align_fin<8>, gf, b, lds, st, a); break;
-        case 16: if (!wave) hipLaunchKernelGGL(k_align_part<16>, gp, b, lds, st, a);
-                 hipLaunchKernelGGL(k_align_fin<16>, gf, b, lds, st, a); break;
+        case 1: if (!wave) MXL(mx, k_align_part, 1, gp, b, lds, st, a);
+                MXL(mx, k_align_fin, 1, gf, b, lds, st, a); break;
+        case 2: if (!wave) MXL(mx, k_align_part, 2, gp, b, lds, st, a);
+                MXL(mx, k_align_fin, 2, gf, b, lds, st, a); break;
+        case 4: if (!wave) MXL(mx, k_align_part, 4, gp, b, lds, st, a);
+                MXL(mx, k_align_fin, 4, gf, b, lds, st, a); break;
+        case 8: if (!wave) MXL(mx, k_align_part, 8, gp, b, lds, st, a);
+                MXL(mx, k_align_fin, 8, gf, b, lds, st, a); break;
+        case 16: if (!wave) MXL(mx, k_align_part, 16, gp, b, lds, st, a);
+                 MXL(mx, k_align_fin, 16, gf, b, lds, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1331,7 +1349,7 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
 // phasor, irfft dropping the DC / Nyquist imaginary parts), then the
 // residual sum of squares over the bins with a fixed-order block reduction.
 // ===========================================================================
-template <int KMAX>
+template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
@@ -1339,7 +1357,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
 #pragma unroll
@@ -1360,7 +1378,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
         if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
     }
     __syncthreads();
-    lds_fft_n(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N, s = a.scales[row];
     const double *m = a.model + (int64_t)a.model_row[row] * a.nbin;
     double acc[1] = {0.0};
@@ -1379,12 +1397,13 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
 hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
+    const bool mx = !is_pow2(a.nbin / 2);
     switch (kmax_pow2(a.nbin / 2)) {
-        case 1: hipLaunchKernelGGL(k_resid_chi2<1>, g, b, lds, st, a); break;
-        case 2: hipLaunchKernelGGL(k_resid_chi2<2>, g, b, lds, st, a); break;
-        case 4: hipLaunchKernelGGL(k_resid_chi2<4>, g, b, lds, st, a); break;
-        case 8: hipLaunchKernelGGL(k_resid_chi2<8>, g, b, lds, st, a); break;
-        case 16: hipLaunchKernelGGL(k_resid_chi2<16>, g, b, lds, st, a); break;
+        case 1: MXL(mx, k_resid_chi2, 1, g, b, lds, st, a); break;
+        case 2: MXL(mx, k_resid_chi2, 2, g, b, lds, st, a); break;
+        case 4: MXL(mx, k_resid_chi2, 4, g, b, lds, st, a); break;
+        case 8: MXL(mx, k_resid_chi2, 8, g, b, lds, st, a); break;
+        case 16: MXL(mx, k_resid_chi2, 16, g, b, lds, st, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1392,17 +1411,20 @@ hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) 
 
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    hipLaunchKernelGGL(k_noise, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_noise<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    else hipLaunchKernelGGL(k_noise<true>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st) {
     size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
-    hipLaunchKernelGGL(k_phase_shift, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+    else hipLaunchKernelGGL(k_phase_shift<true>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
     size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    hipLaunchKernelGGL(k_synth, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
+    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_synth<false>, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
+    else hipLaunchKernelGGL(k_synth<true>, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 
@@ -1421,6 +1443,7 @@ hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
 // (the resampled spectrum with the DC and Nyquist imaginary parts dropped,
 // as the irfft -> rfft round trip does, times the phasor), one irfft.
 // ===========================================================================
+template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double proj[kSplineMaxComp];
@@ -1475,7 +1498,7 @@ __global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
     double2 *spec = lds + NM;              // output spectrum Y_k, k <= N1
     for (int j = tid; j < N0; j += kBlock) buf[j] = cmk(value(2 * j), value(2 * j + 1));
     __syncthreads();
-    lds_fft_n(buf, a.nbin_model >> 1, a.T0, false);
+    lds_fft_n<MX>(buf, a.nbin_model >> 1, a.T0, false);
     const int num = a.nbin, Nx = a.nbin_model;
     const int Nm = num < Nx ? num : Nx, nyq = Nm / 2 + 1;
     const double scale = (double)num / (double)Nx;
@@ -1497,7 +1520,7 @@ __global__ __launch_bounds__(kBlock) void k_spline_port(SplineArgs a) {
         buf[k] = irfft_prebin(Xk, Xn, a.T21[k]);
     }
     __syncthreads();
-    lds_fft_n(buf, a.nbin >> 1, a.T1, true);
+    lds_fft_n<MX>(buf, a.nbin >> 1, a.T1, true);
     const double sc = 1.0 / (double)N1;
     double2 *o2 = reinterpret_cast<double2 *>(o);
     for (int j = tid; j < N1; j += kBlock) o2[j] = cscale(buf[j], sc);
@@ -1507,8 +1530,12 @@ hipError_t launch_spline_port(const SplineArgs &a, hipStream_t st) {
     const int N0 = a.nbin_model >> 1, N1 = a.nbin >> 1;
     const int NM = N0 > N1 ? N0 : N1;
     const size_t lds = a.nbin == a.nbin_model ? 16 : (size_t)(NM + N1 + 1) * sizeof(double2);
-    hipLaunchKernelGGL(k_spline_port, dim3((unsigned)((int64_t)a.nport * a.nchan)), dim3(kBlock), lds,
-                       st, a);
+    if (is_pow2(N0) && is_pow2(N1))
+        hipLaunchKernelGGL(k_spline_port<false>, dim3((unsigned)((int64_t)a.nport * a.nchan)), dim3(kBlock),
+                           lds, st, a);
+    else
+        hipLaunchKernelGGL(k_spline_port<true>, dim3((unsigned)((int64_t)a.nport * a.nchan)), dim3(kBlock),
+                           lds, st, a);
     return hipGetLastError();
 }
 

@@ -369,8 +369,10 @@ def bench_align(args):
     # (profiles/pmc_reduce.py, mode "align")
     traffic = None
     if os.path.exists(args.pmc):
-        pk = json.load(open(args.pmc)).get("modes", {}).get(
-            "align", {}).get("kernels", {}).get(dom)
+        pm = json.load(open(args.pmc)).get("modes", {}).get("align", {})
+        same = ("%dch x %dbin" % (nchan, nbin)) in str(
+            (pm.get("source") or {}).get("bench", ""))
+        pk = pm.get("kernels", {}).get(dom) if same else None
         if pk:
             traffic = round(pk["hbm_bytes"] * count)
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
@@ -970,10 +972,15 @@ def main():
     units_launch = (steps_subints if "launches" not in dk else
                     steps_subints * mean_passes) / nlaunch
     traffic = None
-    # (the PMC / SQ summaries are of the default, cut configuration)
+    # (the PMC / SQ summaries are of the default, cut configuration of this
+    # fit mode, and apply only at the shape they were collected on)
+    shape_tag = "%dch x %dbin" % (nchan, nbin)
+
+    def _same_shape(m):
+        return shape_tag in str((m.get("source") or {}).get("bench", ""))
     if os.path.exists(args.pmc) and not args.no_hcut:
         pm = json.load(open(args.pmc)).get("modes", {}).get(args.fit, {})
-        pk = pm.get("kernels", {}).get(dom)
+        pk = pm.get("kernels", {}).get(dom) if _same_shape(pm) else None
         if pk:
             traffic = round(pk["hbm_bytes"] * units_launch)
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS,
@@ -991,7 +998,7 @@ def main():
     fpath = os.path.join(ROOT, "profiles", "fp64_summary.json")
     if os.path.exists(fpath) and not args.no_hcut:
         fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
-        fk = fm.get("kernels", {}).get(dom)
+        fk = fm.get("kernels", {}).get(dom) if _same_shape(fm) else None
         if fk:
             tf = fk["flops_per_unit"] * units_launch / (dk["ms"] / nlaunch / 1e3) / 1e12
             fp64 = dict(bound="fp64", achieved=round(tf, 2), peak=FP64_PEAK_TF,

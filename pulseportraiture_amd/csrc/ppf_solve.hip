@@ -1471,7 +1471,24 @@ __device__ __noinline__ void nz_solve(const double *c, int nzcase, int option, d
 #else
 #define PPF_POSTFIT_ATTR
 #endif
-__global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
+// PB threads per sub-int.  64 (one wave) lets four sub-ints share a CU at
+// the kernel's one wave per SIMD, so the serial parts (the zero-covariance
+// root finding, the covariance inversion by thread 0) of four sub-ints
+// overlap instead of one: C2 264.0k -> 269.6k fits/s, C3 73.8-74.3 ->
+// 71.7-71.9 ms per step in one call (tools/g27.sh).  Wide sub-ints keep 256
+// (C5, 16384 channels in 500 sub-ints: 85.0-86.0 vs 86.2-86.7 ms with 64).
+// PPF_POSTFIT_PB forces one of them.
+template <int K, int PB>
+__device__ __forceinline__ void pf_sum(double (&v)[K], double *red) {
+    if constexpr (PB == 64) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
+    } else {
+        pf_sum<K, PB>(v, red);
+    }
+}
+template <int PB>
+__global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
     __shared__ double red[kWaves * 32];
     __shared__ double sh_Xinv[25];
     __shared__ double sh_misc[16];
@@ -1485,7 +1502,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
             res->status = S.status;
             res->phi_guess = S.phi_guess;
         }
-        for (int n = tid; n < a.nchan; n += kBlock) {
+        for (int n = tid; n < a.nchan; n += PB) {
             const int64_t o2 = (int64_t)s * a.nchan + n;
             a.scales[o2] = 0.0; a.scale_errs[o2] = 0.0; a.channel_snrs[o2] = 0.0;
         }
@@ -1511,10 +1528,10 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
     {
         const double *chan = a.chan + (int64_t)s * a.nchan * 4;
         const uint8_t *mk = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-        for (int n = tid; n < a.nchan; n += kBlock)
+        for (int n = tid; n < a.nchan; n += PB)
             if (!mk || mk[n]) sdv[0] += chan[n * 4 + 2];
     }
-    block_sum<1>(sdv, red);
+    pf_sum<1, PB>(sdv, red);
     const double Sd = sdv[0];
     const int nchanx = S.nchanx;
     FitGeom g;
@@ -1533,14 +1550,14 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
         gg.tau_lin = taulin;
         if (!scat) { gg.g_sum = gg.g_tau = gg.g_alpha = false; return; }
         double sm[3] = {0.0, 0.0, 0.0};
-        for (int n = tid; n < v.nchan; n += kBlock) {
+        for (int n = tid; n < v.nchan; n += PB) {
             if (v.mask && !v.mask[n]) continue;
             double tn = taulin * pow(v.fr[n] / gg.nu_tau, alpha);
             sm[0] += tn;
             sm[1] += gg.log10_tau ? kLn10 * tn : tn / taulin;
             sm[2] += log(v.fr[n] / gg.nu_tau) * tn;
         }
-        block_sum<3>(sm, red);
+        pf_sum<3, PB>(sm, red);
         gg.g_sum = sm[0] != 0.0;
         gg.g_tau = gg.g_sum && sm[1] != 0.0;
         gg.g_alpha = sm[2] != 0.0;
@@ -1565,7 +1582,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
         double accv[NZ_MAX + 8];
         for (int i = 0; i < NZ_MAX + 8; ++i) accv[i] = 0.0;
         const double cD = kDconst / g.P, cG = kDconst * kDconst / g.P;
-        for (int n = tid; n < v.nchan; n += kBlock) {
+        for (int n = tid; n < v.nchan; n += PB) {
             if (v.mask && !v.mask[n]) continue;
             const double *st = st_fit + (int64_t)n * 10;
             const double nu = v.fr[n];
@@ -1637,7 +1654,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
                 default: break;
             }
         }
-        block_sum<NZ_MAX + 8>(accv, red);
+        pf_sum<NZ_MAX + 8, PB>(accv, red);
         if (tid == 0) {
             for (int i = 0; i < NZ_MAX + 8; ++i) sh_acc[i] = accv[i];
             int nr_flag = 0;
@@ -1680,7 +1697,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
     gates(go, tau_out_lin, x[4]);
     double cv[31];
     for (int i = 0; i < 31; ++i) cv[i] = 0.0;
-    for (int n = tid; n < v.nchan; n += kBlock) {
+    for (int n = tid; n < v.nchan; n += PB) {
         if (v.mask && !v.mask[n]) continue;
         const double *st = st_fit + (int64_t)n * 10;
         Fac fc = make_fac(v.fr[n], go, x[4]);
@@ -1700,7 +1717,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
                 ++q;
             }
     }
-    block_sum<31>(cv, red);
+    pf_sum<31, PB>(cv, red);
     int sing = 0;
     if (tid == 0) {
         double Xm[5][5], Xi[5][5];
@@ -1725,7 +1742,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
         for (int j2 = 0; j2 < 5; ++j2) Xinv[i2][j2] = sh_Xinv[i2 * 5 + j2];
     // per-channel scales, scale errors, channel S/N
     double sn[1] = {0.0};
-    for (int n = tid; n < v.nchan; n += kBlock) {
+    for (int n = tid; n < v.nchan; n += PB) {
         const int64_t o2 = (int64_t)s * a.nchan + n;
         if (v.mask && !v.mask[n]) {
             a.scales[o2] = 0.0; a.scale_errs[o2] = 0.0; a.channel_snrs[o2] = 0.0;
@@ -1756,7 +1773,7 @@ __global__ __launch_bounds__(kBlock) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a
         a.channel_snrs[o2] = csnr;
         sn[0] += csnr * csnr;
     }
-    block_sum<1>(sn, red);
+    pf_sum<1, PB>(sn, red);
     if (tid == 0) {
         double pe[5] = {0, 0, 0, 0, 0};
         double *cov = a.covariance + (int64_t)s * 25;
@@ -1850,7 +1867,13 @@ hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_postfit(const SolveArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_postfit, dim3((unsigned)a.nsub), dim3(kBlock), 0, st, a);
+#ifdef PPF_POSTFIT_PB
+    const int pb = PPF_POSTFIT_PB;
+#else
+    const int pb = a.nchan <= 2048 ? 64 : 256;
+#endif
+    if (pb == 64) hipLaunchKernelGGL(k_postfit<64>, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_postfit<256>, dim3((unsigned)a.nsub), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -173,6 +173,27 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double *scratch) {
     __syncthreads();
 }
 
+// block_sum / block_max for a TB-thread block: one wave (TB = 64) reduces
+// with DPP alone (no LDS round trip, no barrier); otherwise the block forms
+template <int K, int TB>
+__device__ __forceinline__ void blk_sum(double (&v)[K], double *scratch) {
+    if constexpr (TB == 64) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
+    } else {
+        block_sum<K>(v, scratch);
+    }
+}
+template <int K, int TB>
+__device__ __forceinline__ void blk_max(double (&v)[K], double *scratch) {
+    if constexpr (TB == 64) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = wave_max(v[i]);
+    } else {
+        block_max<K>(v, scratch);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // LDS FFT (Stockham autosort, radix-4 with one leading radix-2 pass when
 // log2 N is odd).  In place in buf[0..N); every thread of the block must call

@@ -1158,7 +1158,8 @@ __device__ unsigned long long g_tprof[8];
 // evaluation is one pass over them (moments of the next channel half in
 // flight while the current half is summed), a fixed-order block reduction
 // of f, g, H and the scipy trust-ncg update on thread 0.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WPE))) void k_tr_mom(SolveArgs a) {
+template <int TB>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WPE))) void k_tr_mom(SolveArgs a) {
     __shared__ TRState L;
     __shared__ double red[kWaves * 10];
     __shared__ int cmdb;
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
     TP_INIT();
     static_assert(sizeof(TRState) % 8 == 0, "TRState copy");
     constexpr int NW = (int)(sizeof(TRState) / 8);
-    for (int i = tid; i < NW; i += kBlock)
+    for (int i = tid; i < NW; i += TB)
         reinterpret_cast<double *>(&L)[i] = reinterpret_cast<const double *>(&G)[i];
     __syncthreads();
     const int nharm = (a.nbin >> 1) + 1;
@@ -1190,7 +1191,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
     const double xmax = m16 ? kX16 : kXMax;
     double *stats = a.stats + (int64_t)s * 2 * a.nchan * 10;
     const int flagmask = L.flagmask;
-    const int nit = (a.nchan + kBlock - 1) / kBlock;
+    const int nit = (a.nchan + TB - 1) / TB;
     __syncthreads();
     if (tid == 0) L.need_mom = 0;
     const int cap = (a.max_iter > 0 ? a.max_iter : 1000) + 4;
@@ -1208,12 +1209,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
             const double *rc = MRES + (int64_t)cand * a.nchan;
             const double *hc = HC + (int64_t)cand * a.nchan;
             double xm[1] = {0.0};          // max_n h_n |Delta_n|
-            for (int n0 = 0; n0 < a.nchan; n0 += 4 * kBlock) {   // 4 channels' loads, then use
+            for (int n0 = 0; n0 < a.nchan; n0 += 4 * TB) {   // 4 channels' loads, then use
                 double v1[4], v2[4], vr[4], vh[4];
                 bool ok[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int n = n0 + tid + kBlock * j, nc = min(n, a.nchan - 1);
+                    const int n = n0 + tid + TB * j, nc = min(n, a.nchan - 1);
                     v1[j] = dp[2 * nc]; v2[j] = dp[2 * nc + 1]; vr[j] = rc[nc];
                     vh[j] = m16 ? hc[nc] : h;
                     ok[j] = n < a.nchan && (!use_mask || mk[nc] != 0);
@@ -1222,7 +1223,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                 for (int j = 0; j < 4; ++j)
                     if (ok[j]) xm[0] = fmax(xm[0], vh[j] * fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
             }
-            block_max<1>(xm, red);
+            blk_max<1, TB>(xm, red);
             if (kTwoPi * xm[0] <= xmax) {
                 qsel = cand;
                 xsel = kTwoPi * xm[0];
@@ -1258,13 +1259,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         double c_d1, c_d2, c_rq, c_S, c_h;      // channel scalars, prefetched with quarter 0
         int c_ok;
         auto ldq = [&](int i, int quarter, double2 (&b)[KQ]) {
-            const int n = min(tid + kBlock * i, a.nchan - 1);
+            const int n = min(tid + TB * i, a.nchan - 1);
             const double2 *p = Mq + (int64_t)n * kMoments + KQ * quarter;
 #pragma unroll
             for (int m = 0; m < KQ; ++m) b[m] = p[m];
         };
         auto ldc = [&](int i) {
-            const int n = min(tid + kBlock * i, a.nchan - 1);
+            const int n = min(tid + TB * i, a.nchan - 1);
             c_d1 = dp[2 * n]; c_d2 = dp[2 * n + 1]; c_rq = rq[n]; c_S = chan[n * 4 + 3];
             c_h = m16 ? hq[n] : h;
             c_ok = mk[n];
@@ -1273,7 +1274,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         ldq(0, 0, qa);
         ldc(0);
         for (int i = 0; i < nit; ++i) {
-            const int n = tid + kBlock * i;
+            const int n = tid + TB * i;
             ldq(i, 1, qb);
             const bool valid = n < a.nchan && (!use_mask || c_ok != 0);
             const double d1 = c_d1, d2 = c_d2, Sn = c_S, hn_ = c_h;
@@ -1324,7 +1325,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
                     acc[4 + e] += hn * dph[hi[e]] * dph[hj[e]];
         }
         TP(2);
-        block_sum<10>(acc, red);
+        blk_sum<10, TB>(acc, red);
         TP(3);
         if (tid == 0) {
             double o[21];
@@ -1348,7 +1349,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_TRMO
         if (!cmdb) break;
     }
     __syncthreads();
-    for (int i = tid; i < NW; i += kBlock)
+    for (int i = tid; i < NW; i += TB)
         reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&L)[i];
     TP(6);
     TP_DONE();
@@ -1478,15 +1479,6 @@ __device__ __noinline__ void nz_solve(const double *c, int nzcase, int option, d
 // 71.7-71.9 ms per step in one call (tools/g27.sh).  Wide sub-ints keep 256
 // (C5, 16384 channels in 500 sub-ints: 85.0-86.0 vs 86.2-86.7 ms with 64).
 // PPF_POSTFIT_PB forces one of them.
-template <int K, int PB>
-__device__ __forceinline__ void pf_sum(double (&v)[K], double *red) {
-    if constexpr (PB == 64) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
-    } else {
-        pf_sum<K, PB>(v, red);
-    }
-}
 template <int PB>
 __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
     __shared__ double red[kWaves * 32];
@@ -1531,7 +1523,7 @@ __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
         for (int n = tid; n < a.nchan; n += PB)
             if (!mk || mk[n]) sdv[0] += chan[n * 4 + 2];
     }
-    pf_sum<1, PB>(sdv, red);
+    blk_sum<1, PB>(sdv, red);
     const double Sd = sdv[0];
     const int nchanx = S.nchanx;
     FitGeom g;
@@ -1557,7 +1549,7 @@ __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
             sm[1] += gg.log10_tau ? kLn10 * tn : tn / taulin;
             sm[2] += log(v.fr[n] / gg.nu_tau) * tn;
         }
-        pf_sum<3, PB>(sm, red);
+        blk_sum<3, PB>(sm, red);
         gg.g_sum = sm[0] != 0.0;
         gg.g_tau = gg.g_sum && sm[1] != 0.0;
         gg.g_alpha = sm[2] != 0.0;
@@ -1654,7 +1646,7 @@ __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
                 default: break;
             }
         }
-        pf_sum<NZ_MAX + 8, PB>(accv, red);
+        blk_sum<NZ_MAX + 8, PB>(accv, red);
         if (tid == 0) {
             for (int i = 0; i < NZ_MAX + 8; ++i) sh_acc[i] = accv[i];
             int nr_flag = 0;
@@ -1717,7 +1709,7 @@ __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
                 ++q;
             }
     }
-    pf_sum<31, PB>(cv, red);
+    blk_sum<31, PB>(cv, red);
     int sing = 0;
     if (tid == 0) {
         double Xm[5][5], Xi[5][5];
@@ -1773,7 +1765,7 @@ __global__ __launch_bounds__(PB) PPF_POSTFIT_ATTR void k_postfit(SolveArgs a) {
         a.channel_snrs[o2] = csnr;
         sn[0] += csnr * csnr;
     }
-    pf_sum<1, PB>(sn, red);
+    blk_sum<1, PB>(sn, red);
     if (tid == 0) {
         double pe[5] = {0, 0, 0, 0, 0};
         double *cov = a.covariance + (int64_t)s * 25;
@@ -1862,7 +1854,17 @@ hipError_t launch_moments(const SolveArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(k_tr_mom, dim3((unsigned)a.nsub), dim3(kBlock), 0, st, a);
+    // (one wave per sub-int, as k_postfit, measured slower here: C2 solve
+    // stage 815 vs 777 ms per 24 calls, C4 305-332k vs 338-339k
+    // archive-iterations/s, tools/g28.sh: the evaluation pass, not the
+    // thread-0 update, is most of a launch)
+#ifdef PPF_TRMOM_TB
+    const int tb = PPF_TRMOM_TB;
+#else
+    const int tb = 256;
+#endif
+    if (tb == 64) hipLaunchKernelGGL(k_tr_mom<64>, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_tr_mom<256>, dim3((unsigned)a.nsub), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -610,8 +610,11 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False,
 _PINNED = {}
 _PINNED_LOCK = threading.Lock()
 # page-locked DATA buffers per device (env PPF_PINNED_SLOTS, default 4): a
-# read may run this many archives minus one ahead of the oldest upload
+# read may run this many archives minus one ahead of the oldest upload.
+# Archives so large that the slots would pin more than PPF_PINNED_MAX_MB
+# (default 4096) rotate through fewer of them (at least two).
 _PIN_SLOTS = max(2, int(os.environ.get("PPF_PINNED_SLOTS", "4")))
+_PIN_BUDGET = int(os.environ.get("PPF_PINNED_MAX_MB", "4096")) << 20
 
 
 class _UploadTicket(object):
@@ -635,10 +638,12 @@ class _UploadTicket(object):
 def _pinned_buffer(dev, nbytes):
     import torch
     with _PINNED_LOCK:
-        pool = _PINNED.setdefault(dev.index,
-                                  [[None, None] for _ in range(_PIN_SLOTS)])
-        slot = pool.pop(0)
-        pool.append(slot)
+        pool = _PINNED.setdefault(dev.index, dict(
+            slots=[[None, None] for _ in range(_PIN_SLOTS)], next=0))
+        n = max(2, min(_PIN_SLOTS, _PIN_BUDGET // max(nbytes, 1)))
+        i = pool["next"] % n
+        pool["next"] = i + 1
+        slot = pool["slots"][i]
     buf, ev = slot
     if ev is not None:
         ev.synchronize()

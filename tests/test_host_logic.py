@@ -80,3 +80,29 @@ def test_raise_if_any_failed_puts_the_flag_on_the_device(monkeypatch):
     with pytest.raises(KeyError):
         dist.raise_if_any_failed(KeyError("x"))
     assert seen == [torch.device("cuda", 2)] * 2
+
+
+def test_unflat_matches_the_row_table():
+    """A one-rank fit's outputs come back as ONE buffer (engine._fit_slice's
+    `_flat`: results | scales | scale_errs | channel_snrs | covariance) and
+    are cut on the host by pptoas._unflat; the same arrays as the row table
+    (_pack / _unpack) the sharded path all-gathers."""
+    from pulseportraiture_amd import pptoas
+    nsub, nchan = 3, 5
+    R = _lib.RESULT_DOUBLES
+    sizes = (nsub * R, nsub * nchan, nsub * nchan, nsub * nchan, nsub * 25)
+    flat = torch.arange(sum(sizes), dtype=torch.float64)
+    views, o = [], 0
+    for n in sizes:
+        views.append(flat[o:o + n])
+        o += n
+    res = dict(results=views[0].view(nsub, R),
+               scales=views[1].view(nsub, nchan),
+               scale_errs=views[2].view(nsub, nchan),
+               channel_snrs=views[3].view(nsub, nchan),
+               covariance=views[4].view(nsub, 5, 5), _flat=flat)
+    a = pptoas._unflat(res, flat.numpy())
+    b = pptoas._unpack(pptoas._pack(res).numpy(), nchan)
+    for k in ("results", "scales", "scale_errs", "channel_snrs", "covariance"):
+        np.testing.assert_array_equal(a[k], b[k])
+        np.testing.assert_array_equal(a[k], res[k].numpy())

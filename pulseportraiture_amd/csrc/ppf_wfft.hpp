@@ -272,5 +272,128 @@ __device__ __forceinline__ void fft_row(double2 (&x)[Plan<LOG2N>::R], double2 *b
     stages_from<LOG2N, 1>(buf, T, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Half-buffer variant (round-4 prototype, k_noise_h): the same stages and
+// arithmetic as fft_row, but each exchange goes through a buffer of doubles
+// (the padded slot map of the complex buffer, 8 B per slot) in two sweeps,
+// real parts then imaginary parts.  Half the LDS per wave (8.7 KB at 1024
+// points instead of 17.4 KB), so the LDS no longer caps a CU at two waves
+// per SIMD; the results are bit-identical to fft_row (only the exchange
+// differs).  hb: the wave's buffer_slots<LOG2N>() doubles.
+template <int LOG2N, int ST, int B, int Q, int PART>
+__device__ __forceinline__ void hstage_read_q(const double *hb, const int (&lb)[2],
+                                              double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int rad = P::radix(ST), NB = P::N / rad;
+    if constexpr (Q < rad) {
+        const double t = hb[lane_slot<LOG2N, 64 * B + Q * NB>(lb)];
+        if constexpr (PART == 0) v[B][Q].x = t;
+        else v[B][Q].y = t;
+        hstage_read_q<LOG2N, ST, B, Q + 1, PART>(hb, lb, v);
+    }
+}
+template <int LOG2N, int ST, int B, int PART>
+__device__ __forceinline__ void hstage_read(const double *hb, const int (&lb)[2],
+                                            double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int rad = P::radix(ST), NB = P::N / rad, BPL = NB / 64;
+    if constexpr (B < BPL) {
+        hstage_read_q<LOG2N, ST, B, 0, PART>(hb, lb, v);
+        hstage_read<LOG2N, ST, B + 1, PART>(hb, lb, v);
+    }
+}
+// write the stage outputs v (PART of each) to their slots
+template <int LOG2N, int ST, int PART>
+__device__ __forceinline__ void hstage_write(double *hb, int lane,
+                                             const double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int N = P::N, rad = P::radix(ST), L = P::L(ST);
+    constexpr int NB = N / rad, BPL = NB / 64;
+#pragma unroll
+    for (int b = 0; b < BPL; ++b) {
+        const int j = lane + 64 * b, k = j & (L - 1);
+        const int o = (j - k) * rad + k;
+#pragma unroll
+        for (int q = 0; q < rad; ++q) {
+            const double t = PART == 0 ? v[b][q].x : v[b][q].y;
+            if constexpr (L % Swz<LOG2N>::FREE == 0)
+                hb[pad<LOG2N>(o) + q * L + (use_xor<LOG2N>() ? 0 : (q * L) >> P::S)] = t;
+            else
+                hb[pad<LOG2N>(o + q * L)] = t;
+        }
+    }
+}
+// stage ST >= 1 whose inputs are the previous stage's outputs vp (still in
+// registers): exchange them through hb (two sweeps), twiddle, DFT; the
+// outputs stay in v
+template <int LOG2N, int ST, int PST>
+__device__ __forceinline__ void hstage(double *hb, const double2 *__restrict__ T, int lane,
+                                       const double2 (&vp)[Plan<LOG2N>::N / Plan<LOG2N>::radix(PST) / 64][Plan<LOG2N>::radix(PST)],
+                                       double2 (&v)[Plan<LOG2N>::N / Plan<LOG2N>::radix(ST) / 64][Plan<LOG2N>::radix(ST)]) {
+    using P = Plan<LOG2N>;
+    constexpr int N = P::N, rad = P::radix(ST), L = P::L(ST);
+    constexpr int NB = N / rad, BPL = NB / 64, TS = N / (rad * L);
+    const int lb[2] = {pad<LOG2N>(lane), pad<LOG2N>(lane + 64) - 64};
+    hstage_write<LOG2N, PST, 0>(hb, lane, vp);
+    wave_sync();
+    hstage_read<LOG2N, ST, 0, 0>(hb, lb, v);
+    wave_sync();
+    hstage_write<LOG2N, PST, 1>(hb, lane, vp);
+    wave_sync();
+    hstage_read<LOG2N, ST, 0, 1>(hb, lb, v);
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < BPL; ++b) {
+        const int j = lane + 64 * b, k = j & (L - 1);
+        const double2 w1 = T[k * TS];
+        double2 wq = w1;
+        v[b][1] = cmul(v[b][1], w1);
+#pragma unroll
+        for (int q = 2; q < rad; ++q) {
+            wq = cmul(wq, w1);
+            v[b][q] = cmul(v[b][q], wq);
+        }
+        dft<rad>(v[b]);
+    }
+}
+// the whole transform from registers x (stage-0 inputs, as fft_row) to the
+// last stage's outputs in registers (vl: [N / radix(NST-1) / 64][radix]),
+// written nowhere: the caller reads them out through hb (hwrite_last)
+template <int LOG2N, int ST>
+struct HBlk {
+    using P = Plan<LOG2N>;
+    using T = double2[P::N / P::radix(ST) / 64][P::radix(ST)];
+};
+template <int LOG2N, int ST>
+__device__ __forceinline__ void hstages_from(double *hb, const double2 *__restrict__ T, int lane,
+                                             const typename HBlk<LOG2N, ST - 1>::T &vp,
+                                             typename HBlk<LOG2N, Plan<LOG2N>::NST - 1>::T &vl) {
+    if constexpr (ST == Plan<LOG2N>::NST - 1) {
+        hstage<LOG2N, ST, ST - 1>(hb, T, lane, vp, vl);
+    } else {
+        typename HBlk<LOG2N, ST>::T v;
+        hstage<LOG2N, ST, ST - 1>(hb, T, lane, vp, v);
+        hstages_from<LOG2N, ST + 1>(hb, T, lane, v, vl);
+    }
+}
+template <int LOG2N>
+__device__ __forceinline__ void fft_row_h(double2 (&x)[Plan<LOG2N>::R], double *hb,
+                                          const double2 *__restrict__ T, int lane,
+                                          typename HBlk<LOG2N, Plan<LOG2N>::NST - 1>::T &vl) {
+    using P = Plan<LOG2N>;
+    static_assert(P::NST >= 2, "half-buffer FFT: at least two stages");
+    dft<P::R>(x);
+    typename HBlk<LOG2N, 0>::T v0;
+#pragma unroll
+    for (int q = 0; q < P::R; ++q) v0[0][q] = x[q];
+    hstages_from<LOG2N, 1>(hb, T, lane, v0, vl);
+}
+// the last stage's outputs, PART (0: re, 1: im), to their natural-order slots
+template <int LOG2N, int PART>
+__device__ __forceinline__ void hwrite_last(double *hb, int lane,
+                                            const typename HBlk<LOG2N, Plan<LOG2N>::NST - 1>::T &vl) {
+    hstage_write<LOG2N, Plan<LOG2N>::NST - 1, PART>(hb, lane, vl);
+}
+
 }  // namespace wfft
 }  // namespace ppf

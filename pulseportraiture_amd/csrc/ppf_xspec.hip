@@ -1063,8 +1063,101 @@ __global__ __launch_bounds__(64 * kNoiseW) void k_noise_w(NoiseArgs a, int64_t n
     }
 }
 
+// k_noise_h: k_noise_w on the half-buffer FFT (wfft::fft_row_h) without the
+// next-row prefetch: 8.7 KB of LDS and fewer VGPRs per wave at 1024 points,
+// so more waves per SIMD; bit-identical results (round-4 prototype of the
+// wave-FFT restructure; PPF_NOISE_HALF=1 selects it).
+#ifndef PPF_NOISE_HALF
+#define PPF_NOISE_HALF 0
+#endif
+#ifndef PPF_NOISE_HALF_WPE
+#define PPF_NOISE_HALF_WPE 3
+#endif
+template <int LOG2N, int DT>
+__global__ __launch_bounds__(64 * kNoiseW) __attribute__((amdgpu_waves_per_eu(PPF_NOISE_HALF_WPE)))
+void k_noise_h(NoiseArgs a, int64_t nrows) {
+    using P = wfft::Plan<LOG2N>;
+    constexpr int N = P::N, R = P::R, NP = N / 128;
+    constexpr int SL = wfft::buf_slots<LOG2N>();
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *tw = lds;
+    double *hb = reinterpret_cast<double *>(lds + tw_slots<LOG2N>()) + wave * SL;
+    for (int i = threadIdx.x; i < tw_slots<LOG2N>(); i += 64 * kNoiseW) tw[i] = a.T[i];
+    __syncthreads();
+    const double2 w_seed = a.T2[lane], w_step = a.T2[64];
+    const RowT *rows = reinterpret_cast<const RowT *>(a.in);
+    const int64_t nw = (int64_t)gridDim.x * kNoiseW;
+    for (int64_t row = (int64_t)blockIdx.x * kNoiseW + wave; row < nrows; row += nw) {
+        double2 x[R];
+        const RowT *src = rows + row * N;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const RowT z = src[lane + 64 * q];
+            x[q] = cmk((double)z.x, (double)z.y);
+        }
+        typename wfft::HBlk<LOG2N, P::NST - 1>::T vl;
+        wfft::fft_row_h<LOG2N>(x, hb, tw, lane, vl);
+        // the (k, N - k) pairs: real parts, then imaginary parts
+        double zr[2 * NP + 1], zi[2 * NP + 1];
+        wfft::hwrite_last<LOG2N, 0>(hb, lane, vl);
+        wfft::wave_sync();
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int k = lane + 64 * i;
+            zr[2 * i] = hb[wfft::pad<LOG2N>(k)];
+            zr[2 * i + 1] = hb[k == 0 ? 0 : wfft::pad<LOG2N>(N - k)];
+        }
+        zr[2 * NP] = hb[wfft::pad<LOG2N>(N / 2)];
+        wfft::wave_sync();
+        wfft::hwrite_last<LOG2N, 1>(hb, lane, vl);
+        wfft::wave_sync();
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int k = lane + 64 * i;
+            zi[2 * i] = hb[wfft::pad<LOG2N>(k)];
+            zi[2 * i + 1] = hb[k == 0 ? 0 : wfft::pad<LOG2N>(N - k)];
+        }
+        zi[2 * NP] = hb[wfft::pad<LOG2N>(N / 2)];
+        wfft::wave_sync();
+        double pn = 0.0;
+        double2 w = w_seed;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int klo = lane + 64 * i, khi = N - klo;
+            // rfft_pair on register copies of the two bins
+            const double2 zk = cmk(zr[2 * i], zi[2 * i]), zn = cmk(zr[2 * i + 1], zi[2 * i + 1]);
+            const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+            const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
+            const double2 wo = cmul(w, o);
+            const double2 Dlo = cmk(e.x + wo.y, e.y - wo.x);
+            const double2 Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
+            w = cmul(w, w_step);
+            if (klo >= a.kc) pn += cabs2(Dlo);
+            if (khi >= a.kc) pn += cabs2(Dhi);
+        }
+        if (lane == 0 && N / 2 >= a.kc) pn += cabs2(cmk(zr[2 * NP], zi[2 * NP]));
+        pn = wave_sum(pn);
+        if (lane == 0) a.out[row] = sqrt(pn / (double)a.nbin / (double)(N + 1 - a.kc));
+    }
+}
+
+template <int LOG2N, int DT>
+static void launch_nh(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
+    const size_t lds = (size_t)tw_slots<LOG2N>() * sizeof(double2) +
+                       (size_t)kNoiseW * wfft::buf_slots<LOG2N>() * sizeof(double);
+    const int64_t want = (nrows + kNoiseW - 1) / kNoiseW;
+    const unsigned grid = (unsigned)std::min<int64_t>(want, 256 * 24);
+    hipLaunchKernelGGL((k_noise_h<LOG2N, DT>), dim3(grid), dim3(64 * kNoiseW), lds, st, a, nrows);
+}
+
 template <int LOG2N, int DT>
 static void launch_nw(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
+    if (PPF_NOISE_HALF && LOG2N == 10) {
+        launch_nh<LOG2N, DT>(a, nrows, st);
+        return;
+    }
     const size_t lds = ((size_t)kNoiseW * wfft::buf_slots<LOG2N>() + tw_slots<LOG2N>()) * sizeof(double2);
     // two to four workgroups per CU by LDS; a few rows per wave
     const int64_t want = (nrows + kNoiseW - 1) / kNoiseW;

@@ -1089,13 +1089,29 @@ void k_noise_h(NoiseArgs a, int64_t nrows) {
     const double2 w_seed = a.T2[lane], w_step = a.T2[64];
     const RowT *rows = reinterpret_cast<const RowT *>(a.in);
     const int64_t nw = (int64_t)gridDim.x * kNoiseW;
-    for (int64_t row = (int64_t)blockIdx.x * kNoiseW + wave; row < nrows; row += nw) {
+    // the first PF of the next row's R loads per lane are in flight during
+    // this row's transform (PPF_NOISE_HALF_PF; 0: none)
+#ifndef PPF_NOISE_HALF_PF
+#define PPF_NOISE_HALF_PF 0
+#endif
+    constexpr int PF = PPF_NOISE_HALF_PF < R ? PPF_NOISE_HALF_PF : R;
+    RowT zp[PF > 0 ? PF : 1];
+    int64_t row = (int64_t)blockIdx.x * kNoiseW + wave;
+    if (PF > 0 && row < nrows) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) zp[q] = rows[row * N + lane + 64 * q];
+    }
+    for (; row < nrows; row += nw) {
         double2 x[R];
         const RowT *src = rows + row * N;
 #pragma unroll
         for (int q = 0; q < R; ++q) {
-            const RowT z = src[lane + 64 * q];
+            const RowT z = q < PF ? zp[q % (PF > 0 ? PF : 1)] : src[lane + 64 * q];
             x[q] = cmk((double)z.x, (double)z.y);
+        }
+        if (PF > 0 && row + nw < nrows) {
+#pragma unroll
+            for (int q = 0; q < PF; ++q) zp[q] = rows[(row + nw) * N + lane + 64 * q];
         }
         typename wfft::HBlk<LOG2N, P::NST - 1>::T vl;
         wfft::fft_row_h<LOG2N>(x, hb, tw, lane, vl);

@@ -960,6 +960,73 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
         reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&S)[i];
 }
 
+// k_tr_step_l: the same update with one LANE per sub-int (64 sub-ints per
+// single-wave workgroup, their states in LDS): the serial trust-region update
+// (eigen / secular-equation subproblem, a few thousand dependent f64
+// operations) of 64 sub-ints runs in one wave's lanes instead of one lane of
+// 64 waves.  The block partials are summed in block order (k_tr_step: a wave
+// reduction; identical for one or two blocks).  The scattering gates at the
+// new proposal need a pass over the channels: k_tr_gates, a wave per flagged
+// sub-int, follows.  It pays where there are many narrow sub-ints (C3, 10k
+// x 512 channels: 68.4-70.2 vs 71.3-71.7 ms per step) and not for a few wide
+// ones (C5, 500 x 16384: 87.5-88.2 vs 83.6-85.3 ms; 8 waves on the chip and
+// 64 block partials per lane), tools/g33.sh.  PPF_TRSTEP_LANE: 1 = by shape
+// (nsub >= 2048 and nchan <= 2048; default), 2 = always (the whole GPU suite
+// passed so), 0 = never.
+#ifndef PPF_TRSTEP_LANE
+#define PPF_TRSTEP_LANE 1
+#endif
+template <bool BOX>
+__global__ __launch_bounds__(64) void k_tr_step_l(SolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double tsl[];
+    TRState *Ls = reinterpret_cast<TRState *>(tsl);
+    constexpr int NW = (int)(sizeof(TRState) / 8);
+    const int lane = threadIdx.x;
+    const int n0 = blockIdx.x * 64, cnt = min(64, a.nsub - n0);
+    if (cnt <= 0) return;
+    const double *gsrc = reinterpret_cast<const double *>(a.state + n0);
+    for (int i = lane; i < cnt * NW; i += 64) tsl[i] = gsrc[i];
+    __syncthreads();
+    const int s = n0 + lane;
+    TRState &S = Ls[lane < cnt ? lane : 0];
+    const bool act = lane < cnt && S.phase != PH_DONE && !S.mmode;
+    if (act) {
+        const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
+        double o[21];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) o[i] = 0.0;
+        for (int b = 0; b < nblk; ++b) {
+            const double *p = a.partials + ((int64_t)s * nblk + b) * 21;
+#pragma unroll
+            for (int i = 0; i < 21; ++i) o[i] += p[i];
+        }
+        const int cmd = S.newton ? tr_update_newton_n<5>(S, o, a.max_iter) : tr_update<5, BOX>(S, o, a.max_iter);
+        S.step_cmd = cmd;
+        if (cmd) atomicAdd(a.active, 1u);
+    } else if (lane < cnt) {
+        S.step_cmd = 0;
+    }
+    __syncthreads();
+    double *gdst = reinterpret_cast<double *>(a.state + n0);
+    for (int i = lane; i < cnt * NW; i += 64) gdst[i] = tsl[i];
+}
+
+// the reference gates (taus.sum(), dtau.sum(), dalpha.sum()) at the proposal
+// of every scattering sub-int whose k_tr_step_l update asked for a pass
+__global__ __launch_bounds__(kBlock) void k_tr_gates(SolveArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int s = blockIdx.x * kWaves + wave;
+    if (s >= a.nsub) return;
+    TRState &G = a.state[s];
+    if (!G.step_cmd || !G.scat || G.mmode) return;
+    const double t3 = G.th[3], t4 = G.th[4];
+    const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+    int gs, gt, ga;
+    wave_gates(a.dphi + (int64_t)s * a.nchan * 2, a.mask ? a.mask + (int64_t)s * a.nchan : nullptr,
+               a.nchan, tl, t4, a.log10_tau, gs, gt, ga);
+    if (lane == 0) { G.g_sum = gs; G.g_tau = gt; G.g_alpha = ga; }
+}
+
 // ===========================================================================
 // Moment-expansion evaluation (fits without scattering).
 //
@@ -1840,6 +1907,17 @@ hipError_t launch_pass(const SolveArgs &a, hipStream_t st) {
 
 hipError_t launch_tr_step(const SolveArgs &a, hipStream_t st) {
     const dim3 g((unsigned)((a.nsub + kWaves - 1) / kWaves));
+    const bool lane = PPF_TRSTEP_LANE == 2 || (PPF_TRSTEP_LANE == 1 && a.nsub >= 2048 && a.nchan <= 2048);
+    if (lane) {
+        const dim3 gl((unsigned)((a.nsub + 63) / 64));
+        const size_t lds = 64 * sizeof(TRState);
+        if (a.bounds) hipLaunchKernelGGL(k_tr_step_l<true>, gl, dim3(64), lds, st, a);
+        else hipLaunchKernelGGL(k_tr_step_l<false>, gl, dim3(64), lds, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (a.any_scat) hipLaunchKernelGGL(k_tr_gates, g, dim3(kBlock), 0, st, a);
+        return hipGetLastError();
+    }
     if (a.bounds)
         hipLaunchKernelGGL(k_tr_step<true>, g, dim3(kBlock), 0, st, a);
     else

@@ -31,7 +31,7 @@ struct TRState {
     // box bounds of method='TNC' (pptoas.py:503-513, pptoaslib.py:1041-1053);
     // bnd = 0: none on any fitted parameter (lo = -inf, hi = +inf)
     double lo[5], hi[5];
-    int bnd, pad3;
+    int bnd, step_cmd;    // step_cmd: k_tr_step_l's update asked for another pass
     double pnorm;         // Newton solver: |scaled step| of the pending proposal
     int nsubev, sub0;     // evaluations on the channel subset; its initial stride
 };

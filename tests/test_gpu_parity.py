@@ -1105,3 +1105,26 @@ def test_copy_from_pinned_and_stage_host():
     for (a, _), k, c in zip(items, outs[True], outs[False]):
         np.testing.assert_array_equal(k, a)
         np.testing.assert_array_equal(c, a)
+
+
+@pytest.mark.gpu
+def test_lane_trust_region_step_equals_wave_step():
+    """Scattering fits of a batch large enough for the lane-per-sub-int
+    trust-region step (k_tr_step_l + k_tr_gates: nsub >= 2048, nchan <=
+    2048) equal, bitwise, the same sub-ints fitted in a small batch (the
+    wave-per-sub-int k_tr_step): a sub-int's fit does not depend on its
+    batch, and with one channel block the block sums agree exactly."""
+    from pulseportraiture_amd import engine
+    nsub, nchan, nbin = 2048, 32, 128
+    b, nu_fit, init = _scat_batch(nsub, nchan, nbin, first=777)
+    flags = [1, 1, 0, 1, 1]
+    kw = dict(nu_fits=np.full((nsub, 3), nu_fit), log10_tau=True)
+    big = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags, **kw))
+    k = 24
+    small = engine.results_numpy(engine.fit_batch(
+        b["data"][:k], b["model"], b["freqs"], b["P"][:k], init[:k], flags,
+        nu_fits=kw["nu_fits"][:k], log10_tau=True))
+    for key in ("results", "scales", "scale_errs", "channel_snrs",
+                "covariance"):
+        np.testing.assert_array_equal(small[key], big[key][:k], err_msg=key)

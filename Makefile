@@ -39,3 +39,34 @@ clean:
 	rm -f $(OBJS) $(OUT)
 
 .PHONY: all clean
+
+# Host sanitizer build: the same library with its HOST code
+# under AddressSanitizer + UndefinedBehaviorSanitizer (device code is not
+# instrumented: GPU sanitizers are unavailable on the pool).  Run the CPU
+# tests against it with tools/asan_tests.sh (LD_PRELOADs clang's runtime).
+ASAN_DIR := pulseportraiture_amd/lib/asan
+ASAN_OUT := $(ASAN_DIR)/libppfit.so
+ASAN_HOST := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+             -Xarch_host -fno-omit-frame-pointer -Xarch_host -fno-sanitize-recover=undefined
+ASAN_OBJS := $(patsubst $(CSRC)/%.o,$(ASAN_DIR)/%.o,$(OBJS))
+
+asan: $(ASAN_OUT)
+
+$(ASAN_DIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(HIPFLAGS) -O1 $(ASAN_HOST) -c $< -o $@
+
+$(ASAN_DIR)/ppf_api.o: $(CSRC)/ppf_api.cpp $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(HIPFLAGS) -O1 $(ASAN_HOST) -x hip -c $< -o $@
+
+$(ASAN_DIR)/ppf_io.o: $(CSRC)/ppf_io.cpp include/ppfit.h
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) -O1 -g -std=c++17 -fPIC -Wall -pthread -fsanitize=address,undefined \
+	    -fno-omit-frame-pointer -fno-sanitize-recover=undefined -c $< -o $@
+
+$(ASAN_OUT): $(ASAN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -pthread -shared-libasan \
+	    -fsanitize=address,undefined -o $@ $(ASAN_OBJS)
+
+.PHONY: asan

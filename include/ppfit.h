@@ -17,7 +17,9 @@
  *   - Return value: PPF_OK (0) or a negative PPF_E* code; ppf_last_error()
  *     gives the message.  Per-sub-integration numerical outcomes are reported
  *     in ppf_result.status, never by aborting the batch.
- *   - nbin must be a power of two in [32, 8192].
+ *   - nbin: even, 32 <= nbin <= 8192, with nbin/2 = 2^a 3^b 5^c 7^d (the
+ *     mixed-radix LDS FFT); anything else returns PPF_EUNSUP.  Powers of two
+ *     in [256, 2048] take the wave-per-row kernels.
  *   - Threads: ppf_fit_batch / ppf_fit2_batch must not run concurrently on
  *     the same context (they share its profiling event ring and pinned
  *     iteration counter); any other entry point may run on another host
@@ -36,7 +38,11 @@
 extern "C" {
 #endif
 
-#define PPF_ABI_VERSION 3
+/* ABI 4 (round 5): the options PPF_OPT_MOM_X / PPF_OPT_FUSED_MOM, elem = 3
+ * of ppf_unpack_psrfits_batch, PPF_EIO, ppf_read_rows and
+ * ppf_copy_from_pinned (added in round 4 without a bump), and
+ * ppf_kernel_ms_history slot 0 = the first moment pass of either kind. */
+#define PPF_ABI_VERSION 4
 
 enum ppf_error {
     PPF_OK = 0,
@@ -98,10 +104,14 @@ enum ppf_option {
                                 harmonics), instead of the fused pass that
                                 re-FFTs the data rows for every moment
                                 centre (k_xmom_g): every sub-int then holds
-                                an X slot (x_subints is ignored).  Default
-                                (neither this nor PPF_OPT_FUSED_MOM) where
-                                the GetTOAs guess rides along in the
-                                spectrum pass: guess != 0 and nbin = 2048 */
+                                an X slot (x_subints and PPF_OPT_NO_X are
+                                overridden: nsub * nchan * (nbin/2 + 1) * 16
+                                bytes of workspace, 8.4 MB per 512 x 2048
+                                sub-int; ppf_fit_workspace_bytes includes
+                                it).  Default (neither this nor
+                                PPF_OPT_FUSED_MOM) where the GetTOAs guess
+                                rides along in the spectrum pass: guess != 0
+                                and nbin = 2048 */
     PPF_OPT_FUSED_MOM = 16   /* force the fused k_xmom_g pass (no X for the
                                 phase/DM/GM fits) */
 };
@@ -227,9 +237,13 @@ int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4);
  * in a ring, so a timed loop records without synchronising. */
 int ppf_stage_ms_history(ppf_ctx *ctx, int n, double *ms);
 /* Single-kernel times of the last n profiled ppf_fit_batch calls into
- * ms[n][2]: [0] the first fused moment pass over the data (k_xmom_g, every
- * moment-mode sub-int; 0 if the call had none), [1] the guess-profile pass
- * (k_dsum_w; 0 without a guess).  Same event ring as ppf_stage_ms_history. */
+ * ms[n][2]: [0] the call's first moment pass over every moment-mode sub-int
+ * -- the fused k_xmom_g over the data rows, or, on the moments-from-X path
+ * (PPF_OPT_MOM_X, and the GetTOAs default at nbin 2048), k_moments over the
+ * stored cross spectrum; 0 if the call had none -- and [1] the separate
+ * guess-profile pass (k_dsum_w; 0 without a guess or when the guess rides in
+ * the spectrum pass).  The spectrum pass itself (k_xspec_w) is stage [1] of
+ * ppf_stage_ms_history.  Same event ring as ppf_stage_ms_history. */
 int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms);
 /* The streaming passes (k_pass: one trust-region evaluation of every
  * scattering fit still iterating) of the last n profiled ppf_fit_batch calls

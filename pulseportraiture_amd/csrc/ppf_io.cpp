@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -46,8 +47,15 @@ extern "C" int ppf_read_rows(int32_t fd, int64_t offset, int64_t row_stride, int
     };
     const int nt = (int)std::min<int64_t>(nthreads, npieces);
     std::vector<std::thread> pool;
-    pool.reserve(nt > 0 ? nt - 1 : 0);
-    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    // no exception may cross the C ABI: a thread that cannot be started
+    // (thread limit, memory) leaves its pieces to the threads that did
+    // start (they all take pieces from the shared counter), the calling
+    // thread included
+    try {
+        pool.reserve(nt > 0 ? nt - 1 : 0);
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    } catch (const std::exception &) {
+    }
     work();
     for (auto &th : pool) th.join();
     return failed.load() ? PPF_EIO : PPF_OK;

@@ -960,12 +960,38 @@ __global__ __launch_bounds__(kBlock) void k_tr_step(SolveArgs a) {
         reinterpret_cast<double *>(&G)[i] = reinterpret_cast<const double *>(&S)[i];
 }
 
+// The sum k_tr_step forms from nblk block partials p[b * stride], in ONE
+// lane: lane b of its wave adds blocks b, b + 64, ... in order, and wave_sum
+// adds the 64 lane values as a balanced pairwise tree (DPP xor 1, xor 2,
+// half-row and row mirrors, then rows (r0 + r1) + (r2 + r3); IEEE addition
+// commutes, so each node is left + right).  Lanes past nblk hold 0 and an
+// all-zero subtree passes its sibling through unchanged, so the tree over
+// the first L = 2^ceil(log2 min(nblk, 64)) leaves gives the same bits.  A
+// binary-counter stack builds exactly that tree.
+__device__ __forceinline__ double tree_sum64(const double *p, int nblk, int stride) {
+    const int nl = nblk < 64 ? nblk : 64;
+    int L = 1;
+    while (L < nl) L <<= 1;
+    double st[7];
+    for (int b = 0; b < L; ++b) {
+        double v = 0.0;
+        for (int j = b; j < nblk; j += 64) v += p[(int64_t)j * stride];
+        int lvl = 0;
+        for (; (b >> lvl) & 1; ++lvl) v = st[lvl] + v;
+        st[lvl] = v;
+    }
+    int top = 0;
+    while ((1 << top) < L) ++top;
+    return st[top];
+}
+
 // k_tr_step_l: the same update with one LANE per sub-int (64 sub-ints per
 // single-wave workgroup, their states in LDS): the serial trust-region update
 // (eigen / secular-equation subproblem, a few thousand dependent f64
 // operations) of 64 sub-ints runs in one wave's lanes instead of one lane of
-// 64 waves.  The block partials are summed in block order (k_tr_step: a wave
-// reduction; identical for one or two blocks).  The scattering gates at the
+// 64 waves.  The block partials are summed in k_tr_step's order
+// (tree_sum64), so a sub-int's fit does not depend on which of the two
+// kernels its batch size selects.  The scattering gates at the
 // new proposal need a pass over the channels: k_tr_gates, a wave per flagged
 // sub-int, follows.  It pays where there are many narrow sub-ints (C3, 10k
 // x 512 channels: 68.4-70.2 vs 71.3-71.7 ms per step) and not for a few wide
@@ -992,14 +1018,9 @@ __global__ __launch_bounds__(64) void k_tr_step_l(SolveArgs a) {
     const bool act = lane < cnt && S.phase != PH_DONE && !S.mmode;
     if (act) {
         const int nblk = (a.nchan + kPassChans - 1) / kPassChans;
+        const double *ps = a.partials + (int64_t)s * nblk * 21;
         double o[21];
-#pragma unroll
-        for (int i = 0; i < 21; ++i) o[i] = 0.0;
-        for (int b = 0; b < nblk; ++b) {
-            const double *p = a.partials + ((int64_t)s * nblk + b) * 21;
-#pragma unroll
-            for (int i = 0; i < 21; ++i) o[i] += p[i];
-        }
+        for (int i = 0; i < 21; ++i) o[i] = tree_sum64(ps + i, nblk, 21);
         const int cmd = S.newton ? tr_update_newton_n<5>(S, o, a.max_iter) : tr_update<5, BOX>(S, o, a.max_iter);
         S.step_cmd = cmd;
         if (cmd) atomicAdd(a.active, 1u);

@@ -103,14 +103,23 @@ def _stage_host(items, dev):
     for a, off in zip(arrs, offs):
         hb[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
     d = torch.empty(total, dtype=torch.uint8, device=dev)
+    global _STAGE_KERNEL
+    staged = False
     if _STAGE_KERNEL:
         # read by a kernel over PCIe: no copy-engine transfer, so it never
-        # queues behind an archive upload (ppf_copy_from_pinned)
+        # queues behind an archive upload (ppf_copy_from_pinned).  A pinned
+        # buffer the device cannot map (host-registered without the mapped
+        # flag, another allocator) makes the call return an error: then the
+        # copy engine takes this and every later staging of the process
         ctx = _lib.context(dev.index)
-        _lib.check(_lib.load().ppf_copy_from_pinned(
+        rc = _lib.load().ppf_copy_from_pinned(
             ctx, _p(d), ctypes.c_void_p(slot[0].data_ptr()), total,
-            _stream(dev)), ctx)
-    else:
+            _stream(dev))
+        if rc == 0:
+            staged = True
+        else:
+            _STAGE_KERNEL = False
+    if not staged:
         d.copy_(slot[0][:total], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))

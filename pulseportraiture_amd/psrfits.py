@@ -726,32 +726,41 @@ class _Pending(object):
         naux = 4 * (2 * nsc + nsub * nchan)
         with torch.cuda.device(dev):
             buf, slot = _pinned_buffer(dev, nraw + naux)
-            # the next user of this slot waits for this load's upload
+            # the next user of this slot waits for this load's upload; until
+            # the read is submitted, any failure here releases the slot (a
+            # ticket that is never set would block that next load for ever)
             self._ticket = slot[1] = _UploadTicket()
-            host = buf[:nsub * nbytes].view(nsub, nbytes)
-            aux = buf[nraw:nraw + naux].view(torch.float32)
-            a = aux.numpy()
-            a[:nsc] = scl.reshape(-1)
-            a[nsc:2 * nsc] = offs.reshape(-1)
-            a[2 * nsc:] = self.weights.reshape(-1)
-        # the rest of the metadata while the file is open
-        self.tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
-            if f.subint.has("TSUBINT") else np.zeros(nsub)
-        self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
-            if f.subint.has("PAR_ANG") else np.zeros(nsub)
-        self.pred = _PolycoRows(f.polyco) if (
-            tscrunch and f.polyco is not None and f.polyco.nrows) else None
-        del raw
-        self._q = dict(dev=dev, buf=buf, slot=slot, host=host, aux=aux,
-                       nraw=nraw, naux=naux, nsc=nsc, nbytes=nbytes,
-                       elem=elem, pol_mode=pol_mode, rm_baseline=rm_baseline)
-        self._qlock = threading.Lock()
-        self._queued = False
-        # the DATA read runs on the reader threads from here, and the upload
-        # and device work are queued as soon as it completes (on the queueing
-        # thread, in read order); queue() / finish() wait for that
-        self._rfut = _read_master().submit(self._read_then_queue, nbytes,
-                                           host.numpy())
+        try:
+            with torch.cuda.device(dev):
+                host = buf[:nsub * nbytes].view(nsub, nbytes)
+                aux = buf[nraw:nraw + naux].view(torch.float32)
+                a = aux.numpy()
+                a[:nsc] = scl.reshape(-1)
+                a[nsc:2 * nsc] = offs.reshape(-1)
+                a[2 * nsc:] = self.weights.reshape(-1)
+            # the rest of the metadata while the file is open
+            self.tsub = f.subint.column("TSUBINT")[:, 0].astype(float) \
+                if f.subint.has("TSUBINT") else np.zeros(nsub)
+            self.par = f.subint.column("PAR_ANG")[:, 0].astype(float) \
+                if f.subint.has("PAR_ANG") else np.zeros(nsub)
+            self.pred = _PolycoRows(f.polyco) if (
+                tscrunch and f.polyco is not None and f.polyco.nrows) else None
+            del raw
+            self._q = dict(dev=dev, buf=buf, slot=slot, host=host, aux=aux,
+                           nraw=nraw, naux=naux, nsc=nsc, nbytes=nbytes,
+                           elem=elem, pol_mode=pol_mode,
+                           rm_baseline=rm_baseline)
+            self._qlock = threading.Lock()
+            self._queued = False
+            # the DATA read runs on the reader threads from here, and the
+            # upload and device work are queued as soon as it completes (on
+            # the queueing thread, in read order); queue() / finish() wait
+            # for that
+            self._rfut = _read_master().submit(self._read_then_queue, nbytes,
+                                               host.numpy())
+        except BaseException:
+            self._ticket.set(None)
+            raise
         self._m = self._meta()
 
     def _read_then_queue(self, nbytes, dst):

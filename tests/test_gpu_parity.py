@@ -1128,3 +1128,24 @@ def test_lane_trust_region_step_equals_wave_step():
     for key in ("results", "scales", "scale_errs", "channel_snrs",
                 "covariance"):
         np.testing.assert_array_equal(small[key], big[key][:k], err_msg=key)
+
+
+def test_lane_trust_region_step_equals_wave_step_multiblock():
+    """As above with 1024 channels: four 256-channel block partials per
+    sub-int, where a block-order sum and the wave reduction's pairwise tree
+    round differently.  k_tr_step_l adds them in the tree's
+    order, so the big batch equals the small one bitwise."""
+    from pulseportraiture_amd import engine
+    nsub, nchan, nbin = 2048, 1024, 128
+    b, nu_fit, init = _scat_batch(nsub, nchan, nbin, first=991)
+    flags = [1, 1, 0, 1, 1]
+    kw = dict(nu_fits=np.full((nsub, 3), nu_fit), log10_tau=True)
+    big = engine.results_numpy(engine.fit_batch(
+        b["data"], b["model"], b["freqs"], b["P"], init, flags, **kw))
+    k = 16
+    small = engine.results_numpy(engine.fit_batch(
+        b["data"][:k], b["model"], b["freqs"], b["P"][:k], init[:k], flags,
+        nu_fits=kw["nu_fits"][:k], log10_tau=True))
+    for key in ("results", "scales", "scale_errs", "channel_snrs",
+                "covariance"):
+        np.testing.assert_array_equal(small[key], big[key][:k], err_msg=key)

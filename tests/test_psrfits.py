@@ -355,3 +355,35 @@ def test_gettoas_tscrunch_psrfits_equals_databunch_path(tmp_path,
         np.testing.assert_array_equal(np.asarray(getattr(fast, key)[0]),
                                       np.asarray(getattr(slow, key)[0]),
                                       err_msg=key)
+
+
+@pytest.mark.gpu
+def test_failed_load_releases_pinned_slot(tmp_path, monkeypatch):
+    """A load that fails after it reserved a pinned slot (here: the read
+    cannot be submitted) releases the slot: the loads after it, which rotate
+    through every slot including the failed one, complete (an
+    unset ticket blocked the next user of the slot for ever)."""
+    import threading
+    fn = _archive(tmp_path)[0]
+
+    class _Refuse(object):
+        def submit(self, *a, **k):
+            raise RuntimeError("read refused")
+
+    real = PF._read_master
+    monkeypatch.setattr(PF, "_read_master", lambda: _Refuse())
+    with pytest.raises(RuntimeError):
+        PF.load_data(fn, pscrunch=True, quiet=True)
+    monkeypatch.setattr(PF, "_read_master", real)
+    done = []
+
+    def good():
+        for _ in range(PF._PIN_SLOTS + 1):
+            d = PF.load_data(fn, pscrunch=True, quiet=True)
+            done.append(d.subints.shape)
+
+    t = threading.Thread(target=good, daemon=True)
+    t.start()
+    t.join(60.0)
+    assert not t.is_alive(), "a load after the failed one blocked"
+    assert len(done) == PF._PIN_SLOTS + 1

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 evidence run: the GPU parity suite, then every bench line with its
+# Evidence run: the GPU parity suite, then every bench line with its
 # CPU baseline and parity sample (C2 headline, single-call latency, C3 and C5
 # with >= 5 timed steps, C4 ppalign, GetTOAs from 16-bit PSRFITS and from
 # float32 archives, phase+DM at the mixed-radix nbin 1000 and 1536).
-# usage: tools/evid_r4.sh TAG [tests|notests]
+# usage: tools/evid.sh TAG [tests|notests]
 tag=${1:-a}
 mode=${2:-tests}
 export TMPDIR=/tmp

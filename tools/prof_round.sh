@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 profiles: tools/prof.sh (kernel stats + FETCH/WRITE + SQ/f64 + TCC
+# Profiles: tools/prof.sh (kernel stats + FETCH/WRITE + SQ/f64 + TCC
 # passes, each its own rocprofv3 run) for the named BASELINE configs.
-# usage: tools/prof_r4.sh TAG c2|c3|c5|c4 ...
+# usage: tools/prof_round.sh TAG c2|c3|c5|c4 ...
 tag=${1:-a}; shift
 for c in "$@"; do
   case $c in
@@ -10,6 +10,6 @@ for c in "$@"; do
     c5) a="--fit scat --nchan 16384 --nbin 1024 --nsub 500";;
     c4) a="--fit align --nsub 1000 --nchan 256 --nbin 1024";;
   esac
-  bash tools/prof.sh r4${tag}_$c $a || exit 1
-  echo "$c done" >> gpurun_out/prof_r4${tag}_status.txt
+  bash tools/prof.sh ${tag}_$c $a || exit 1
+  echo "$c done" >> gpurun_out/prof_${tag}_status.txt
 done

@@ -4,7 +4,7 @@ ARCH ?= gfx950
 CSRC := pulseportraiture_amd/csrc
 OUT := pulseportraiture_amd/lib/libppfit.so
 SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_xspec.hip $(CSRC)/ppf_solve.hip $(CSRC)/ppf_psrfits.hip $(CSRC)/ppf_api.cpp $(CSRC)/ppf_io.cpp
-HDRS := $(CSRC)/ppf_device.hpp $(CSRC)/ppf_state.hpp $(CSRC)/ppf_wfft.hpp $(CSRC)/ppf_internal.hpp include/ppfit.h
+HDRS := $(CSRC)/ppf_device.hpp $(CSRC)/ppf_state.hpp $(CSRC)/ppf_wfft.hpp $(CSRC)/ppf_wfft2.hpp $(CSRC)/ppf_internal.hpp include/ppfit.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed \
             -ffp-contract=fast -munsafe-fp-atomics
 

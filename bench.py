@@ -880,6 +880,11 @@ def main():
     phist = np.zeros((ncalls, 2))
     pgot = lib.ppf_pass_ms_history(ctx, ncalls, phist.ctypes.data)
     pass_ms, pass_launches = phist[:pgot].sum(axis=0)
+    # solver kernels: [k_tr_mom ms, launches, k_tr_step ms, launches,
+    # k_postfit ms, launches] summed over the calls
+    shist = np.zeros((ncalls, 6))
+    sgot = lib.ppf_solver_ms_history(ctx, ncalls, shist.ctypes.data)
+    solv_ms = shist[:max(sgot, 0)].sum(axis=0)
     res_np = last.cpu().numpy()
     I = _lib.RESULT_INDEX
     nfev = res_np[:, I["nfeval"]]
@@ -1022,6 +1027,58 @@ def main():
                 roof["issue_floor_ms"] = fp64["issue_floor_ms"]
                 roof["issue_floor_frac"] = fp64["issue_floor_frac"]
                 roof["valu_active_per_wave"] = fk.get("valu_active_per_wave")
+    # fp64 utilisation of the SOLVER (north star: "fp64 VALU utilisation for
+    # the solver"): the trust-region kernels of the fit mode, their f64
+    # flops per unit from the same SQ counter passes (fp64_summary.json) x
+    # the units of the timed calls / their HIP-event time.  Moment path
+    # (phase+DM, align): k_tr_mom (every iteration of every fit from the
+    # moments) + k_moments (the moment sets; for the fused path k_xmom_g
+    # carries them and is priced above); scattering path: k_pass (the
+    # objective / gradient / Hessian sums of every evaluation) + k_tr_step.
+    # k_postfit (covariance, zero-covariance roots) is listed for both.
+    solver = None
+    if os.path.exists(fpath) and not args.no_hcut:
+        fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
+        fk = fm.get("kernels", {}) if _same_shape(fm) else {}
+        parts = []
+        if scat_fit:
+            parts.append(("pass", "k_pass<true>", pass_ms,
+                          steps_subints * mean_passes, pass_launches))
+            parts.append(("tr_step", "k_tr_step", solv_ms[2], None, solv_ms[3]))
+        else:
+            parts.append(("tr_mom", "k_tr_mom", solv_ms[0], None, solv_ms[1]))
+            if "moments" in kern:
+                parts.append(("moments", "k_moments", kern["moments"]["ms"],
+                              steps_subints, ncalls))
+        parts.append(("postfit", "k_postfit", solv_ms[4], steps_subints,
+                      solv_ms[5]))
+        items = {}
+        tot_fl = tot_ms = 0.0
+        for key, name, ms, units, nl in parts:
+            k = fk.get(key)
+            it = dict(name=name, total_ms=round(float(ms), 3),
+                      launches=int(nl))
+            if k is not None and ms > 0:
+                # units: sub-ints (or sub-int evaluations); k_tr_mom and
+                # k_tr_step count per launch in the SQ pass's units, so
+                # their units follow from the profiled run's ratio
+                if units is None:
+                    units = k["units"] / max(k["dispatches"], 1) * nl
+                fl = k["flops_per_unit"] * units
+                tf = fl / (ms / 1e3) / 1e12
+                it.update(flops_per_unit=round(k["flops_per_unit"]),
+                          achieved_tflops=round(tf, 3),
+                          frac=round(tf / FP64_PEAK_TF, 4),
+                          valu_active_per_wave=k.get("valu_active_per_wave"))
+                tot_fl += fl
+                tot_ms += ms
+            items[key] = it
+        solver = dict(bound="fp64", peak=FP64_PEAK_TF, unit="TFLOP/s",
+                      achieved=round(tot_fl / max(tot_ms, 1e-9) / 1e9, 3)
+                      if tot_ms else None,
+                      frac=round(tot_fl / max(tot_ms, 1e-9) / 1e9 /
+                                 FP64_PEAK_TF, 4) if tot_ms else None,
+                      kernels=items, source=os.path.relpath(fpath, ROOT))
     names = ["model_rfft", "xspec", "guess", "solve"]
     stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
     kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),
@@ -1060,7 +1117,8 @@ def main():
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
                            parallelism="dp%d" % world),
-               roofline=roof, fp64_roofline=fp64, stage_ms=stages, kernels=kernels,
+               roofline=roof, fp64_roofline=fp64, solver_fp64=solver,
+               stage_ms=stages, kernels=kernels,
                # algorithmic HBM bytes of the priced kernels per fit (the
                # guess pass, the spectrum / moment pass and, for scattering
                # fits, every streaming evaluation)

@@ -41,7 +41,8 @@ extern "C" {
 /* ABI 4 (round 5): the options PPF_OPT_MOM_X / PPF_OPT_FUSED_MOM, elem = 3
  * of ppf_unpack_psrfits_batch, PPF_EIO, ppf_read_rows and
  * ppf_copy_from_pinned (added in round 4 without a bump), and
- * ppf_kernel_ms_history slot 0 = the first moment pass of either kind. */
+ * ppf_kernel_ms_history slot 0 = the first moment pass of either kind;
+ * ppf_solver_ms_history, ppf_host_copy. */
 #define PPF_ABI_VERSION 4
 
 enum ppf_error {
@@ -250,6 +251,12 @@ int ppf_kernel_ms_history(ppf_ctx *ctx, int n, double *ms);
  * into ms[n][2]: [0] their summed duration in ms (HIP events around each
  * launch), [1] the number of launches. */
 int ppf_pass_ms_history(ppf_ctx *ctx, int n, double *ms);
+/* The solver kernels of the last n profiled ppf_fit_batch calls into
+ * ms[n][6] (ABI 4): summed ms and launch count of k_tr_mom (the moment-path
+ * trust-region iterations), of k_tr_step (+ k_tr_gates; the scattering
+ * path's update), and of k_postfit (zero-covariance frequencies, output
+ * transform, covariance, scales), each launch bracketed by HIP events. */
+int ppf_solver_ms_history(ppf_ctx *ctx, int n, double *ms);
 
 /* Workspace needed by ppf_fit_batch for `desc` (only sizes/flags are read). */
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc);
@@ -381,6 +388,13 @@ int ppf_copy_from_pinned(ppf_ctx *ctx, void *dst, const void *src, int64_t nbyte
  * read failed or hit end of file). */
 int ppf_read_rows(int32_t fd, int64_t offset, int64_t row_stride, int64_t nbytes,
                   int64_t nrows, void *dst, int64_t dst_stride, int32_t nthreads);
+
+/* Parallel host memcpy (ABI 4): nbytes from src to dst in 4-MiB pieces taken
+ * in turn by nthreads threads (1..64).  GetTOAs stages in-memory archives
+ * (pageable numpy rows) into its page-locked upload buffers with it
+ * (pptoas._Stager; the reference hands the rows to fit_portrait_full
+ * directly, pptoas.py:530-533).  Host memory only: PPF_OK or PPF_EINVAL. */
+int ppf_host_copy(void *dst, const void *src, int64_t nbytes, int32_t nthreads);
 
 /* Gaussian-component model portraits: pplib.gen_gaussian_portrait
  * (pplib.py:886-963, join_ichans = []) as called by pplib.read_model

@@ -125,6 +125,8 @@ SIGNATURES = {
     "ppf_read_rows": (ctypes.c_int, [_i32, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int64, ctypes.c_int64, _vp,
                                      ctypes.c_int64, _i32]),
+    "ppf_solver_ms_history": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+    "ppf_host_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _i32]),
     "ppf_poly_real_roots_host": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
     "ppf_tr_subproblem_host": (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                               ctypes.c_double, _vp]),

@@ -35,6 +35,11 @@ struct ppf_ctx {
     // the pool grown on demand and reused by the ring slot
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pass_ev[kRing];
     int npass[kRing] = {};
+    // the solver kernels of a call (kind 0 k_tr_mom, 1 k_tr_step (+ gates),
+    // 2 k_postfit): (start, end) pairs, as pass_ev
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> solv_ev[kRing];
+    std::vector<int> solv_kind[kRing];
+    int nsolv[kRing] = {};
     long ncalls = 0;
     unsigned *host_active = nullptr;   // pinned, for the iteration loop
 };
@@ -315,6 +320,30 @@ int ppf_pass_ms_history(ppf_ctx *ctx, int n, double *ms) {
     return n;
 }
 
+int ppf_solver_ms_history(ppf_ctx *ctx, int n, double *ms) {
+    if (!ctx || !ms || n < 0) return PPF_EINVAL;
+    if (!ctx->prof) return fail(ctx, PPF_EINVAL, "profiling is off");
+    long avail = ctx->ncalls < ppf_ctx::kRing ? ctx->ncalls : ppf_ctx::kRing;
+    if (n > avail) n = (int)avail;
+    for (int c = 0; c < n; ++c) {
+        int slot = (int)((ctx->ncalls - n + c) % ppf_ctx::kRing);
+        double *o = ms + c * 6;
+        for (int i = 0; i < 6; ++i) o[i] = 0.0;
+        for (int i = 0; i < ctx->nsolv[slot]; ++i) {
+            const auto &pr = ctx->solv_ev[slot][i];
+            hipError_t e = hipEventSynchronize(pr.second);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+            float t = 0.f;
+            e = hipEventElapsedTime(&t, pr.first, pr.second);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipEventElapsedTime");
+            const int k = ctx->solv_kind[slot][i];
+            o[2 * k] += (double)t;
+            o[2 * k + 1] += 1.0;
+        }
+    }
+    return n;
+}
+
 int ppf_last_stage_ms(ppf_ctx *ctx, double *ms4) {
     int n = ppf_stage_ms_history(ctx, 1, ms4);
     if (n < 0) return n;
@@ -357,6 +386,27 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     };
     for (int i = 0; i < 4; ++i) ctx->ran[slot][i] = true;
     ctx->npass[slot] = 0;
+    ctx->nsolv[slot] = 0;
+    // events around one solver launch (profiling only)
+    auto solv_begin = [&](int kind) -> std::pair<hipEvent_t, hipEvent_t> * {
+        if (!ctx->prof) return nullptr;
+        auto &v = ctx->solv_ev[slot];
+        auto &kv = ctx->solv_kind[slot];
+        if ((int)v.size() <= ctx->nsolv[slot]) {
+            std::pair<hipEvent_t, hipEvent_t> pr{};
+            if (hipEventCreate(&pr.first) != hipSuccess || hipEventCreate(&pr.second) != hipSuccess)
+                return nullptr;
+            v.push_back(pr);
+            kv.push_back(0);
+        }
+        kv[ctx->nsolv[slot]] = kind;
+        auto *pe = &v[ctx->nsolv[slot]++];
+        (void)hipEventRecord(pe->first, st);
+        return pe;
+    };
+    auto solv_end = [&](std::pair<hipEvent_t, hipEvent_t> *pe) {
+        if (pe) (void)hipEventRecord(pe->second, st);
+    };
     ctx->ran[slot][2] = d->guess != 0;
     ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
@@ -587,10 +637,16 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             }
             if ((e = hipMemsetAsync(sa.active, 0, 2 * sizeof(unsigned), st)) != hipSuccess)
                 return hip_fail(ctx, e, "hipMemsetAsync");
-            if (any_pass && (e = ppf::launch_tr_step(sa, st)) != hipSuccess)
-                return hip_fail(ctx, e, "k_tr_step");
-            if (sa.moments && any_mom && (e = ppf::launch_tr_mom(sa, st)) != hipSuccess)
-                return hip_fail(ctx, e, "k_tr_mom");
+            if (any_pass) {
+                auto *pe = solv_begin(1);
+                if ((e = ppf::launch_tr_step(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_step");
+                solv_end(pe);
+            }
+            if (sa.moments && any_mom) {
+                auto *pe = solv_begin(0);
+                if ((e = ppf::launch_tr_mom(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_mom");
+                solv_end(pe);
+            }
         }
         iter += group;
         if ((e = hipMemcpyAsync(ctx->host_active, sa.active, sizeof(unsigned), hipMemcpyDeviceToHost,
@@ -599,7 +655,11 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
         if (*ctx->host_active == 0 || iter > maxiter + 2) break;
     }
-    if ((e = ppf::launch_postfit(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_postfit");
+    {
+        auto *pe = solv_begin(2);
+        if ((e = ppf::launch_postfit(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_postfit");
+        solv_end(pe);
+    }
     mark(4);
     if (ctx->prof) ++ctx->ncalls;
     return PPF_OK;

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <cstring>
 #include <system_error>
 #include <thread>
 #include <vector>
@@ -59,4 +60,35 @@ extern "C" int ppf_read_rows(int32_t fd, int64_t offset, int64_t row_stride, int
     work();
     for (auto &th : pool) th.join();
     return failed.load() ? PPF_EIO : PPF_OK;
+}
+
+// Parallel host memcpy (the pageable -> page-locked staging copy of
+// GetTOAs' in-memory archives, pptoas._Stager): nbytes from src to dst in
+// 4-MiB pieces taken in turn by nthreads threads (1..64), outside the
+// interpreter lock.  Host memory only; no device, no context.
+extern "C" int ppf_host_copy(void *dst, const void *src, int64_t nbytes, int32_t nthreads) {
+    if (nbytes < 0 || (nbytes > 0 && (!dst || !src)) || nthreads < 1 || nthreads > 64)
+        return PPF_EINVAL;
+    if (nbytes == 0) return PPF_OK;
+    const int64_t piece = 4ll << 20;
+    const int64_t npieces = (nbytes + piece - 1) / piece;
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int64_t i = next.fetch_add(1, std::memory_order_relaxed);
+            if (i >= npieces) return;
+            const int64_t b0 = i * piece, b1 = std::min(nbytes, b0 + piece);
+            std::memcpy((char *)dst + b0, (const char *)src + b0, (size_t)(b1 - b0));
+        }
+    };
+    const int nt = (int)std::min<int64_t>(nthreads, npieces);
+    std::vector<std::thread> pool;
+    try {
+        pool.reserve(nt > 0 ? nt - 1 : 0);
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    } catch (const std::exception &) {
+    }
+    work();
+    for (auto &th : pool) th.join();
+    return PPF_OK;
 }

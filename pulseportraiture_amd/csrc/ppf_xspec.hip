@@ -39,6 +39,7 @@
 #include "ppf_internal.hpp"
 #include "ppf_state.hpp"
 #include "ppf_wfft.hpp"
+#include "ppf_wfft2.hpp"
 
 namespace ppf {
 
@@ -975,10 +976,302 @@ __global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan
 }
 
 // ===========================================================================
+// k_xspec_w2: k_xspec_w for 1024-point rows (2048 bins) on the one-exchange
+// wave FFT of ppf_wfft2.hpp (round 5).  Same outputs and the same
+// workgroup structure (4 waves, a round of 4 channel rows, X written
+// harmonic-major after a barrier), but per row:
+//   - one LDS exchange inside the FFT instead of three, no natural-order
+//     write-back: the real post-pass takes each pair (Z_k, Z_{N-k}) from
+//     registers after a v_permlane32_swap (wf2::pairs);
+//   - each lane's slot i holds the harmonics k = kA + 64 i and N - k; the
+//     lower one (< N/2) is what X and the guess need below their cutoffs,
+//     so one model load, one D conj(M) and one LDS store per slot (two only
+//     when the group's cutoff passes N/2);
+//   - the X staging slots are k + k/64 (k <= N): no special Nyquist slot.
+// get_noise_PS (pplib.py:2312-2332), Sd, S(tau = 0) and X = D conj(M) /
+// sigma~^2 (pptoaslib.py:1014-1031) as k_xspec_w; the fused GetTOAs guess
+// (GS, pptoas.py:461-464) as k_xspec_w, its terms in the slots of N - k.
+// PPF_XSPEC2=0 (environment) selects k_xspec_w instead.
+// ===========================================================================
+constexpr int kX2W = 4;                                   // waves per workgroup
+constexpr int kX2SL = wf2::kXSlots + wf2::kSpSlots;       // 1072 slots per wave
+constexpr int kX2IE = 1041;                               // the row's 1/errs_FT^2 (.x)
+__device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 1024 -> <= 1040
+#ifndef PPF_X2_MD
+#define PPF_X2_MD 4
+#endif
+#ifndef PPF_XSPEC2
+#define PPF_XSPEC2 1
+#endif
+
+template <int DT, bool GS>
+__global__ __launch_bounds__(64 * kX2W) __attribute__((amdgpu_waves_per_eu(2)))
+void k_xspec_w2(XspecArgs a) {
+    constexpr int N = 1024, NH = N + 1;
+    constexpr int MD = PPF_X2_MD;
+    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *buf = lds + wave * kX2SL;
+
+    int s, cb;
+    block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
+    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
+    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
+    const int nround = (a.cb + kX2W - 1) / kX2W;
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double sqrtN = sqrt((double)N);
+    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
+    const wf2::Seeds sd = wf2::make_seeds(lane0);
+    // post-pass twiddle e^{-i pi k / N} of the lane's first pair, step
+    // e^{-i pi 64 / N}
+    double2 wA0, wstep;
+    {
+        double sn, cs;
+        sincospi(-(double)wf2::pair_k0(lane0) / (double)N, &sn, &cs);
+        wA0 = cmk(cs, sn);
+        sincospi(-64.0 / (double)N, &sn, &cs);
+        wstep = cmk(cs, sn);
+    }
+    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
+    int kw = NH;
+    if (a.KC) {
+        const int nn = (cbase & ~63) + lane0;
+        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
+    }
+    const int mlane = (cbase + lane0 < cend && (!mask || mask[cbase + lane0])) ? 1 : 0;
+    auto usable = [&](int n) {
+        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
+    };
+    constexpr int NL = 64 * guess_npl(10);
+    bool gon = false;
+    double g_Dg = 0.0, g_nrm2 = 0.0, g_w2e2 = 0.0;
+    auto g_wn = [&](int nn) {
+        return a.guess_weights[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
+    };
+    auto g_dgn = [&](int nn) {
+        const double f = a.freqs[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
+        return g_Dg * (1.0 / (f * f) - g_nrm2);
+    };
+    double2 *gacc = lds + kX2W * kX2SL;
+    if constexpr (GS) {
+        gon = a.gflag[s] != 0;                         // uniform
+        if (gon) {
+            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) gacc[t] = cmk(0.0, 0.0);
+            const double *fr = a.freqs + (int64_t)s * a.nchan;
+            double v0 = 0.0, v1 = 0.0;
+            for (int nn = lane0; nn < a.nchan; nn += 64)
+                if (!mask || mask[nn]) { v0 += fr[nn]; v1 += 1.0; }
+            v0 = wave_sum(v0);
+            v1 = wave_sum(v1);
+            const double mu = v0 / v1;
+            double nu_ref_m2 = 1.0 / (mu * mu);
+            if (a.guess_ref) {
+                const double nf = a.nu_fits[(int64_t)s * 3];
+                if (nf == nf) nu_ref_m2 = 1.0 / (nf * nf);
+            }
+            g_Dg = readlane_d(kDconst * a.guess_DM[s] / a.P[s], 0);
+            g_nrm2 = readlane_d(nu_ref_m2, 0);
+            __syncthreads();
+        }
+    }
+    RowT zr[16];
+    auto fetch = [&](int n) {
+        const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) zr[q] = src[lane0 + 64 * q];
+    };
+    int n = cbase + wave;
+    if (usable(n)) fetch(n);
+    for (int r = 0; r < nround; ++r, n += kX2W) {
+        const bool live = usable(n);
+        if (n < cend && !live) {
+            if (lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
+            if (usable(n + kX2W)) fetch(n + kX2W);
+        }
+        if (live) {
+            const int64_t crow = (int64_t)s * a.nchan + n;
+            double2 x[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+            if (usable(n + kX2W)) fetch(n + kX2W);      // next row in flight during this FFT
+            // per-lane indices re-derived every row from an opaque lane
+            // (hoisted out of the round loop they would hold VGPRs for good)
+            int lane = lane0;
+            asm volatile("" : "+v"(lane));
+            wf2::fft1024(x, buf, lane, sd);
+            double2 zm = cmk(0.0, 0.0);
+            wf2::pairs(x, buf + wf2::kXSlots, lane, zm);
+            // slot i: harmonics k = kA + 64 i and N - k; hl = the lower one
+            // (lanes <= 32: k, the others: N - k), D of it in Dl
+            const bool lo = lane <= 32;
+            const int kA = wf2::pair_k0(lane);
+            const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            // guess phasor w_n e^{2 pi i hl dphi}, step e^{+-2 pi i 64 dphi}
+            double2 El = cmk(0.0, 0.0), Est = El;
+            if (GS && gon) {
+                const double dg = g_dgn(n);
+                const double2 E1 = cexp2pi((double)hl0 * dg);
+                El = cscale(E1, g_wn(n));
+                const double2 e1 = cexp2pi(dg);
+                Est = e1;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
+                if (!lo) Est = cconj(Est);
+            }
+            // the first MD slots' model values, loaded now (the FFT is done)
+            double2 Mq[MD > 0 ? MD : 1];
+#pragma unroll
+            for (int i = 0; i < MD; ++i) {
+                const int h = hl0 + hstep * i;
+                Mq[i] = h < kw ? Mrow[h] : cmk(0.0, 0.0);
+            }
+            double pn = 0.0, pd = 0.0;
+            double2 w = wA0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = kA + 64 * i, kh = N - k;
+                double2 Dlo, Dhi;
+                {
+                    const double2 zk = x[i], zn = x[i + 8];
+                    const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+                    const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
+                    const double2 wo = cmul(w, o);
+                    Dlo = cmk(e.x + wo.y, e.y - wo.x);
+                    Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
+                }
+                w = cmul(w, wstep);
+                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
+                if (k >= a.kc) pn += p0;
+                if (kh >= a.kc) pn += p1;
+                if (k >= 1) pd += p0;
+                pd += p1;
+                const int hl = hl0 + hstep * i;
+                const double2 Dl = lo ? Dlo : Dhi;
+                double2 Ml;
+                if constexpr (MD > 0) {
+                    Ml = Mq[i % MD];
+                    if (i + MD < 8) {
+                        const int h2 = hl + hstep * MD;
+                        Mq[i % MD] = h2 < kw ? Mrow[h2] : cmk(0.0, 0.0);
+                    }
+                } else {
+                    Ml = hl < kw ? Mrow[hl] : cmk(0.0, 0.0);
+                }
+                // unscaled X of the low harmonic (the write-out applies
+                // 1/sigma~^2); k = 0 zeroed (F0_fact = 0)
+                if (hl < kw) buf[x2slot(hl)] = hl == 0 ? cmk(0.0, 0.0) : cmulc(Dl, Ml);
+                if (GS && gon) {
+                    // the row's guess term of harmonic hl, in the slot of
+                    // N - hl (past X's cutoff: kw <= NL < N/2)
+                    if (hl >= 1 && hl < NL) buf[x2slot(N - hl)] = cmul(Dl, El);
+                    El = cmul(El, Est);
+                } else if (kw > N / 2) {
+                    // the group's cutoff passes N/2: the high harmonic too
+                    const int hh = N - hl;
+                    if (hh < kw) buf[x2slot(hh)] = cmulc(lo ? Dhi : Dlo, Mrow[hh]);
+                }
+            }
+            if (lane == 0) {
+                const double2 Dm = cmk(zm.x, -zm.y);              // D_{N/2}
+                const double p = cabs2(Dm);
+                if (N / 2 >= a.kc) pn += p;
+                pd += p;
+                if (N / 2 < kw) buf[x2slot(N / 2)] = cmulc(Dm, Mrow[N / 2]);
+            }
+            pn = wave_sum(pn);
+            pd = wave_sum(pd);
+            double errs_FT;
+            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+            if (GS && gon) {
+                const double wn = g_wn(n);
+                g_w2e2 += wn * wn * errs_FT * errs_FT;
+            }
+            if (lane == 0) {
+                reinterpret_cast<double *>(buf + kX2IE)[0] = inv_e2;   // for the write-out
+                double *chan = a.chan + crow * 4;
+                chan[0] = errs_FT;
+                chan[1] = inv_e2;
+                chan[2] = pd * inv_e2;                                  // Sd_n
+                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+            }
+        }
+        __syncthreads();
+        // write-out: thread t -> channel c = t % 4 of the round, harmonics
+        // k = t / 4 + 64 j
+        {
+            const int c = threadIdx.x % kX2W, n0 = cbase + r * kX2W;
+            const int nc = n0 + c;
+            if (nc < cend) {
+                const bool ok = !mask || mask[nc];
+                const double2 *b = lds + c * kX2SL;
+                const double ie2 = ok ? reinterpret_cast<const double *>(b + kX2IE)[0] : 0.0;
+                for (int k = threadIdx.x / kX2W; k < kw; k += 64)
+                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[x2slot(k)], ie2) : cmk(0.0, 0.0);
+            }
+        }
+        if (GS && gon) {
+            // the round's rows' guess terms, in wave order
+            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) {
+                if (t == 0) continue;
+                double2 acc = gacc[t];
+#pragma unroll
+                for (int w2 = 0; w2 < kX2W; ++w2)
+                    if (usable(cbase + r * kX2W + w2)) acc = cadd(acc, lds[w2 * kX2SL + x2slot(N - t)]);
+                gacc[t] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (GS) {
+        if (gon) {
+            double2 *gp = a.gpart + ((int64_t)s * a.nblk + cb) * NL;
+            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) gp[t] = gacc[t];
+            const double gwl = mlane ? a.guess_weights[(int64_t)s * a.nchan + cbase + lane0] : 0.0;
+            const double wsum = wave_sum(gwl), cnt = wave_sum(mlane ? 1.0 : 0.0);
+            if (lane0 == 0) reinterpret_cast<double *>(buf)[0] = g_w2e2;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double acc = 0.0;
+                for (int w2 = 0; w2 < kX2W; ++w2) acc += reinterpret_cast<const double *>(lds + w2 * kX2SL)[0];
+                double *o = a.gw + ((int64_t)s * a.nblk + cb) * 3;
+                o[0] = wsum;
+                o[1] = cnt;
+                o[2] = acc;
+            }
+        }
+    }
+}
+
+// k_xspec_w2 at 1024 points unless PPF_XSPEC2=0 (environment, read once)
+static bool use_xspec2() {
+    static const bool on = [] {
+        const char *e = getenv("PPF_XSPEC2");
+        return e ? atoi(e) != 0 : (PPF_XSPEC2 != 0);
+    }();
+    return on;
+}
+
+// ===========================================================================
 // launchers
 // ===========================================================================
 template <int L2, int DT>
 static void launch_w(const XspecArgs &a, hipStream_t st) {
+    if constexpr (L2 == 10) {
+        if (use_xspec2()) {
+            const size_t lds = (size_t)kX2W * kX2SL * sizeof(double2);
+            dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kX2W);
+            if (a.gflag)
+                hipLaunchKernelGGL((k_xspec_w2<DT, true>), g, b, lds + (size_t)guess_slots(10) * sizeof(double2),
+                                   st, a);
+            else hipLaunchKernelGGL((k_xspec_w2<DT, false>), g, b, lds, st, a);
+            return;
+        }
+    }
     const size_t lds = ((size_t)xsw<L2>() * xspec_slw<L2>() + (PPF_TW_LDS ? tw_slots<L2>() : 0)) *
                        sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * xsw<L2>());

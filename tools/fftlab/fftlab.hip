@@ -80,7 +80,7 @@ __device__ __forceinline__ void post_nat(const double2 *buf, int lane, double2 w
     if (lane == 0) {
         const double2 zm = buf[wfft::pad<10>(N / 2)];
         const double2 Dm = cmk(zm.x, -zm.y);
-        pn += cabs2(Dm);
+        if (N / 2 >= KC) pn += cabs2(Dm);
         pd += cabs2(Dm);
         if (chk) chk[N / 2] = Dm;
     }
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * WG) __attribute__((amdgpu_waves_per_eu(WPE))) 
             }
             if (lane == 0) {
                 const double2 Dm = cmk(zm.x, -zm.y);
-                pn += cabs2(Dm);
+                if (N / 2 >= KC) pn += cabs2(Dm);
                 pd += cabs2(Dm);
                 if (chk) chk[N / 2] = Dm;
             }

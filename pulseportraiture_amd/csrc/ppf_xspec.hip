@@ -1003,6 +1003,12 @@ __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 
 #ifndef PPF_XSPEC2
 #define PPF_XSPEC2 1
 #endif
+#ifndef PPF_X2_MEARLY
+#define PPF_X2_MEARLY 0
+#endif
+#ifndef PPF_X2_LATEPF
+#define PPF_X2_LATEPF 0
+#endif
 
 template <int DT, bool GS>
 __global__ __launch_bounds__(64 * kX2W) __attribute__((amdgpu_waves_per_eu(2)))
@@ -1047,13 +1053,6 @@ void k_xspec_w2(XspecArgs a) {
     constexpr int NL = 64 * guess_npl(10);
     bool gon = false;
     double g_Dg = 0.0, g_nrm2 = 0.0, g_w2e2 = 0.0;
-    auto g_wn = [&](int nn) {
-        return a.guess_weights[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
-    };
-    auto g_dgn = [&](int nn) {
-        const double f = a.freqs[(int64_t)s * a.nchan + __builtin_amdgcn_readfirstlane(nn)];
-        return g_Dg * (1.0 / (f * f) - g_nrm2);
-    };
     double2 *gacc = lds + kX2W * kX2SL;
     if constexpr (GS) {
         gon = a.gflag[s] != 0;                         // uniform
@@ -1076,6 +1075,19 @@ void k_xspec_w2(XspecArgs a) {
             __syncthreads();
         }
     }
+    // the block's per-channel scalars in lane registers (lane l: channel
+    // cbase + l): a global load of them inside the round loop would wait,
+    // vmcnt being in order, for the next row's prefetch
+    const int nl = cbase + lane0;
+    const bool lin = nl < cend;
+    const double ch_mpow = lin ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
+    const double ch_err = (a.errs && lin) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
+    double ch_wn = 0.0, ch_dg = 0.0;
+    if (GS && gon && lin) {
+        ch_wn = a.guess_weights[(int64_t)s * a.nchan + nl];
+        const double f = a.freqs[(int64_t)s * a.nchan + nl];
+        ch_dg = g_Dg * (1.0 / (f * f) - g_nrm2);
+    }
     RowT zr[16];
     auto fetch = [&](int n) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
@@ -1084,6 +1096,7 @@ void k_xspec_w2(XspecArgs a) {
     };
     int n = cbase + wave;
     if (usable(n)) fetch(n);
+    XP_INIT();
     for (int r = 0; r < nround; ++r, n += kX2W) {
         const bool live = usable(n);
         if (n < cend && !live) {
@@ -1095,112 +1108,139 @@ void k_xspec_w2(XspecArgs a) {
             double2 x[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-            if (usable(n + kX2W)) fetch(n + kX2W);      // next row in flight during this FFT
+            const int rr = n - cbase;
             // per-lane indices re-derived every row from an opaque lane
             // (hoisted out of the round loop they would hold VGPRs for good)
             int lane = lane0;
             asm volatile("" : "+v"(lane));
-            wf2::fft1024(x, buf, lane, sd);
-            double2 zm = cmk(0.0, 0.0);
-            wf2::pairs(x, buf + wf2::kXSlots, lane, zm);
             // slot i: harmonics k = kA + 64 i and N - k; hl = the lower one
             // (lanes <= 32: k, the others: N - k), D of it in Dl
             const bool lo = lane <= 32;
             const int kA = wf2::pair_k0(lane);
             const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
             const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            // the first MD slots' model values.  PPF_X2_MEARLY: issued before
+            // the next row's prefetch (so their wait does not include it),
+            // held through the FFT; else after the FFT.  PPF_X2_LATEPF: the
+            // prefetch is issued after the FFT and the model loads.
+            // The loads are unconditional (hl < N/2 is always a valid
+            // index): under a lane-divergent branch the compiler cannot
+            // count the loads in flight and waits for all of them (vmcnt(0),
+            // the next row's prefetch included) at every slot.
+            double2 Mq[MD > 0 ? MD : 1];
+            auto mpre = [&]() {
+#pragma unroll
+                for (int i = 0; i < MD; ++i) Mq[i] = Mrow[hl0 + hstep * i];
+            };
+            if (PPF_X2_MEARLY) mpre();
+            if (!PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
+            XP(0);
+            wf2::fft1024(x, buf, lane, sd);
+            XP(1);
+            if (!PPF_X2_MEARLY) mpre();
+            if (PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);
+            double2 zm = cmk(0.0, 0.0);
+            wf2::pairs(x, buf + wf2::kXSlots, lane, zm);
+            XP(2);
             // guess phasor w_n e^{2 pi i hl dphi}, step e^{+-2 pi i 64 dphi}
             double2 El = cmk(0.0, 0.0), Est = El;
             if (GS && gon) {
-                const double dg = g_dgn(n);
+                const double dg = readlane_d(ch_dg, rr);
                 const double2 E1 = cexp2pi((double)hl0 * dg);
-                El = cscale(E1, g_wn(n));
+                El = cscale(E1, readlane_d(ch_wn, rr));
                 const double2 e1 = cexp2pi(dg);
                 Est = e1;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
                 if (!lo) Est = cconj(Est);
             }
-            // the first MD slots' model values, loaded now (the FFT is done)
-            double2 Mq[MD > 0 ? MD : 1];
-#pragma unroll
-            for (int i = 0; i < MD; ++i) {
-                const int h = hl0 + hstep * i;
-                Mq[i] = h < kw ? Mrow[h] : cmk(0.0, 0.0);
-            }
+            // Per slot (the real-FFT post-pass in doubled form: the 0.5 of
+            // e and o dropped, so Dl = 2 D_hl, v = the other harmonic's 2 D
+            // up to conjugation; every product below is rescaled by an
+            // exact power of two):
+            //   e = Z_k + conj Z_{N-k}, o = Z_k - conj Z_{N-k}, wo = w o
+            //   lanes <= 32 (sg = +1): 2 D_k = (e.x + wo.y, e.y - wo.x)
+            //   the others (sg = -1):  2 D_{N-k} = conj of (e.x - wo.y, e.y + wo.x)
+            // u = e + sg (wo.y, -wo.x): Dl = (u.x, sg u.y) is 2 D_hl; v = e -
+            // sg (...) has |v| = |2 D_{N - hl}|.
+            const double sg = lo ? 1.0 : -1.0;
+            const int hcut = N - a.kc;            // N - hl >= kc  <=>  hl <= hcut
             double pn = 0.0, pd = 0.0;
             double2 w = wA0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int k = kA + 64 * i, kh = N - k;
-                double2 Dlo, Dhi;
-                {
-                    const double2 zk = x[i], zn = x[i + 8];
-                    const double2 e = cmk(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
-                    const double2 o = cmk(0.5 * (zk.x - zn.x), 0.5 * (zk.y + zn.y));
-                    const double2 wo = cmul(w, o);
-                    Dlo = cmk(e.x + wo.y, e.y - wo.x);
-                    Dhi = cmk(e.x - wo.y, -(e.y + wo.x));
-                }
+                const double2 zk = x[i], zn = x[i + 8];
+                const double ex = zk.x + zn.x, ey = zk.y - zn.y;
+                const double ox = zk.x - zn.x, oy = zk.y + zn.y;
+                const double wox = fma(w.x, ox, -w.y * oy), woy = fma(w.x, oy, w.y * ox);
                 w = cmul(w, wstep);
-                const double p0 = cabs2(Dlo), p1 = cabs2(Dhi);
-                if (k >= a.kc) pn += p0;
-                if (kh >= a.kc) pn += p1;
-                if (k >= 1) pd += p0;
-                pd += p1;
+                const double ux = fma(sg, woy, ex), uy = fma(-sg, wox, ey);
+                const double vx = fma(-sg, woy, ex), vy = fma(sg, wox, ey);
+                const double2 Dl = cmk(ux, sg * uy);
+                const double ph = fma(vx, vx, vy * vy), pl = fma(ux, ux, uy * uy);
                 const int hl = hl0 + hstep * i;
-                const double2 Dl = lo ? Dlo : Dhi;
+                if (hl <= hcut) pn += ph;
+                // (lane 0, slot 0: pl = |2 D_0|^2, which Sd leaves out)
+                if (i == 0) pd += lane == 0 ? ph : pl + ph;
+                else pd += pl + ph;
                 double2 Ml;
                 if constexpr (MD > 0) {
                     Ml = Mq[i % MD];
-                    if (i + MD < 8) {
-                        const int h2 = hl + hstep * MD;
-                        Mq[i % MD] = h2 < kw ? Mrow[h2] : cmk(0.0, 0.0);
-                    }
+                    if (i + MD < 8) Mq[i % MD] = Mrow[hl + hstep * MD];
                 } else {
-                    Ml = hl < kw ? Mrow[hl] : cmk(0.0, 0.0);
+                    Ml = Mrow[hl];
                 }
-                // unscaled X of the low harmonic (the write-out applies
-                // 1/sigma~^2); k = 0 zeroed (F0_fact = 0)
+                // 2 x the unscaled X of the low harmonic (the write-out
+                // applies 1/(2 sigma~^2)); k = 0 zeroed (F0_fact = 0)
                 if (hl < kw) buf[x2slot(hl)] = hl == 0 ? cmk(0.0, 0.0) : cmulc(Dl, Ml);
                 if (GS && gon) {
-                    // the row's guess term of harmonic hl, in the slot of
-                    // N - hl (past X's cutoff: kw <= NL < N/2)
+                    // 2 x the row's guess term of harmonic hl, in the slot
+                    // of N - hl (past X's cutoff: kw <= NL < N/2)
                     if (hl >= 1 && hl < NL) buf[x2slot(N - hl)] = cmul(Dl, El);
                     El = cmul(El, Est);
                 } else if (kw > N / 2) {
                     // the group's cutoff passes N/2: the high harmonic too
+                    // (2 D_{N - hl} = (vx, -sg vy))
                     const int hh = N - hl;
-                    if (hh < kw) buf[x2slot(hh)] = cmulc(lo ? Dhi : Dlo, Mrow[hh]);
+                    if (hh < kw) buf[x2slot(hh)] = cmulc(cmk(vx, -sg * vy), Mrow[hh]);
                 }
             }
+            XP(3);
             if (lane == 0) {
-                const double2 Dm = cmk(zm.x, -zm.y);              // D_{N/2}
+                // D_{N/2} (pairs: zm = Z_{N/2}), doubled like the rest
+                const double2 Dm = cmk(2.0 * zm.x, -2.0 * zm.y);
                 const double p = cabs2(Dm);
                 if (N / 2 >= a.kc) pn += p;
                 pd += p;
                 if (N / 2 < kw) buf[x2slot(N / 2)] = cmulc(Dm, Mrow[N / 2]);
             }
+            // the doubled sums: exact factor 4
+            pn *= 0.25;
+            pd *= 0.25;
             pn = wave_sum(pn);
             pd = wave_sum(pd);
             double errs_FT;
-            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            if (a.errs) errs_FT = readlane_d(ch_err, rr) * sqrtN;
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
             if (GS && gon) {
-                const double wn = g_wn(n);
+                const double wn = readlane_d(ch_wn, rr);
                 g_w2e2 += wn * wn * errs_FT * errs_FT;
             }
+            const double mpow = readlane_d(ch_mpow, rr);
             if (lane == 0) {
-                reinterpret_cast<double *>(buf + kX2IE)[0] = inv_e2;   // for the write-out
+                // for the write-out: the staged X are doubled
+                reinterpret_cast<double *>(buf + kX2IE)[0] = 0.5 * inv_e2;
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
                 chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+                chan[3] = mpow * inv_e2;                                // S_n at tau = 0
             }
         }
+        XP(4);
         __syncthreads();
+        XP(5);
         // write-out: thread t -> channel c = t % 4 of the round, harmonics
         // k = t / 4 + 64 j
         {
@@ -1226,11 +1266,17 @@ void k_xspec_w2(XspecArgs a) {
             }
         }
         __syncthreads();
+        XP(6);
+    }
+    {
+        const int lane = lane0;
+        XP_DONE();
     }
     if constexpr (GS) {
         if (gon) {
             double2 *gp = a.gpart + ((int64_t)s * a.nblk + cb) * NL;
-            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) gp[t] = gacc[t];
+            // (the staged guess terms are doubled: exact factor 1/2)
+            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) gp[t] = cscale(gacc[t], 0.5);
             const double gwl = mlane ? a.guess_weights[(int64_t)s * a.nchan + cbase + lane0] : 0.0;
             const double wsum = wave_sum(gwl), cnt = wave_sum(mlane ? 1.0 : 0.0);
             if (lane0 == 0) reinterpret_cast<double *>(buf)[0] = g_w2e2;

@@ -4,7 +4,8 @@
 # same-call comparisons count).  A variant is `lib:PATH` (a libppfit build,
 # e.g. varlib/libppfit_NAME.so from tools/build_variant.sh), `env:K=V[,K=V]`
 # (environment settings) or `base` (the default library and environment).
-# Optionally runs a GPU test subset first (TESTS="-k expr").
+# Optionally runs a GPU test subset first (TESTK="pytest -k expression",
+# TESTK=all: the whole GPU suite).
 #   usage: tools/ab.sh TAG "c2 c3 c5 c4 gtps gt nb1000 nb1536" "base lib:... env:..." [REPS]
 #   out:   gpurun_out/ab_TAG/{CONFIG}_{VARIANT}_{REP}.json, ab_TAG/status.txt
 tag=$1; cfgs=$2; vars=$3; reps=${4:-1}
@@ -12,8 +13,9 @@ export TMPDIR=/tmp
 out=gpurun_out/ab_$tag
 mkdir -p $out
 st=$out/status.txt
-if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread $TESTS > $out/pytest.log 2>&1
+if [ -n "$TESTK" ]; then
+  kx=(); [ "$TESTK" != all ] && kx=(-k "$TESTK")
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread "${kx[@]}" > $out/pytest.log 2>&1
   rc=$?; echo "tests rc=$rc $(tail -1 $out/pytest.log)" >> $st
   [ $rc -eq 0 ] || exit $rc
 fi

@@ -1148,8 +1148,9 @@ void k_xspec_w2(XspecArgs a) {
                 const double dg = readlane_d(ch_dg, rr);
                 const double2 E1 = cexp2pi((double)hl0 * dg);
                 El = cscale(E1, readlane_d(ch_wn, rr));
-                const double2 e1 = cexp2pi(dg);
-                Est = e1;
+                // step e^{2 pi i 64 dphi}: lane 1's phasor (hl0 = 1) squared
+                // six times
+                Est = cmk(readlane_d(E1.x, 1), readlane_d(E1.y, 1));
 #pragma unroll
                 for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
                 if (!lo) Est = cconj(Est);

@@ -940,7 +940,12 @@ def main():
         kern["moments"] = dict(name="k_moments", ms=kern_ms[0], unit=mu,
                                bytes=steps_subints * mu)
     elif scat_fit or momx_used:
-        kern["xspec"] = dict(name="k_xspec_w<%d, 0>" % L2N, ms=stage_ms[1],
+        # 1024-point rows: k_xspec_w2 (the one-exchange wave FFT) unless
+        # PPF_XSPEC2=0 selects k_xspec_w
+        xname = ("k_xspec_w2<0>" if L2N == 10 and
+                 os.environ.get("PPF_XSPEC2", "1") != "0"
+                 else "k_xspec_w<%d, 0>" % L2N)
+        kern["xspec"] = dict(name=xname, ms=stage_ms[1],
                              unit=xspec_unit,
                              bytes=steps_subints * xspec_unit +
                              ncalls * nchan * nharm * 16)

@@ -26,7 +26,7 @@ import json
 import os
 
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
-           "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
+           "xspec": ("k_xspec_w", ""), "pass": ("k_pass<true>", ""),
            "tr_mom": ("k_tr_mom", ""), "postfit": ("k_postfit", ""),
            "moments": ("k_moments", ""), "accum": ("k_align", "")}
 

@@ -28,7 +28,7 @@ import json
 import os
 
 KERNELS = {"xmom": ("k_xmom_g<", ", true>"), "dsum": ("k_dsum_w<", ""),
-           "xspec": ("k_xspec_w<", ""), "pass": ("k_pass<true>", ""),
+           "xspec": ("k_xspec_w", ""), "pass": ("k_pass<true>", ""),
            "moments": ("k_moments", ""), "accum": ("k_align", ""), "noise": ("k_noise_w<", "")}
 
 

@@ -1955,8 +1955,15 @@ hipError_t launch_moments(const SolveArgs &a, hipStream_t st) {
 hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
     // (one wave per sub-int, as k_postfit, measured slower here: C2 solve
     // stage 815 vs 777 ms per 24 calls, C4 305-332k vs 338-339k
-    // archive-iterations/s, tools/g28.sh: the evaluation pass, not the
-    // thread-0 update, is most of a launch)
+    // archive-iterations/s: the evaluation pass, not the thread-0 update,
+    // is most of a launch.  Round 5: a variant with thread = channel and the
+    // moment set resident in registers for the whole launch (no per-
+    // evaluation re-reads) was slower too, C2 224 vs 168 ms of k_tr_mom per
+    // 120 calls, C4 unchanged: with the thread-0 update's registers on top
+    // of 64 resident ones it spills (256 VGPRs + 324 B scratch) and holds
+    // one 512-thread workgroup per CU, so the serial updates no longer
+    // overlap other workgroups' evaluations; capped at three waves per SIMD
+    // it spills 670 B and takes 247 ms)
 #ifdef PPF_TRMOM_TB
     const int tb = PPF_TRMOM_TB;
 #else

@@ -11,6 +11,7 @@ corrections, TOA flags, DeltaDM).  Archive I/O stays on PSRCHIVE via
 Reference: /root/reference/pptoas.py (file:line cited per block).
 """
 import contextlib
+import ctypes
 import gc
 import os
 import sys
@@ -40,6 +41,10 @@ rm_baseline = bool(_pplib.F0_fact)  # pptoas.py:36-39
 # per-sub-int loops, which remain the general path; False forces those)
 FAST_HOST = True
 _SWITCH_MS = float(os.environ.get("PPF_SWITCH_INTERVAL_MS", "0") or 0)
+# threads of the native pageable -> page-locked staging copy of in-memory
+# archives (_Stager; 0: torch's copy_)
+_STAGE_COPY_THREADS = max(0, min(64, int(os.environ.get(
+    "PPF_STAGE_COPY_THREADS", "8"))))
 
 
 def _is_fits(filename):
@@ -198,7 +203,17 @@ class _Stager(object):
             self.bufs[k] = torch.empty(need, dtype=torch.uint8,
                                        pin_memory=True)
         host = self.bufs[k][:need].view(src.dtype).view(src.shape)
-        host.copy_(src)
+        if _STAGE_COPY_THREADS > 0 and src.is_contiguous():
+            # native parallel memcpy outside the interpreter lock
+            # (ppf_host_copy; torch's copy_ reached 30-38 GB/s here, which
+            # bounded float32 archives below the PCIe rate)
+            rc = _lib.load().ppf_host_copy(
+                ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                need, _STAGE_COPY_THREADS)
+            if rc != 0:
+                raise RuntimeError("ppf_host_copy failed (%d)" % rc)
+        else:
+            host.copy_(src)
         with torch.cuda.device(dev):
             if self.stream is None:
                 self.stream = torch.cuda.Stream(dev)

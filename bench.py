@@ -932,9 +932,14 @@ def main():
     # pass, which writes every harmonic of X, and k_moments
     wave = (nbin & (nbin - 1)) == 0 and 256 <= nbin <= 2048
     if not wave and not scat_fit:
-        xfull = nchan * nbin * 4 + nchan * nharm * 16 + 4 * nchan * 8
-        kern["xspec"] = dict(name="k_xspec (block FFT)", ms=stage_ms[1],
-                             unit=xfull, bytes=steps_subints * xfull +
+        # nbin / 2 not a power of two, <= 1024: the wave-per-row mixed-radix
+        # pass k_xspec_wm, which writes X below the cutoffs (like
+        # k_xspec_w); longer rows: the block-FFT k_xspec, every harmonic
+        wm = nbin // 2 <= 1024 and (nbin & (nbin - 1)) != 0
+        xfull = nchan * nbin * 4 + (xh if wm else nchan * nharm) * 16 + 4 * nchan * 8
+        kern["xspec"] = dict(name="k_xspec_wm" if wm else "k_xspec (block FFT)",
+                             ms=stage_ms[1], unit=xfull,
+                             bytes=steps_subints * xfull +
                              ncalls * nchan * nharm * 16)
         mu = xh * 16 + nchan * 16 + nchan * (32 * 16 + 8)
         kern["moments"] = dict(name="k_moments", ms=kern_ms[0], unit=mu,
@@ -988,8 +993,11 @@ def main():
 
     def _same_shape(m):
         return shape_tag in str((m.get("source") or {}).get("bench", ""))
+    # summary entry: the fit mode, or "mode@nbin" for non-power-of-two nbin
+    # (profiles/pmc_reduce.py, fp64_reduce.py)
+    mkey = args.fit if nbin & (nbin - 1) == 0 else "%s@%d" % (args.fit, nbin)
     if os.path.exists(args.pmc) and not args.no_hcut:
-        pm = json.load(open(args.pmc)).get("modes", {}).get(args.fit, {})
+        pm = json.load(open(args.pmc)).get("modes", {}).get(mkey, {})
         pk = pm.get("kernels", {}).get(dom) if _same_shape(pm) else None
         if pk:
             traffic = round(pk["hbm_bytes"] * units_launch)
@@ -1007,7 +1015,7 @@ def main():
     fp64 = None
     fpath = os.path.join(ROOT, "profiles", "fp64_summary.json")
     if os.path.exists(fpath) and not args.no_hcut:
-        fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
+        fm = json.load(open(fpath)).get("modes", {}).get(mkey, {})
         fk = fm.get("kernels", {}).get(dom) if _same_shape(fm) else None
         if fk:
             tf = fk["flops_per_unit"] * units_launch / (dk["ms"] / nlaunch / 1e3) / 1e12
@@ -1043,7 +1051,7 @@ def main():
     # k_postfit (covariance, zero-covariance roots) is listed for both.
     solver = None
     if os.path.exists(fpath) and not args.no_hcut:
-        fm = json.load(open(fpath)).get("modes", {}).get(args.fit, {})
+        fm = json.load(open(fpath)).get("modes", {}).get(mkey, {})
         fk = fm.get("kernels", {}) if _same_shape(fm) else {}
         parts = []
         if scat_fit:
@@ -1118,6 +1126,8 @@ def main():
                            moments="cross spectrum (k_xspec_w + k_moments)"
                            if momx_used and wave else (
                                "fused pass (k_xmom_g)" if wave else
+                               "cross spectrum (k_xspec_wm + k_moments)"
+                               if nbin // 2 <= 1024 and (nbin & (nbin - 1)) else
                                "cross spectrum (block FFT + k_moments)"),
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],

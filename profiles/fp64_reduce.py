@@ -95,7 +95,9 @@ def main():
             # GRBM_GUI_ACTIVE rows sum the 8 XCDs
             e["clock_ghz"] = v["GRBM_GUI_ACTIVE"] / rows / 8.0 / (sum(dn) / len(dn))
         ent["kernels"][key] = e
-    out["modes"][cfg["fit"]] = ent
+    # (non-power-of-two nbin: its own entry, e.g. "phase+DM@1000")
+    nb = cfg.get("nbin", 2048)
+    out["modes"][cfg["fit"] if nb & (nb - 1) == 0 else "%s@%d" % (cfg["fit"], nb)] = ent
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(ent, indent=1))
 

@@ -51,7 +51,9 @@ def main():
             if ln.startswith("{")][-1]
     bench = json.loads(line)
     cfg = bench["config"]
-    mode = cfg["fit"]
+    # (non-power-of-two nbin: its own entry, e.g. "phase+DM@1000")
+    nb = cfg.get("nbin", 2048)
+    mode = cfg["fit"] if nb & (nb - 1) == 0 else "%s@%d" % (cfg["fit"], nb)
     calls = bench["steps"] + bench["warmup"]
     per_launch = min(cfg.get("chunk", cfg["nsub_per_gpu"]), cfg["nsub_per_gpu"])
     fr = load(os.path.join(a.prof_dir, "fetch"))

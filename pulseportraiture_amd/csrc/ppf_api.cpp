@@ -67,9 +67,9 @@ bool pow2_in_range(int nbin) {
     return nbin >= 32 && nbin <= 8192 && (nbin & (nbin - 1)) == 0;
 }
 
-// nbin the FFT kernels take: even, 32..8192, nbin / 2 = 2^a 3^b 5^c 7^d
-// (power-of-two nbin on the register / radix-4 paths, the others on the
-// mixed-radix LDS FFT)
+// nbin the FFT kernels take: even, 32..8192 (power-of-two nbin on the
+// register / radix-4 paths, the others on the mixed-radix LDS FFT, whose
+// generic-radix stage takes prime factors of nbin / 2 above 7)
 bool nbin_supported(int nbin) {
     return nbin >= 32 && nbin <= 8192 && (nbin & 1) == 0 && ppf::fft_len_supported(nbin / 2);
 }
@@ -184,7 +184,7 @@ int check_fit_desc(ppf_ctx *ctx, const ppf_fit_desc *d) {
     if (d->nsub < 1 || d->nchan < 1) return fail(ctx, PPF_EINVAL, "nsub=%d nchan=%d", d->nsub, d->nchan);
     if (!nbin_supported(d->nbin))
         return fail(ctx, PPF_EUNSUP,
-                    "nbin=%d: must be even, in [32, 8192], with nbin/2 = 2^a 3^b 5^c 7^d", d->nbin);
+                    "nbin=%d: must be even, in [32, 8192]", d->nbin);
     if (d->data_dtype != PPF_F32 && d->data_dtype != PPF_F64)
         return fail(ctx, PPF_EINVAL, "data_dtype=%d", d->data_dtype);
     if (d->nmodel < 1) return fail(ctx, PPF_EINVAL, "nmodel=%d", d->nmodel);
@@ -435,7 +435,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // fused guess: the sub-ints k_xspec_w streams whose mean-model cutoff
     // fits its guess harmonics accumulate the guess spectrum there
     uint8_t *gflag = nullptr;
-    if (d->guess && L.fused && fft_log2(d->nbin / 2) == 10) {   // (xspec_guess_fused)
+    if (d->guess && L.fused && ppf::xspec_guess_fused_n(fft_log2(d->nbin / 2))) {
         gflag = (uint8_t *)(ws + L.gflag);
         const int klim = 64 * ppf::guess_npl(fft_log2(d->nbin / 2));
         if ((e = ppf::launch_gflag(d->nsub, d->nchan, needx, (const int32_t *)(ws + L.KC),
@@ -477,7 +477,9 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     xa.needx = (fused || L.momx) ? needx : nullptr;
     // fused: only k_pass reads X, and only below its channels' cutoffs;
     // momx: k_moments reads it below the same cutoffs
-    xa.KC = (fused || L.momx) ? (const int32_t *)(ws + L.KC) : nullptr;
+    // block-FFT path: only k_xspec_wm (the smooth non-power-of-two lengths)
+    // uses it, writing X below the same cutoffs its readers stop at
+    xa.KC = (fused || L.momx || !wave) ? (const int32_t *)(ws + L.KC) : nullptr;
     if (wave) {
         // (nothing to do when the caller has ruled out X: every sub-int is
         // fitted from k_xmom_g's moments)

@@ -184,6 +184,33 @@ __device__ __forceinline__ void blk_sum(double (&v)[K], double *scratch) {
         block_sum<K>(v, scratch);
     }
 }
+// blk_sum of K values and a block max of one more, in one LDS round trip
+// (the sums in blk_sum's order, bit-identical); scratch: kWaves * (K + 1)
+template <int K, int TB>
+__device__ __forceinline__ void blk_sum_max(double (&v)[K], double &m, double *scratch) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
+    m = wave_max(m);
+    if constexpr (TB != 64) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) scratch[wave * (K + 1) + i] = v[i];
+            scratch[wave * (K + 1) + K] = m;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double s = 0.0;
+            for (int w = 0; w < kWaves; ++w) s += scratch[w * (K + 1) + i];
+            v[i] = s;
+        }
+        double mm = scratch[K];
+        for (int w = 1; w < kWaves; ++w) mm = fmax(mm, scratch[w * (K + 1) + K]);
+        m = mm;
+        __syncthreads();
+    }
+}
 template <int K, int TB>
 __device__ __forceinline__ void blk_max(double (&v)[K], double *scratch) {
     if constexpr (TB == 64) {
@@ -270,34 +297,42 @@ __device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, 
 }
 
 // ---------------------------------------------------------------------------
-// Mixed-radix LDS FFT for N = 2^a 3^b 5^c 7^d <= 4096 (nbin = 2N not a power
+// Mixed-radix LDS FFT for any N <= 4096 (nbin = 2N not a power
 // of two: 1000, 1536, 600, ...; numpy's pocketfft takes any length,
 // pptoaslib.py:1022-1025, pplib.py:2455).  Stockham autosort as lds_fft:
 // stage with radix R and span L reads x_q = buf[j + q N/R] (j < N/R,
 // k = j mod L), twiddles x_q by T[q k N/(R L)], takes the R-point DFT and
 // writes buf[(j - k) R + k + q L].  Radices: 4s (one 2 first when the
-// power of two is odd), then 3s, 5s, 7s.  Power-of-two N goes to lds_fft
+// power of two is odd), then 3s, 5s, 7s, then larger prime factors on the
+// generic-radix stage (mr_stage_g).  Power-of-two N goes to lds_fft
 // (bitwise unchanged).
 // ---------------------------------------------------------------------------
 constexpr int kMaxFftN = 4096;
 
-// Stage radices of N in order; returns their count, 0 when N has a prime
-// factor above 7 (or N < 2).
+// Stage radices of N in order: 4s (one 2 first when the power of two is
+// odd), 3s, 5s, 7s, then any larger prime factors (the generic-radix stage
+// below).  Returns their count, 0 for N < 2.
 __host__ __device__ inline int fft_radices(int N, int *r) {
     if (N < 2) return 0;
     int n = N, p2 = 0, c = 0;
     while ((n & 1) == 0) { n >>= 1; ++p2; }
     if (p2 & 1) r[c++] = 2;
     for (int i = 0; i < p2 / 2; ++i) r[c++] = 4;
-    const int odd[3] = {3, 5, 7};
-    for (int f : odd)
+    for (int f = 3; f * f <= n; f += 2)
         while (n % f == 0) { n /= f; r[c++] = f; }
-    return n == 1 ? c : 0;
+    if (n > 1) r[c++] = n;
+    return c;
 }
-__host__ __device__ inline bool fft_len_supported(int N) {
-    int r[32];
-    return N >= 2 && N <= kMaxFftN && fft_radices(N, r) > 0;
+// N = 2^a 3^b 5^c 7^d: every stage has a hard-coded butterfly
+__host__ __device__ inline bool fft_len_smooth(int N) {
+    if (N < 2) return false;
+    int n = N;
+    const int f[4] = {2, 3, 5, 7};
+    for (int p : f)
+        while (n % p == 0) n /= p;
+    return n == 1;
 }
+__host__ __device__ inline bool fft_len_supported(int N) { return N >= 2 && N <= kMaxFftN; }
 __host__ __device__ inline bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 // cos / sin (2 pi m / R), m < R, for the odd radices (exact decimal expansions)
@@ -330,19 +365,37 @@ __device__ __forceinline__ void dft_small(double2 (&x)[R], bool inv) {
         x[2] = csub(s02, s13);
         x[3] = csub(d02, id13);
     } else {
+        // odd R over the pairs a_j = x_j + x_{R-j}, b_j = x_j - x_{R-j}
+        // (j = 1 .. H): c_m = x_0 + sum_j cos(2 pi j m / R) a_j,
+        // d_m = sum_j sin(2 pi j m / R) b_j, and y_m = c_m -+ i d_m,
+        // y_{R-m} = c_m +- i d_m (forward / inverse): H^2 real-by-complex
+        // products per part instead of (R-1)^2 complex ones
+        constexpr int H = (R - 1) / 2;
         const double *C = R == 3 ? kCos3 : (R == 5 ? kCos5 : kCos7);
         const double *S = R == 3 ? kSin3 : (R == 5 ? kSin5 : kSin7);
-        const double sg = inv ? 1.0 : -1.0;
+        double2 pa[H], pb[H];
+        double2 y0 = x[0];
+#pragma unroll
+        for (int j = 1; j <= H; ++j) {
+            pa[j - 1] = cadd(x[j], x[R - j]);
+            pb[j - 1] = csub(x[j], x[R - j]);
+            y0 = cadd(y0, pa[j - 1]);
+        }
         double2 y[R];
+        y[0] = y0;
 #pragma unroll
-        for (int m = 0; m < R; ++m) {
-            double2 acc = x[0];
+        for (int m = 1; m <= H; ++m) {
+            double2 c = x[0], d = cmk(0.0, 0.0);
 #pragma unroll
-            for (int q = 1; q < R; ++q) {
-                const int e = (m * q) % R;
-                acc = cadd(acc, cmul(x[q], cmk(C[e], sg * S[e])));
+            for (int j = 1; j <= H; ++j) {
+                const int e = (j * m) % R;
+                c = cmk(fma(C[e], pa[j - 1].x, c.x), fma(C[e], pa[j - 1].y, c.y));
+                d = cmk(fma(S[e], pb[j - 1].x, d.x), fma(S[e], pb[j - 1].y, d.y));
             }
-            y[m] = acc;
+            // -i d (forward) / +i d (inverse)
+            const double2 id = inv ? cmk(-d.y, d.x) : cmk(d.y, -d.x);
+            y[m] = cadd(c, id);
+            y[R - m] = csub(c, id);
         }
 #pragma unroll
         for (int m = 0; m < R; ++m) x[m] = y[m];
@@ -382,6 +435,55 @@ __device__ void mr_stage(double2 *buf, int N, int L, const double2 *__restrict__
     __syncthreads();
 }
 
+// Generic-radix stage for a prime factor R > 7 of N (1002 = 2 * 3 * 167,
+// 1022 = 2 * 7 * 73 bins ...), the same Stockham step with the stage twiddle
+// and the R-point DFT folded into one table index: the output at
+// o = (j - k) R + k + m L is sum_q buf[j + q N/R] T[q (k N/(R L) + m N/R) mod N].
+// One output per thread per pass (NT threads starting at t0), O(N R) work;
+// all of a thread's reads are done before the caller's barrier, its writes
+// after it.
+template <int QO>
+__device__ __forceinline__ void gr_stage_read(const double2 *buf, int N, int L, int R,
+                                              const double2 *__restrict__ T, bool inv, int t0, int NT,
+                                              double2 (&y)[QO]) {
+    const int nb = N / R, ts = N / (R * L), RL = R * L;
+#pragma unroll
+    for (int i = 0; i < QO; ++i) {
+        const int o = t0 + i * NT;
+        if (o < N) {
+            const int blk = o / RL, rem = o - blk * RL, m = rem / L, k = rem - m * L;
+            const int j = blk * L + k;
+            int e = k * ts + m * nb;
+            e = e >= N ? e - N : e;
+            double2 acc = buf[j];
+            for (int q = 1, idx = e; q < R; ++q) {
+                const double2 w = twid(T, idx, inv);
+                acc = cadd(acc, cmul(buf[j + q * nb], w));
+                idx += e;
+                idx = idx >= N ? idx - N : idx;
+            }
+            y[i] = acc;
+        }
+    }
+}
+template <int QO>
+__device__ __forceinline__ void gr_stage_write(double2 *buf, int N, int t0, int NT, const double2 (&y)[QO]) {
+#pragma unroll
+    for (int i = 0; i < QO; ++i) {
+        const int o = t0 + i * NT;
+        if (o < N) buf[o] = y[i];
+    }
+}
+__device__ __noinline__ void mr_stage_g(double2 *buf, int N, int L, int R, const double2 *__restrict__ T,
+                                        bool inv) {
+    constexpr int QO = kMaxFftN / kBlock;
+    double2 y[QO];
+    gr_stage_read<QO>(buf, N, L, R, T, inv, threadIdx.x, kBlock, y);
+    __syncthreads();
+    gr_stage_write<QO>(buf, N, threadIdx.x, kBlock, y);
+    __syncthreads();
+}
+
 // Any supported N (fft_len_supported); every thread of the block calls it.
 __device__ void lds_fft(double2 *buf, int log2N, const double2 *__restrict__ T, bool inverse);
 __device__ __forceinline__ void lds_fft_mixed(double2 *buf, int N, const double2 *__restrict__ T,
@@ -395,7 +497,8 @@ __device__ __forceinline__ void lds_fft_mixed(double2 *buf, int N, const double2
             case 3: mr_stage<3>(buf, N, L, T, inverse); break;
             case 4: mr_stage<4>(buf, N, L, T, inverse); break;
             case 5: mr_stage<5>(buf, N, L, T, inverse); break;
-            default: mr_stage<7>(buf, N, L, T, inverse); break;
+            case 7: mr_stage<7>(buf, N, L, T, inverse); break;
+            default: mr_stage_g(buf, N, L, r[s], T, inverse); break;
         }
         L *= r[s];
     }

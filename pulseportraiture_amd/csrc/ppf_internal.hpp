@@ -295,6 +295,12 @@ hipError_t launch_gflag(int nsub, int nchan, const uint8_t *needx, const int32_t
                         const int32_t *model_index, int klim, uint8_t *gflag, hipStream_t st);
 hipError_t launch_dsum(const DsumArgs &a, hipStream_t st);
 bool xspec_wave_supported(int log2N, int cb);
+// wave-per-row mixed-radix spectrum pass (k_xspec_wm): nbin / 2 smooth, not
+// a power of two, <= 1024
+bool xspec_wm_supported(int nbin);
+// the spectrum pass accumulates the GetTOAs guess at this FFT size (k_gflag)
+bool xspec_guess_fused_n(int log2N);
+hipError_t launch_xspec_wm(const XspecArgs &a, hipStream_t st);
 hipError_t launch_xspec_wave(const XspecArgs &a, hipStream_t st);
 hipError_t launch_xmom(const XmomArgs &a, bool full, hipStream_t st);
 hipError_t launch_btab(int N, double *Bt, hipStream_t st);

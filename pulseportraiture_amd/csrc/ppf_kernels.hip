@@ -626,6 +626,124 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
 }
 
 // ===========================================================================
+// k_dsum_wn: k_dsum_w for any nbin <= NBMAX (nbin not a power of two: 1000,
+// 1536, 1022 ...; round 5).  The same wave-per-row streaming (next row in
+// flight, channel scalars in lane registers, fixed-order wave sums), with
+// per-lane element loads and the (t + i0) mod nbin index by compare-subtract.
+// ===========================================================================
+template <int DT, int NBMAX>
+__global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
+    using ElT = typename std::conditional<DT == 0, float, double>::type;
+    constexpr int J = NBMAX / 64;
+    extern __shared__ __attribute__((aligned(16))) double dlds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = a.nbin;
+    ElT *xs = reinterpret_cast<ElT *>(dlds) + wave * NBMAX;
+    const int s = blockIdx.x / a.nblkd, blk = blockIdx.x % a.nblkd;
+    if (a.gflag && a.gflag[s]) return;        // guess fused into the spectrum pass
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    const double *gwt = a.guess_weights + (int64_t)s * a.nchan;
+    double v0 = 0.0, v1 = 0.0;
+    for (int n = lane; n < a.nchan; n += 64)
+        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    const double Dg = (double)nb * kDconst * a.guess_DM[s] / a.P[s];
+    const double mu = v0 / v1;
+    double nu_mean_m2 = 1.0 / (mu * mu);
+    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
+        const double nf = a.nu_fits[(int64_t)s * 3];
+        if (nf == nf) nu_mean_m2 = 1.0 / (nf * nf);
+    }
+    const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
+    const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)s * a.nchan * nb;
+    double t_w[2], t_f[2];
+    int t_m[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int ch = c0 + lane + 64 * k;
+        const bool in = ch < c1;
+        t_w[k] = in ? gwt[ch] : 0.0;
+        t_f[k] = in ? fr[ch] : 1.0;
+        t_m[k] = (in && (!mask || mask[ch])) ? 1 : 0;
+    }
+    auto usable = [&](int n) {
+        const int r = n - c0;
+        return n < c1 && __builtin_amdgcn_readlane(r < 64 ? t_m[0] : t_m[1], r & 63) != 0;
+    };
+    double acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = 0.0;
+    double wsum = 0.0, wcnt = 0.0;
+    // element t = lane + 64 i of a row; past nbin: element nbin - 1 again
+    // (unconditional loads keep the prefetch in VGPRs)
+    auto load = [&](ElT (&p)[J], int m) {
+        const ElT *src = rows + (int64_t)m * nb;
+#pragma unroll
+        for (int i = 0; i < J; ++i) {
+            const int t = lane + 64 * i;
+            p[i] = src[t < nb ? t : nb - 1];
+        }
+    };
+    int n = c0 + wave;
+    while (n < c1 && !usable(n)) n += kWaves;
+    ElT pre[J];
+    load(pre, min(n, c1 - 1));
+    while (n < c1) {
+        wave_lds_sync();                      // the previous row's reads are issued
+#pragma unroll
+        for (int i = 0; i < J; ++i) xs[lane + 64 * i] = pre[i];
+        int nn = n + kWaves;
+        while (nn < c1 && !usable(nn)) nn += kWaves;
+        load(pre, nn < c1 ? nn : n);          // next row in flight during this one
+        const int r = n - c0;
+        const double w = readlane_d(r < 64 ? t_w[0] : t_w[1], r & 63),
+                     f0 = readlane_d(r < 64 ? t_f[0] : t_f[1], r & 63);
+        const double tau = Dg * (1.0 / (f0 * f0) - nu_mean_m2);
+        const double fl = floor(tau), f = tau - fl;
+        const int i0 = (int)(fl - (double)nb * floor(fl / (double)nb));   // mod nbin
+        const double wa = w * (1.0 - f), wb = w * f;
+        wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int t = lane + 64 * j;
+            int ia = t + i0;
+            ia -= ia >= nb ? nb : 0;
+            const int ib = ia + 1 == nb ? 0 : ia + 1;
+            if (t < nb) acc[j] = fma(wa, (double)xs[ia], fma(wb, (double)xs[ib], acc[j]));
+        }
+        wsum += w;
+        wcnt += 1.0;
+        n = nn;
+    }
+    // fixed-order sum of the four waves' profiles (LDS reused as NBMAX doubles)
+    __syncthreads();
+    double *part = dlds;
+    for (int w2 = 0; w2 < kWaves; ++w2) {
+        if (wave == w2) {
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int t = lane + 64 * j;
+                part[t] = w2 == 0 ? acc[j] : part[t] + acc[j];
+            }
+        }
+        __syncthreads();
+    }
+    double *out = a.gP + ((int64_t)s * a.nblkd + blk) * nb;
+    for (int t = threadIdx.x; t < nb; t += kBlock) out[t] = part[t];
+    __shared__ double wred[kWaves * 2];
+    if (lane == 0) { wred[wave * 2] = wsum; wred[wave * 2 + 1] = wcnt; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int w2 = 0; w2 < kWaves; ++w2) { s0 += wred[w2 * 2]; s1 += wred[w2 * 2 + 1]; }
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 0] = s0;
+        a.gw[((int64_t)s * a.nblkd + blk) * 2 + 1] = s1;
+    }
+}
+
+// ===========================================================================
 // k_guess: GetTOAs initial phase (pptoas.py:461-499): FFTFIT of the weighted,
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
@@ -1133,6 +1251,11 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
         case 11: launch_xspec_t<11>(a, st); break;
         case 12: launch_xspec_t<12>(a, st); break;
         case 0: {      // nbin / 2 not a power of two
+#ifndef PPF_XSPEC_WM
+#define PPF_XSPEC_WM 1
+#endif
+            // wave per row (k_xspec_wm) up to N = 1024; the block kernel above
+            if (PPF_XSPEC_WM && xspec_wm_supported(a.nbin) && a.cb <= 64) return launch_xspec_wm(a, st);
             dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(kBlock);
             const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
             if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_any<0>), g, b, lds, st, a);
@@ -1144,6 +1267,10 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 bool dsum_wave_supported(int nbin) { return nbin >= 256 && nbin <= 2048 && is_pow2(nbin); }
+// k_dsum_wn for the other nbin <= 2048 (0: the block kernel k_dsum)
+#ifndef PPF_DSUM_WN
+#define PPF_DSUM_WN 1
+#endif
 
 template <int DT, int L2>
 static void launch_dsum_w(const DsumArgs &a, hipStream_t st) {
@@ -1170,6 +1297,20 @@ hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
         return hipGetLastError();
     }
     dim3 g((unsigned)((int64_t)a.nsub * a.nblkd)), b(kBlock);
+    if (PPF_DSUM_WN && a.nbin <= 2048 && a.cbd <= 128) {
+        // wave-per-row pass at any nbin (k_dsum_wn), NBMAX 1024 or 2048
+        const int nbm = a.nbin <= 1024 ? 1024 : 2048;
+        const size_t row = (size_t)kWaves * nbm * (a.dtype == 0 ? 4 : 8);
+        const size_t lds = row > (size_t)nbm * 8 ? row : (size_t)nbm * 8;
+        if (nbm == 1024) {
+            if (a.dtype == 0) hipLaunchKernelGGL((k_dsum_wn<0, 1024>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_dsum_wn<1, 1024>), g, b, lds, st, a);
+        } else {
+            if (a.dtype == 0) hipLaunchKernelGGL((k_dsum_wn<0, 2048>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_dsum_wn<1, 2048>), g, b, lds, st, a);
+        }
+        return hipGetLastError();
+    }
     const int jb = a.nbin >= 2048 ? 8 : (a.nbin + kBlock - 1) / kBlock;
     if (a.dtype == 0) {
         if (jb >= 8) hipLaunchKernelGGL((k_dsum<0, 8>), g, b, 0, st, a);

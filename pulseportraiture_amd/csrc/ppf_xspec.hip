@@ -151,18 +151,25 @@ __host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() 
 // minimum waves per SIMD: at 1024 points the LDS admits two 4-wave
 // workgroups per CU (two waves per SIMD), and the fused-guess variant must
 // keep that register budget (<= 256)
-template <int LOG2N>
-__host__ __device__ constexpr int xspec_wpe() { return LOG2N == 10 ? 2 : 1; }
-// the fused guess runs at 1024 points only: below, its extra registers cost
-// a wave per SIMD or spill (those shapes take k_dsum)
-__host__ __device__ constexpr bool xspec_guess_fused(int log2N) { return log2N == 10; }
+// PPF_GS9: the fused guess at 512 points as well (1: capped at four waves
+// per SIMD, spilling; 2: uncapped, two waves per SIMD; 0: those shapes take
+// k_dsum_w)
+#ifndef PPF_GS9
+#define PPF_GS9 1
+#endif
+template <int LOG2N, bool GS = false>
+__host__ __device__ constexpr int xspec_wpe() { return LOG2N == 10 ? 2 : (LOG2N == 9 && GS && PPF_GS9 == 1 ? 4 : 1); }
+// the fused guess runs at 1024 points (and 512 with PPF_GS9): below, its
+// extra registers cost a wave per SIMD or spill (those shapes take k_dsum)
+__host__ __device__ constexpr bool xspec_guess_fused(int log2N) { return log2N == 10 || (log2N == 9 && PPF_GS9 != 0); }
+bool xspec_guess_fused_n(int log2N) { return xspec_guess_fused(log2N); }
 // one post-pass over the transform (power sums and X together, X scaled at
 // the write-out); 0: the two-pass form (sums, then X scaled in the buffer)
 #ifndef PPF_XS_ONEPASS
 #define PPF_XS_ONEPASS 1
 #endif
 template <int LOG2N, int DT, bool GS>
-__global__ __launch_bounds__(64 * xsw<LOG2N>()) __attribute__((amdgpu_waves_per_eu(xspec_wpe<LOG2N>())))
+__global__ __launch_bounds__(64 * xsw<LOG2N>()) __attribute__((amdgpu_waves_per_eu(xspec_wpe<LOG2N, GS>())))
 void k_xspec_w(XspecArgs a) {
     constexpr int kXSW = xsw<LOG2N>();
     using P = wfft::Plan<LOG2N>;
@@ -182,7 +189,7 @@ void k_xspec_w(XspecArgs a) {
 #ifdef PPF_XS_MPRE
     constexpr int MD = PPF_XS_MPRE;
 #else
-    constexpr int MD = LOG2N == 10 ? 4 : (LOG2N == 9 ? PPF_XS_MPRE9 : 0);
+    constexpr int MD = LOG2N == 10 ? 4 : (LOG2N == 9 ? (GS && PPF_GS9 == 1 ? 0 : PPF_XS_MPRE9) : 0);
 #endif
     using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -1271,6 +1278,7 @@ void k_xspec_w2(XspecArgs a) {
     }
     {
         const int lane = lane0;
+        (void)lane;
         XP_DONE();
     }
     if constexpr (GS) {
@@ -1292,6 +1300,229 @@ void k_xspec_w2(XspecArgs a) {
             }
         }
     }
+}
+
+// ===========================================================================
+// k_xspec_wm: the spectrum pass for nbin / 2 = 2^a 3^b 5^c 7^d not a power
+// of two (1000, 1536, 2000 bins ...), N <= 1024 (round 5).  k_xspec_any gave
+// each row to a 256-thread workgroup (a barrier per FFT stage and per
+// block sum; 2 points per thread at 1000 bins) and wrote X one channel per
+// lane, every harmonic.  Here, as k_xspec_w: a 4-wave workgroup takes a
+// block of channels of one sub-int, a round of 4 rows, one row per wave:
+// the row's mixed-radix Stockham stages run in the wave's own LDS buffer
+// (wave-level ordering only, no workgroup barrier inside a row), the real
+// post-pass forms the noise / Sd sums and X = D conj(M) in place, and after
+// one barrier the workgroup writes the round's X harmonic-major, below each
+// 64-channel group's cutoff (k_model_cut), as k_pass / k_moments read it.
+// Same arithmetic as k_xspec_any (lds_fft_mixed's stages, rfft_bin).
+// ===========================================================================
+constexpr int kWmW = 4;              // waves per workgroup
+constexpr int kWmMaxN = 1024;        // largest N (complex points) per wave
+
+// j mod L for j < 8192 with a float reciprocal (L is wave-uniform; an
+// integer division by a runtime divisor is a ~40-instruction sequence)
+__device__ __forceinline__ int mod_small(int j, int L, float invL) {
+    const int q = (int)((float)j * invL);
+    int k = j - q * L;
+    k += k < 0 ? L : 0;
+    k -= k >= L ? L : 0;
+    return k;
+}
+
+// one mixed-radix Stockham stage of radix R (span L) over N points, by one
+// wave: all of a lane's reads before its writes (a wave's LDS operations
+// are processed in order, so no lane's write overtakes another's read);
+// stage twiddles from the workgroup's LDS copy of T
+template <int R, int NMAX>
+__device__ __forceinline__ void wmr_stage(double2 *buf, int N, int L, const double2 *tw, int lane) {
+    constexpr int QM = (NMAX / R + 63) / 64;
+    const int nb = N / R, ts = N / (R * L);
+    const float invL = 1.0f / (float)L;
+    double2 x[QM][R];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int j = lane + 64 * q;
+        if (j < nb) {
+            const int k = mod_small(j, L, invL);
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[q][r] = buf[j + r * nb];
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[q][r] = cmul(x[q][r], tw[r * k * ts]);
+            dft_small<R>(x[q], false);
+        }
+    }
+    wfft::wave_sync();
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+        const int j = lane + 64 * q;
+        if (j < nb) {
+            const int k = mod_small(j, L, invL);
+            const int o = (j - k) * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[o + r * L] = x[q][r];
+        }
+    }
+    wfft::wave_sync();
+}
+
+// radix 7 and the generic-radix stage (prime factors above 7) out of line:
+// inlined, their butterflies' registers on top of the row loop's spill
+template <int NMAX>
+__device__ __noinline__ void wmr_stage7(double2 *buf, int N, int L, const double2 *tw, int lane) {
+    wmr_stage<7, NMAX>(buf, N, L, tw, lane);
+}
+template <int NMAX>
+__device__ __noinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, const double2 *tw, int lane) {
+    double2 y[NMAX / 64];
+    gr_stage_read<NMAX / 64>(buf, N, L, R, tw, false, lane, 64, y);
+    wfft::wave_sync();
+    gr_stage_write<NMAX / 64>(buf, N, lane, 64, y);
+    wfft::wave_sync();
+}
+
+// NMAX: the largest N of the instantiation (512: <= 128 VGPRs, four waves
+// per SIMD; 1024: two), which sizes every stage's register footprint (a
+// lane holds all of its butterflies between the stage's reads and writes)
+template <int DT, int NMAX>
+__global__ __launch_bounds__(64 * kWmW) __attribute__((amdgpu_waves_per_eu(NMAX <= 512 ? 4 : 2)))
+void k_xspec_wm(XspecArgs a) {
+    const int N = a.nbin >> 1, NH = N + 1;
+    const int SL = N + 2;                      // [0, N]: Z then X; [N + 1]: 1/errs_FT^2
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *buf = lds + wave * SL;
+    double2 *twl = lds + kWmW * SL;            // T[0, N): the stage twiddles
+    int s, cb;
+    block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
+    if (a.needx && !a.needx[s]) return;
+    for (int i = threadIdx.x; i < N; i += 64 * kWmW) twl[i] = a.T[i];
+    __syncthreads();
+    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
+    const int nround = (a.cb + kWmW - 1) / kWmW;
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double sqrtN = sqrt((double)N);
+    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
+    int kw = NH;
+    if (a.KC) {
+        const int nn = (cbase & ~63) + lane;
+        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
+    }
+    const int mlane = (cbase + lane < cend && (!mask || mask[cbase + lane])) ? 1 : 0;
+    auto usable = [&](int n) {
+        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
+    };
+    const int nl = cbase + lane;
+    const double ch_mpow = nl < cend ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
+    const double ch_err = (a.errs && nl < cend) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
+    const bool two0 = (__builtin_ctz((unsigned)N) & 1) != 0;
+    for (int r = 0, n = cbase + wave; r < nround; ++r, n += kWmW) {
+        const bool live = usable(n);
+        if (n < cend && !live && lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
+        if (live) {
+            const int64_t crow = (int64_t)s * a.nchan + n;
+            if (DT == 0) {
+                const float2 *src = reinterpret_cast<const float2 *>(a.data) + crow * (int64_t)N;
+                for (int j = lane; j < N; j += 64) {
+                    const float2 v = src[j];
+                    buf[j] = cmk((double)v.x, (double)v.y);
+                }
+            } else {
+                const double2 *src = reinterpret_cast<const double2 *>(a.data) + crow * (int64_t)N;
+                for (int j = lane; j < N; j += 64) buf[j] = src[j];
+            }
+            wfft::wave_sync();
+            // the stages in fft_radices' order (one 2 when the power of two
+            // is odd, 4s, then the odd primes ascending), wave-uniform
+            int L = 1, rem = N;
+            bool two = two0;
+            while (rem > 1) {
+                int R;
+                if (two) { R = 2; two = false; }
+                else if ((rem & 3) == 0) R = 4;
+                else { R = 3; while (rem % R) R += 2; }
+                switch (R) {
+                    case 2: wmr_stage<2, NMAX>(buf, N, L, twl, lane); break;
+                    case 3: wmr_stage<3, NMAX>(buf, N, L, twl, lane); break;
+                    case 4: wmr_stage<4, NMAX>(buf, N, L, twl, lane); break;
+                    case 5: wmr_stage<5, NMAX>(buf, N, L, twl, lane); break;
+                    case 7: wmr_stage7<NMAX>(buf, N, L, twl, lane); break;
+                    default: wmr_stage_g<NMAX>(buf, N, L, R, twl, lane); break;
+                }
+                L *= R;
+                rem /= R;
+            }
+            // real post-pass on the pairs (k, N - k), k <= N/2, in place:
+            // X_k into slot k, X_{N-k} into slot N - k (k = 0: X_N into
+            // slot N); unscaled, the write-out applies 1/errs_FT^2
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            double pn = 0.0, pd = 0.0;
+            for (int k = lane; k <= N / 2; k += 64) {
+                const int kn = N - k;
+                const double2 dk = rfft_bin(buf, N, a.T2, k);
+                const double2 dn = rfft_bin(buf, N, a.T2, kn);
+                const double p0 = cabs2(dk), p1 = cabs2(dn);
+                if (k >= a.kc) pn += p0;
+                if (k >= 1) pd += p0;
+                if (kn != k) {
+                    if (kn >= a.kc) pn += p1;
+                    pd += p1;
+                }
+                // (every read of this pair is done: rfft_bin read slots k
+                // and N - k only, and no other lane touches them)
+                if (k < kw) buf[k] = k == 0 ? cmk(0.0, 0.0) : cmulc(dk, Mrow[k]);
+                if (kn < kw) buf[kn] = cmulc(dn, Mrow[kn]);
+            }
+            pn = wave_sum(pn);
+            pd = wave_sum(pd);
+            const int rr = n - cbase;
+            double errs_FT;
+            if (a.errs) errs_FT = readlane_d(ch_err, rr) * sqrtN;
+            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+            const double mpow = readlane_d(ch_mpow, rr);
+            if (lane == 0) {
+                reinterpret_cast<double *>(buf + N + 1)[0] = inv_e2;
+                double *chan = a.chan + crow * 4;
+                chan[0] = errs_FT;
+                chan[1] = inv_e2;
+                chan[2] = pd * inv_e2;          // Sd_n
+                chan[3] = mpow * inv_e2;        // S_n at tau = 0
+            }
+        }
+        __syncthreads();
+        // write-out: thread t -> channel c = t % 4 of the round, harmonics
+        // k = t / 4 + 64 j
+        {
+            const int c = threadIdx.x % kWmW, nc = cbase + r * kWmW + c;
+            if (nc < cend) {
+                const bool ok = !mask || mask[nc];
+                const double2 *b = lds + c * SL;
+                const double ie2 = ok ? reinterpret_cast<const double *>(b + N + 1)[0] : 0.0;
+                for (int k = threadIdx.x / kWmW; k < kw; k += 64)
+                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[k], ie2) : cmk(0.0, 0.0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+bool xspec_wm_supported(int nbin) {
+    const int N = nbin / 2;
+    return (nbin & 1) == 0 && !is_pow2(N) && N <= kWmMaxN && fft_len_supported(N);
+}
+
+hipError_t launch_xspec_wm(const XspecArgs &a, hipStream_t st) {
+    const size_t lds = ((size_t)kWmW * (a.nbin / 2 + 2) + a.nbin / 2) * sizeof(double2);
+    dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kWmW);
+    if (a.nbin / 2 <= 512) {
+        if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wm<0, 512>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_xspec_wm<1, 512>), g, b, lds, st, a);
+    } else {
+        if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wm<0, 1024>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_xspec_wm<1, 1024>), g, b, lds, st, a);
+    }
+    return hipGetLastError();
 }
 
 // k_xspec_w2 at 1024 points unless PPF_XSPEC2=0 (environment, read once)

@@ -420,8 +420,7 @@ def _desc_workspace_bytes(lib, d):
     nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
-                                  " (nbin must be even, in [32, 8192], with "
-                                  "nbin/2 = 2^a 3^b 5^c 7^d)" %
+                                  " (nbin must be even, in [32, 8192])" %
                                   (d.nsub, d.nchan, d.nbin))
     return nbytes
 
@@ -573,15 +572,8 @@ def noise_rows(rows, frac=4, dev=None):
 
 
 def noise_len_supported(n):
-    """Row lengths ppf_noise_batch transforms (its LDS FFT): even, 32..8192,
-    n/2 = 2^a 3^b 5^c 7^d."""
-    if n % 2 or n < 32 or n > 8192:
-        return False
-    m = n // 2
-    for r in (2, 3, 5, 7):
-        while m % r == 0:
-            m //= r
-    return m == 1
+    """Row lengths ppf_noise_batch transforms (its LDS FFT): even, 32..8192."""
+    return n % 2 == 0 and 32 <= n <= 8192
 
 
 def noise_long(row, frac=4, dev=None):

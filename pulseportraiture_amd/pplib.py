@@ -343,8 +343,8 @@ def get_noise_PS(data, frac=4, chans=False):
     row = data.ravel()
     if not engine.noise_len_supported(row.size):
         # the flattened portrait (nchan nbin samples; pplib.py:2334-2338) is
-        # longer than the LDS transforms of ppf_noise_batch (<= 8192 points,
-        # 2^a 3^b 5^c 7^d): one library rFFT on the device (rocFFT) instead
+        # longer than the LDS transforms of ppf_noise_batch (even, <= 8192
+        # points) or odd: one library rFFT on the device (rocFFT) instead
         return engine.noise_long(row, frac)
     return float(engine.noise_rows(row[None, :], frac).cpu().numpy()[0])
 

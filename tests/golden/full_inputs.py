@@ -90,6 +90,13 @@ FITS = [
          seed=110),
     dict(name="pdta_128x1536", nchan=128, nbin=1536, flags=[1, 1, 0, 1, 1],
          seed=111, tau=2e-3),
+    # round 5: nbin / 2 with a prime factor above 7 (the generic-radix
+    # stage): 1022 = 2 * 7 * 73 (wave-per-row spectrum pass), 2006 =
+    # 2 * 17 * 59 (block FFT, nbin / 2 > 1024)
+    dict(name="pd_128x1022", nchan=128, nbin=1022, flags=[1, 1, 0, 0, 0],
+         seed=112),
+    dict(name="pdta_64x2006", nchan=64, nbin=2006, flags=[1, 1, 0, 1, 1],
+         seed=113, tau=2e-3),
 ]
 
 
@@ -201,6 +208,8 @@ TOAS = [
     # (h) round 4: nbin = 1000 through the whole get_TOAs loop (guess
     # profile, its FFTFIT, the fit) on the mixed-radix FFT
     dict(name="nb1000", nfile=1, nsub=3, nchan=64, nbin=1000, seed=213),
+    # (i) round 5: nbin = 1022 (2 * 7 * 73), the generic-radix FFT stage
+    dict(name="nb1022", nfile=1, nsub=3, nchan=64, nbin=1022, seed=214),
 ]
 
 

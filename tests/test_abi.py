@@ -63,12 +63,13 @@ def test_workspace_query_and_validation_without_gpu():
     d.options = _lib.OPT_NO_X          # ignored off the fused path
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == nb3
     d.options = 0
-    # nbin 1000 (nbin/2 = 2^2 5^3) runs on the mixed-radix LDS FFT; nbin/2
-    # with a prime factor above 7 (1002 = 2 x 3 x 167), odd nbin and nbin
-    # past 8192 are refused
-    d.nbin = 1000
-    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0
-    for nb in (1002, 1001, 8194, 16):
+    # nbin 1000 (nbin/2 = 2^2 5^3) runs on the mixed-radix LDS FFT, nbin/2
+    # with a prime factor above 7 (1002 = 2 x 3 x 167, 8186 = 2 x 4093) on
+    # its generic-radix stage; odd nbin and nbin past 8192 are refused
+    for nb in (1000, 1002, 1022, 8186):
+        d.nbin = nb
+        assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
+    for nb in (1001, 8194, 16):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
     # with the GetTOAs guess at nbin 2048 the phase/DM fits take their

@@ -34,7 +34,8 @@ def _kept_harmonic_fraction(model):
                                   "pd_64x4096", "pdta_64x128",
                                   "lowsnr_pd_512x2048", "lowsnr_pd_64x512",
                                   "lowsnr_all_512x2048", "pd_128x1000",
-                                  "pdta_128x1536"])
+                                  "pdta_128x1536", "pd_128x1022",
+                                  "pdta_64x2006"])
 def test_fullshape_fit_matches_reference(name):
     """configs[2]'s fit (phi, DM, GM, tau, alpha) and phi+DM+tau+alpha at
     512 x 2048, a narrow-component template at 512 x 2048 (no harmonic
@@ -210,7 +211,7 @@ def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True,
 
 
 BRANCHES = ["scatgm", "scatfix", "opts", "chan12", "tscr", "tnc", "tncscat",
-            "ncg", "nb1000"]
+            "ncg", "nb1000", "nb1022"]
 
 
 @pytest.mark.timeout(300)

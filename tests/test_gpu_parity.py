@@ -37,8 +37,19 @@ def test_noise_matches_reference(ppl):
         np.testing.assert_allclose(
             ppl.get_noise(m["noise_in_%d" % nb], chans=True),
             m["noise_out_%d" % nb], rtol=1e-12)
-    with pytest.raises(NotImplementedError):     # nbin/2 = 3 x 167
-        ppl.get_noise(np.ones((2, 1002)), chans=True)
+    # nbin/2 with a prime factor above 7 (the generic-radix stage): 1002 =
+    # 2 x 3 x 167, 1022 = 2 x 7 x 73, 4094 = 2 x 23 x 89; the reference's
+    # arithmetic (pplib.py:2312-2338) restated in NumPy
+    for shape in ((2, 1002), (3, 1022), (2, 4094)):
+        x = np.random.default_rng(6).normal(size=shape)
+        F = np.fft.rfft(x, axis=-1)
+        p = np.real(F * np.conj(F)) / shape[-1]
+        want = np.sqrt(np.mean(p[:, int((1 - 4 ** -1) * p.shape[-1]):],
+                               axis=-1))
+        np.testing.assert_allclose(ppl.get_noise(x, chans=True), want,
+                                   rtol=1e-12, err_msg=str(shape))
+    with pytest.raises(NotImplementedError):     # odd nbin
+        ppl.get_noise(np.ones((2, 1001)), chans=True)
     # chans=False ravels the portrait (pplib.py:2334-2338): 64 x 2048 and an
     # odd length go through the device FFT library (no LDS-size cap); the
     # restatement is the reference's own NumPy arithmetic
@@ -87,6 +98,20 @@ def test_rotate_matches_reference(ppl, ppt):
     np.testing.assert_allclose(
         ppt.rotate_portrait_full(m["rot_port"], 0.1, 3.0, 2.0, m["rot_freqs"],
                                  1500., 1600., P0), m["rotf_dmgm"], **tol)
+
+
+@pytest.mark.parametrize("nbin", [1000, 1022, 2006, 4094])
+def test_rotate_any_even_nbin_matches_numpy(ppl, nbin):
+    """rotate_data (pplib.py:2427-2480) at nbin/2 not a power of two, on
+    the mixed-radix (1000) and generic-radix (1022 = 2 x 7 x 73, 2006 =
+    2 x 17 x 59, 4094 = 2 x 23 x 89) LDS FFTs, against its own NumPy
+    arithmetic: rfft, phasor, irfft."""
+    x = np.random.default_rng(nbin).normal(size=(3, nbin))
+    ph = 0.2718
+    k = np.arange(nbin // 2 + 1)
+    want = np.fft.irfft(np.fft.rfft(x, axis=-1) *
+                        np.exp(2j * np.pi * k * ph), n=nbin, axis=-1)
+    np.testing.assert_allclose(ppl.rotate_data(x, ph), want, atol=1e-11)
 
 
 def test_rotate_round_trip_and_bad_shapes(ppl, capsys):

@@ -356,7 +356,8 @@ def bench_align(args):
         "xmom": dict(name="k_xmom_g<%d, 0, true, true>" % L2N, ms=kern_ms[0],
                      unit=xmom_unit, bytes=ncalls * (count * xmom_unit +
                                                      nchan * nharm * 16)),
-        "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
+        "dsum": dict(name="k_dsum_w" if (nbin & (nbin - 1)) == 0 else "k_dsum_wn",
+                     ms=kern_ms[1], unit=dsum_unit,
                      bytes=ncalls * count * dsum_unit),
         "accum": dict(name="k_align", ms=acc_ms, unit=acc_unit,
                       bytes=ncalls * (count * acc_unit + nchan * nbin * 8 +
@@ -920,7 +921,8 @@ def main():
     xspec_unit = nchan * nbin * 4 + xh * 16 + 4 * nchan * 8
     L2N = (nbin // 4).bit_length()
     kern = {
-        "dsum": dict(name="k_dsum_w", ms=kern_ms[1], unit=dsum_unit,
+        "dsum": dict(name="k_dsum_w" if (nbin & (nbin - 1)) == 0 else "k_dsum_wn",
+                     ms=kern_ms[1], unit=dsum_unit,
                      bytes=steps_subints * dsum_unit),
     }
     # the library's MOM_X rule (ppf_api.cpp fit_layout): X moments when asked,

@@ -152,10 +152,13 @@ __host__ __device__ constexpr int xspec_slw() { return wfft::buf_slots<LOG2N>() 
 // workgroups per CU (two waves per SIMD), and the fused-guess variant must
 // keep that register budget (<= 256)
 // PPF_GS9: the fused guess at 512 points as well (1: capped at four waves
-// per SIMD, spilling; 2: uncapped, two waves per SIMD; 0: those shapes take
-// k_dsum_w)
+// per SIMD, spilling; 2: uncapped, two waves per SIMD; 0, default: those
+// shapes take k_dsum_w).  Measured (round 5, C5 per 500 sub-ints, one call):
+// C5's model reaches harmonic ~430 of 513, above the NL = 192 guess
+// harmonics, so k_gflag sets no sub-int and the GS=1 variant only costs its
+// registers: k_xspec_w<9> 26.5 vs 22.0 ms, 90.1 vs 84.7 ms per step.
 #ifndef PPF_GS9
-#define PPF_GS9 1
+#define PPF_GS9 0
 #endif
 template <int LOG2N, bool GS = false>
 __host__ __device__ constexpr int xspec_wpe() { return LOG2N == 10 ? 2 : (LOG2N == 9 && GS && PPF_GS9 == 1 ? 4 : 1); }
@@ -1365,14 +1368,12 @@ __device__ __forceinline__ void wmr_stage(double2 *buf, int N, int L, const doub
     wfft::wave_sync();
 }
 
-// radix 7 and the generic-radix stage (prime factors above 7) out of line:
-// inlined, their butterflies' registers on top of the row loop's spill
+// radix 7 and the prime factors above it: the generic-radix stage (one
+// output per lane per pass, R LDS loads and products each; no butterfly
+// arrays, so no spill at the four-wave budget).  Inline: a call from this
+// kernel (out-of-line stages, round 5) faulted on the device.
 template <int NMAX>
-__device__ __noinline__ void wmr_stage7(double2 *buf, int N, int L, const double2 *tw, int lane) {
-    wmr_stage<7, NMAX>(buf, N, L, tw, lane);
-}
-template <int NMAX>
-__device__ __noinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, const double2 *tw, int lane) {
+__device__ __forceinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, const double2 *tw, int lane) {
     double2 y[NMAX / 64];
     gr_stage_read<NMAX / 64>(buf, N, L, R, tw, false, lane, 64, y);
     wfft::wave_sync();
@@ -1446,7 +1447,6 @@ void k_xspec_wm(XspecArgs a) {
                     case 3: wmr_stage<3, NMAX>(buf, N, L, twl, lane); break;
                     case 4: wmr_stage<4, NMAX>(buf, N, L, twl, lane); break;
                     case 5: wmr_stage<5, NMAX>(buf, N, L, twl, lane); break;
-                    case 7: wmr_stage7<NMAX>(buf, N, L, twl, lane); break;
                     default: wmr_stage_g<NMAX>(buf, N, L, R, twl, lane); break;
                 }
                 L *= R;

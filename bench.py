@@ -1087,6 +1087,20 @@ def main():
                           valu_active_per_wave=k.get("valu_active_per_wave"))
                 tot_fl += fl
                 tot_ms += ms
+            if key == "tr_mom" and ms > 0:
+                # k_tr_mom re-reads the moment set of every channel on every
+                # evaluation (16 complex moments on the X-moment path, up to
+                # 32 otherwise) plus the channel scalars and the radius
+                # test's dphi / centre residual: its memory-side rate against
+                # the HBM peak (the sets outgrow the L2s; re-reads of one
+                # sub-int's set within a launch may hit the MALL)
+                nmom = 16 if momx_used else 32
+                bpe = nchan * (nmom * 16 + 40 + 32)
+                mb = steps_subints * mean_nfev * bpe
+                it["memory"] = dict(bytes_per_evaluation=bpe,
+                                    evaluations=round(steps_subints * mean_nfev),
+                                    achieved_gbs=round(mb / (ms / 1e3) / 1e9, 1),
+                                    hbm_frac=round(mb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
             items[key] = it
         solver = dict(bound="fp64", peak=FP64_PEAK_TF, unit="TFLOP/s",
                       achieved=round(tot_fl / max(tot_ms, 1e-9) / 1e9, 3)

@@ -184,33 +184,6 @@ __device__ __forceinline__ void blk_sum(double (&v)[K], double *scratch) {
         block_sum<K>(v, scratch);
     }
 }
-// blk_sum of K values and a block max of one more, in one LDS round trip
-// (the sums in blk_sum's order, bit-identical); scratch: kWaves * (K + 1)
-template <int K, int TB>
-__device__ __forceinline__ void blk_sum_max(double (&v)[K], double &m, double *scratch) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
-    m = wave_max(m);
-    if constexpr (TB != 64) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < K; ++i) scratch[wave * (K + 1) + i] = v[i];
-            scratch[wave * (K + 1) + K] = m;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            double s = 0.0;
-            for (int w = 0; w < kWaves; ++w) s += scratch[w * (K + 1) + i];
-            v[i] = s;
-        }
-        double mm = scratch[K];
-        for (int w = 1; w < kWaves; ++w) mm = fmax(mm, scratch[w * (K + 1) + K]);
-        m = mm;
-        __syncthreads();
-    }
-}
 template <int K, int TB>
 __device__ __forceinline__ void blk_max(double (&v)[K], double *scratch) {
     if constexpr (TB == 64) {

@@ -1242,11 +1242,6 @@ __device__ __forceinline__ void taylor_seg(const double2 (&mu)[M1 - M0], double 
 #ifndef PPF_TRMOM_WPE
 #define PPF_TRMOM_WPE 2
 #endif
-// evaluate from the first valid moment set with the radius test folded into
-// the evaluation pass (0: the separate test pass first)
-#ifndef PPF_TRMOM_SPEC
-#define PPF_TRMOM_SPEC 1
-#endif
 #ifdef PPF_TM_PROF
 // section cycle counters of k_tr_mom, thread 0 of each workgroup (profiling
 // builds only: tools/tprof.py)
@@ -1269,7 +1264,7 @@ __device__ unsigned long long g_tprof[8];
 template <int TB>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WPE))) void k_tr_mom(SolveArgs a) {
     __shared__ TRState L;
-    __shared__ double red[kWaves * 11];
+    __shared__ double red[kWaves * 10];
     __shared__ int cmdb;
     const int tid = threadIdx.x;
     const int s = blockIdx.x;
@@ -1304,18 +1299,61 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
     if (tid == 0) L.need_mom = 0;
     const int cap = (a.max_iter > 0 ? a.max_iter : 1000) + 4;
     TP(0);
-    // one evaluation from moment set q at the trial point: the channel pass
-    // (f, g, H sums in acc; per-channel stats) and, in xm, max_n h_n |Delta_n|
-    // (the expansion-radius test's quantity, formed from the same Delta_n)
-    auto evaluate = [&](int qs, double e0, double e1, double e2, double (&acc)[10], double &xm,
-                        bool q4) {
-        const double2 *Mq = MOM + (int64_t)qs * a.nchan * kMoments;
-        const double *rq = MRES + (int64_t)qs * a.nchan;
-        const double *hq = HC + (int64_t)qs * a.nchan;
+    for (int it = 0; it < cap; ++it) {
+        __syncthreads();
+        const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
+        // moment set whose centre is within the expansion radius for every channel
+        int qsel = -1;
+        double xsel = 0.0;
+        for (int t = 0; t < 2 && qsel < 0; ++t) {
+            const int cand = t == 0 ? L.macc : 1 - L.macc;
+            if (!L.mvalid[cand]) continue;
+            const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
+            const double *rc = MRES + (int64_t)cand * a.nchan;
+            const double *hc = HC + (int64_t)cand * a.nchan;
+            double xm[1] = {0.0};          // max_n h_n |Delta_n|
+            for (int n0 = 0; n0 < a.nchan; n0 += 4 * TB) {   // 4 channels' loads, then use
+                double v1[4], v2[4], vr[4], vh[4];
+                bool ok[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int n = n0 + tid + TB * j, nc = min(n, a.nchan - 1);
+                    v1[j] = dp[2 * nc]; v2[j] = dp[2 * nc + 1]; vr[j] = rc[nc];
+                    vh[j] = m16 ? hc[nc] : h;
+                    ok[j] = n < a.nchan && (!use_mask || mk[nc] != 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (ok[j]) xm[0] = fmax(xm[0], vh[j] * fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
+            }
+            blk_max<1, TB>(xm, red);
+            if (kTwoPi * xm[0] <= xmax) {
+                qsel = cand;
+                xsel = kTwoPi * xm[0];
+            }
+        }
+        TP(1);
+        if (qsel < 0) {
+            if (tid == 0) {
+                const int tgt = L.mvalid[L.macc] ? 1 - L.macc : L.macc;
+                L.mtarget = tgt;
+                L.mc[tgt][0] = t0; L.mc[tgt][1] = t1; L.mc[tgt][2] = t2;
+                L.mvalid[tgt] = 1;
+                L.need_mom = 1;
+                L.nmom += 1;
+                atomicAdd(a.active, 1u);
+                if (a.rc_list) a.rc_list[atomicAdd(a.rc_count, 1u)] = s;
+            }
+            break;
+        }
+        const double e0 = t0 - L.mc[qsel][0], e1 = t1 - L.mc[qsel][1], e2 = t2 - L.mc[qsel][2];
+        const double2 *Mq = MOM + (int64_t)qsel * a.nchan * kMoments;
+        const double *rq = MRES + (int64_t)qsel * a.nchan;
+        const double *hq = HC + (int64_t)qsel * a.nchan;
         double *st = stats + (int64_t)L.slot_eval * a.nchan * 10;
+        double acc[10];
 #pragma unroll
         for (int i = 0; i < 10; ++i) acc[i] = 0.0;
-        xm = 0.0;
         // channel n = tid + 256 i; its 32 moments come in quarters of 8
         // (8 x 16 B loads), two buffers rotating so that the next quarter is
         // in flight while the current one is summed
@@ -1335,6 +1373,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
             c_h = m16 ? hq[n] : h;
             c_ok = mk[n];
         };
+        const bool q4 = !m16 && xsel > kX24;   // uniform: all 32 moments needed
         ldq(0, 0, qa);
         ldc(0);
         for (int i = 0; i < nit; ++i) {
@@ -1343,7 +1382,6 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
             const bool valid = n < a.nchan && (!use_mask || c_ok != 0);
             const double d1 = c_d1, d2 = c_d2, Sn = c_S, hn_ = c_h;
             const double del = e0 + e1 * d1 + e2 * d2 + c_rq;
-            if (valid) xm = fmax(xm, hn_ * fabs(del));
             const double x = kTwoPi * hn_ * del;
             double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
             double r0 = 1.0, r1 = 0.0, r2 = 0.0;
@@ -1389,101 +1427,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
                 if ((flagmask >> hi[e] & 1) && (flagmask >> hj[e] & 1))
                     acc[4 + e] += hn * dph[hi[e]] * dph[hj[e]];
         }
-    };
-    double xpred = 1e30;                     // last accepted radius (q4 prediction)
-    for (int it = 0; it < cap; ++it) {
-        __syncthreads();
-        const double t0 = L.th[0], t1 = L.th[1], t2 = L.th[2];
-        double acc[10];
-        int qsel = -1;
-        // speculative (PPF_TRMOM_SPEC): evaluate from the first valid moment
-        // set (the one the radius test tries first) and test the radius on
-        // the same pass's Delta_n, one block reduction for both; only when
-        // that set's radius fails does the two-set test run and the
-        // evaluation repeat (then as before).  Same choice of set, same sums:
-        // the results are unchanged.  32-moment sets sum the last quarter
-        // only beyond kX24, predicted from the previous accepted evaluation
-        // (a wrong prediction also takes the two-set path).
-        int spec = -1;
-        if (PPF_TRMOM_SPEC)
-            spec = L.mvalid[L.macc] ? L.macc : (L.mvalid[1 - L.macc] ? 1 - L.macc : -1);
-        bool recentre = false;
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            bool q4;
-            if (spec >= 0) {
-                qsel = spec;
-                q4 = !m16 && xpred > kX24;
-            } else {
-                // moment set whose centre is within the expansion radius for every channel
-                double xsel = 0.0;
-                qsel = -1;
-                for (int t = 0; t < 2 && qsel < 0; ++t) {
-                    const int cand = t == 0 ? L.macc : 1 - L.macc;
-                    if (!L.mvalid[cand]) continue;
-                    const double e0 = t0 - L.mc[cand][0], e1 = t1 - L.mc[cand][1], e2 = t2 - L.mc[cand][2];
-                    const double *rc = MRES + (int64_t)cand * a.nchan;
-                    const double *hc = HC + (int64_t)cand * a.nchan;
-                    double xm[1] = {0.0};          // max_n h_n |Delta_n|
-                    for (int n0 = 0; n0 < a.nchan; n0 += 4 * TB) {   // 4 channels' loads, then use
-                        double v1[4], v2[4], vr[4], vh[4];
-                        bool ok[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int n = n0 + tid + TB * j, nc = min(n, a.nchan - 1);
-                            v1[j] = dp[2 * nc]; v2[j] = dp[2 * nc + 1]; vr[j] = rc[nc];
-                            vh[j] = m16 ? hc[nc] : h;
-                            ok[j] = n < a.nchan && (!use_mask || mk[nc] != 0);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (ok[j]) xm[0] = fmax(xm[0], vh[j] * fabs(e0 + e1 * v1[j] + e2 * v2[j] + vr[j]));
-                    }
-                    blk_max<1, TB>(xm, red);
-                    if (kTwoPi * xm[0] <= xmax) {
-                        qsel = cand;
-                        xsel = kTwoPi * xm[0];
-                    }
-                }
-                TP(1);
-                if (qsel < 0) {
-                    recentre = true;
-                    break;
-                }
-                q4 = !m16 && xsel > kX24;   // uniform: all 32 moments needed
-                xpred = xsel;
-            }
-            const double e0 = t0 - L.mc[qsel][0], e1 = t1 - L.mc[qsel][1], e2 = t2 - L.mc[qsel][2];
-            double xm;
-            evaluate(qsel, e0, e1, e2, acc, xm, q4);
-            TP(2);
-            if (spec >= 0) {
-                blk_sum_max<10, TB>(acc, xm, red);
-                TP(3);
-                const double xs = kTwoPi * xm;
-                if (xs <= xmax && (m16 || (xs > kX24) == q4)) {
-                    xpred = xs;
-                    break;
-                }
-                spec = -1;                    // the two-set test, then evaluate again
-            } else {
-                blk_sum<10, TB>(acc, red);
-                TP(3);
-                break;
-            }
-        }
-        if (recentre) {
-            if (tid == 0) {
-                const int tgt = L.mvalid[L.macc] ? 1 - L.macc : L.macc;
-                L.mtarget = tgt;
-                L.mc[tgt][0] = t0; L.mc[tgt][1] = t1; L.mc[tgt][2] = t2;
-                L.mvalid[tgt] = 1;
-                L.need_mom = 1;
-                L.nmom += 1;
-                atomicAdd(a.active, 1u);
-                if (a.rc_list) a.rc_list[atomicAdd(a.rc_count, 1u)] = s;
-            }
-            break;
-        }
+        TP(2);
+        blk_sum<10, TB>(acc, red);
+        TP(3);
         if (tid == 0) {
             double o[21];
 #pragma unroll
@@ -2033,7 +1979,13 @@ hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
     // of 64 resident ones it spills (256 VGPRs + 324 B scratch) and holds
     // one 512-thread workgroup per CU, so the serial updates no longer
     // overlap other workgroups' evaluations; capped at three waves per SIMD
-    // it spills 670 B and takes 247 ms)
+    // it spills 670 B and takes 247 ms).  Also measured in round 5 and not
+    // kept: the expansion-radius test folded into the evaluation pass
+    // (evaluate from the first valid moment set, one block reduction for
+    // the sums and the radius max, the two-set test only when that fails):
+    // the evaluation as a lambda with two call sites raised the spills from
+    // 30 to 70 VGPRs, 229-232 ms vs 168 ms per 120 C2 calls (with the test
+    // off, the same structure took 209 ms), C4 299-311k vs 330k)
 #ifdef PPF_TRMOM_TB
     const int tb = PPF_TRMOM_TB;
 #else

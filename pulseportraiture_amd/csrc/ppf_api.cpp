@@ -116,7 +116,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 }
 
 struct FitLayout {
-    size_t M, X, chan, stats, x0, gP, gw, Msum, gpart, gwx, gflag, state, partials, active, mom, dphi,
+    size_t M, X, chan, stats, x0, gP, gw, nuref, Msum, gpart, gwx, gflag, state, partials, active, mom, dphi,
         mres, hcen, Mpow, MP, KC, needx, xslot, rclist, Bt, total;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
@@ -167,6 +167,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     if (d->guess) {
         L.gP = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * (size_t)d->nbin);
         L.gw = o; o += align256(sizeof(double) * nsub * (size_t)L.nblkd * 2);
+        L.nuref = o; o += align256(sizeof(double) * nsub);
         L.Msum = o; o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nharm);
         if (L.fused) {   // guess spectrum fused into k_xspec_w (k_gflag)
             const size_t ng = (size_t)ppf::guess_slots(fft_log2(d->nbin / 2));
@@ -501,6 +502,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         da.guess_weights = d->guess_weights;
         da.guess_ref = d->guess_ref; da.nu_fits = d->nu_fits;
         da.gP = (double *)(ws + L.gP); da.gw = (double *)(ws + L.gw);
+        da.nuref = (double *)(ws + L.nuref);
         da.gflag = gflag;
         mark(7);
         if ((e = ppf::launch_dsum(da, st)) != hipSuccess) return hip_fail(ctx, e, "k_dsum");

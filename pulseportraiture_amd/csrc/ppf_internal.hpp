@@ -60,6 +60,8 @@ struct DsumArgs {
     double *gP;                  // [nsub][nblkd][nbin] partial profiles
     double *gw;                  // [nsub][nblkd][2] (sum w, count)
     const uint8_t *gflag;        // [nsub]: 1 = fused into k_xspec_w (skip), or null
+    double *nuref;               // [nsub] nu_ref^-2 per sub-int (k_nu_ref), or null:
+                                 // every workgroup reduces the frequencies itself
 };
 
 // k_xmom: fused re-FFT + cross spectrum + Taylor moments (no X in HBM)

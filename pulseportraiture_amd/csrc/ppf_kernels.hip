@@ -435,6 +435,35 @@ __global__ __launch_bounds__(kBlock) void k_dsum(DsumArgs a) {
     }
 }
 
+// nu_ref^-2 of sub-int s for the wave-per-row guess passes: the mean usable
+// frequency (GetTOAs, pptoas.py:461-464) or nu_fit (ppalign), one wave's
+// fixed-order sum.  At many channels (C5: 16,384) every workgroup of
+// k_dsum_w repeating this over the whole band cost more than its rows'
+// loads, so k_nu_ref forms it once per sub-int (same arithmetic, same bits).
+__device__ __forceinline__ double nu_ref_m2(const DsumArgs &a, int s, int lane) {
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double *fr = a.freqs + (int64_t)s * a.nchan;
+    double v0 = 0.0, v1 = 0.0;
+    for (int n = lane; n < a.nchan; n += 64)
+        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
+    v0 = wave_sum(v0);
+    v1 = wave_sum(v1);
+    const double mu = v0 / v1;
+    double nu_mean_m2 = 1.0 / (mu * mu);
+    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
+        const double nf = a.nu_fits[(int64_t)s * 3];
+        if (nf == nf) nu_mean_m2 = 1.0 / (nf * nf);
+    }
+    return nu_mean_m2;
+}
+
+__global__ __launch_bounds__(64) void k_nu_ref(DsumArgs a) {
+    const int s = blockIdx.x;
+    if (a.gflag && a.gflag[s]) return;
+    const double v = nu_ref_m2(a, s, threadIdx.x);
+    if (threadIdx.x == 0) a.nuref[s] = v;
+}
+
 // ===========================================================================
 // k_dsum_w: k_dsum with one wave per channel row (256 <= nbin <= 2048).
 // Each wave streams its rows (channels c0 + wave + 4 i) with 16-B loads, one
@@ -470,18 +499,8 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     const double *gwt = a.guess_weights + (int64_t)s * a.nchan;
-    double v0 = 0.0, v1 = 0.0;
-    for (int n = lane; n < a.nchan; n += 64)
-        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
-    v0 = wave_sum(v0);
-    v1 = wave_sum(v1);
     const double Dg = (double)NB * kDconst * a.guess_DM[s] / a.P[s];
-    const double mu = v0 / v1;
-    double nu_mean_m2 = 1.0 / (mu * mu);
-    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
-        const double nf = a.nu_fits[(int64_t)s * 3];
-        if (nf == nf) nu_mean_m2 = 1.0 / (nf * nf);
-    }
+    const double nu_mean_m2 = a.nuref ? a.nuref[s] : nu_ref_m2(a, s, lane);
     const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
     const VecT *rows = reinterpret_cast<const VecT *>(a.data) + (int64_t)s * a.nchan * (NB / VW);
     // the block's channel scalars in lane registers (channel c0 + lane + 64 k,
@@ -644,18 +663,8 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     const double *gwt = a.guess_weights + (int64_t)s * a.nchan;
-    double v0 = 0.0, v1 = 0.0;
-    for (int n = lane; n < a.nchan; n += 64)
-        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
-    v0 = wave_sum(v0);
-    v1 = wave_sum(v1);
     const double Dg = (double)nb * kDconst * a.guess_DM[s] / a.P[s];
-    const double mu = v0 / v1;
-    double nu_mean_m2 = 1.0 / (mu * mu);
-    if (a.guess_ref) {                       // ppalign: dedisperse at nu_fit
-        const double nf = a.nu_fits[(int64_t)s * 3];
-        if (nf == nf) nu_mean_m2 = 1.0 / (nf * nf);
-    }
+    const double nu_mean_m2 = a.nuref ? a.nuref[s] : nu_ref_m2(a, s, lane);
     const int c0 = blk * a.cbd, c1 = min(a.nchan, c0 + a.cbd);
     const ElT *rows = reinterpret_cast<const ElT *>(a.data) + (int64_t)s * a.nchan * nb;
     double t_w[2], t_f[2];
@@ -1281,7 +1290,18 @@ static void launch_dsum_w(const DsumArgs &a, hipStream_t st) {
                        lds, st, a);
 }
 
-hipError_t launch_dsum(const DsumArgs &a, hipStream_t st) {
+#ifndef PPF_NUREF
+#define PPF_NUREF 1
+#endif
+hipError_t launch_dsum(const DsumArgs &a_in, hipStream_t st) {
+    DsumArgs a = a_in;
+    // many channels: nu_ref once per sub-int (the wave-per-row kernels read it)
+    if (PPF_NUREF && a.nuref && a.nchan >= 2048 && a.nbin <= 2048 &&
+        (dsum_wave_supported(a.nbin) || PPF_DSUM_WN)) {
+        hipLaunchKernelGGL(k_nu_ref, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
+    } else {
+        a.nuref = nullptr;
+    }
     if (dsum_wave_supported(a.nbin)) {
         switch (__builtin_ctz((unsigned)a.nbin) * 2 + a.dtype) {
             case 16: launch_dsum_w<0, 8>(a, st); break;

@@ -1087,7 +1087,10 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #endif
 // (measured, C2 per 10k sub-ints, same call: KU = 8 6.12 vs 5.76 ms; the
 // loop unrolled by two over two buffers, so that no batch waits for loads it
-// has just issued, 5.77 at KU = 4 and 5.91 at KU = 2: no latency to hide)
+// has just issued, 5.77 at KU = 4 and 5.91 at KU = 2: no latency to hide.
+// Round 5, with the loads unconditional: KU = 2 / 8 5.61-5.77 / 5.70-5.97
+// vs 5.68-5.83 ms; the first two batches requested before the dphi / cutoff
+// loads, 5.83-5.85 vs 5.61-5.65 ms: not kept)
 #ifndef PPF_MOM_KU
 #define PPF_MOM_KU 4
 #endif

@@ -1384,8 +1384,14 @@ __device__ __forceinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, c
 // NMAX: the largest N of the instantiation (512: <= 128 VGPRs, four waves
 // per SIMD; 1024: two), which sizes every stage's register footprint (a
 // lane holds all of its butterflies between the stage's reads and writes)
+// (the LDS of a workgroup -- four row buffers and the twiddles -- admits
+// three of them per CU at NMAX 512 and two at 1024, so the register budget
+// is three / two waves per SIMD)
+#ifndef PPF_WM_PRE
+#define PPF_WM_PRE 1
+#endif
 template <int DT, int NMAX>
-__global__ __launch_bounds__(64 * kWmW) __attribute__((amdgpu_waves_per_eu(NMAX <= 512 ? 4 : 2)))
+__global__ __launch_bounds__(64 * kWmW) __attribute__((amdgpu_waves_per_eu(NMAX <= 512 ? 3 : 2)))
 void k_xspec_wm(XspecArgs a) {
     const int N = a.nbin >> 1, NH = N + 1;
     const int SL = N + 2;                      // [0, N]: Z then X; [N + 1]: 1/errs_FT^2
@@ -1417,11 +1423,38 @@ void k_xspec_wm(XspecArgs a) {
     const double ch_mpow = nl < cend ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
     const double ch_err = (a.errs && nl < cend) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
     const bool two0 = (__builtin_ctz((unsigned)N) & 1) != 0;
+#if PPF_WM_PRE
+    // the wave's next row in registers while this one is transformed
+    // (unconditional loads of a valid row: the prefetch stays in VGPRs)
+    using LT = typename std::conditional<DT == 0, float2, double2>::type;
+    constexpr int PJ = NMAX / 64;
+    LT pre[PJ];
+    auto fetch = [&](int m) {
+        const LT *src = reinterpret_cast<const LT *>(a.data) + ((int64_t)s * a.nchan + m) * (int64_t)N;
+#pragma unroll
+        for (int i = 0; i < PJ; ++i) {
+            const int t = lane + 64 * i;
+            pre[i] = src[t < N ? t : N - 1];
+        }
+    };
+    fetch(min(cbase + wave, cend - 1));
+#endif
     for (int r = 0, n = cbase + wave; r < nround; ++r, n += kWmW) {
         const bool live = usable(n);
         if (n < cend && !live && lane < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane] = 0.0;
+#if PPF_WM_PRE
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < PJ; ++i) {
+                const int t = lane + 64 * i;
+                if (t < N) buf[t] = cmk((double)pre[i].x, (double)pre[i].y);
+            }
+        }
+        fetch(min(n + kWmW, cend - 1));
+#endif
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
+#if !PPF_WM_PRE
             if (DT == 0) {
                 const float2 *src = reinterpret_cast<const float2 *>(a.data) + crow * (int64_t)N;
                 for (int j = lane; j < N; j += 64) {
@@ -1432,6 +1465,7 @@ void k_xspec_wm(XspecArgs a) {
                 const double2 *src = reinterpret_cast<const double2 *>(a.data) + crow * (int64_t)N;
                 for (int j = lane; j < N; j += 64) buf[j] = src[j];
             }
+#endif
             wfft::wave_sync();
             // the stages in fft_radices' order (one 2 when the power of two
             // is odd, 4s, then the odd primes ascending), wave-uniform

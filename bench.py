@@ -943,7 +943,9 @@ def main():
                              ms=stage_ms[1], unit=xfull,
                              bytes=steps_subints * xfull +
                              ncalls * nchan * nharm * 16)
-        mu = xh * 16 + nchan * 16 + nchan * (32 * 16 + 8)
+        # (16 moments per channel about its band centre, and the centre:
+        # ppf_api.cpp PPF_MOM16_BLOCK)
+        mu = xh * 16 + nchan * 16 + nchan * (16 * 16 + 8 + 8)
         kern["moments"] = dict(name="k_moments", ms=kern_ms[0], unit=mu,
                                bytes=steps_subints * mu)
     elif scat_fit or momx_used:
@@ -1094,7 +1096,7 @@ def main():
                 # test's dphi / centre residual: its memory-side rate against
                 # the HBM peak (the sets outgrow the L2s; re-reads of one
                 # sub-int's set within a launch may hit the MALL)
-                nmom = 16 if momx_used else 32
+                nmom = 16 if (momx_used or not wave) else 32
                 bpe = nchan * (nmom * 16 + 40 + 32)
                 mb = steps_subints * mean_nfev * bpe
                 it["memory"] = dict(bytes_per_evaluation=bpe,

@@ -126,6 +126,12 @@ struct FitLayout {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// 16-moment sets on the non-power-of-two shapes too (their moments always
+// come from X): nbin 1000 278-280k -> 293-294k, 1536 178-179k -> 183k fits/s
+// in one call (profiles/r05/ab_m16_status.txt)
+#ifndef PPF_MOM16_BLOCK
+#define PPF_MOM16_BLOCK 1
+#endif
 FitLayout fit_layout(const ppf_fit_desc *d) {
     FitLayout L{};
     const size_t nharm = (size_t)d->nbin / 2 + 1;
@@ -156,7 +162,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
     L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
     L.mres = o;  o += align256(sizeof(double) * nsub * 2 * nchan);
-    L.hcen = o;  o += L.momx ? align256(sizeof(double) * nsub * 2 * nchan) : 0;
+    L.hcen = o;  o += (L.momx || (!L.fused && PPF_MOM16_BLOCK)) ? align256(sizeof(double) * nsub * 2 * nchan) : 0;
     L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.MP = o;    o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
     L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
@@ -559,8 +565,12 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
     sa.mres = (double *)(ws + L.mres);
-    sa.mom16 = L.momx;
-    sa.hcen = L.momx ? (double *)(ws + L.hcen) : nullptr;
+    // 16 moments about each wave's band centre wherever the moments come
+    // from a stored X: the wave shapes' MOM_X path and (PPF_MOM16_BLOCK) the
+    // non-power-of-two shapes
+    const bool m16 = L.momx || (!L.fused && PPF_MOM16_BLOCK);
+    sa.mom16 = m16;
+    sa.hcen = m16 ? (double *)(ws + L.hcen) : nullptr;
     sa.xslot = xslot;
     if (sa.moments) sa.any_plain = 0;      // plain fits go through the moments
     if ((e = ppf::launch_tr_init(sa, st)) != hipSuccess) return hip_fail(ctx, e, "k_tr_init");

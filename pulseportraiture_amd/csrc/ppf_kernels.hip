@@ -444,8 +444,15 @@ __device__ __forceinline__ double nu_ref_m2(const DsumArgs &a, int s, int lane) 
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
     const double *fr = a.freqs + (int64_t)s * a.nchan;
     double v0 = 0.0, v1 = 0.0;
-    for (int n = lane; n < a.nchan; n += 64)
-        if (!mask || mask[n]) { v0 += fr[n]; v1 += 1.0; }
+    // (loads unconditional, so that eight channels' loads are in flight;
+    // adding 0.0 for a masked channel leaves the sums' bits unchanged)
+#pragma unroll 8
+    for (int n = lane; n < a.nchan; n += 64) {
+        const double f = fr[n];
+        const bool ok = !mask || mask[n];
+        v0 += ok ? f : 0.0;
+        v1 += ok ? 1.0 : 0.0;
+    }
     v0 = wave_sum(v0);
     v1 = wave_sum(v1);
     const double mu = v0 / v1;

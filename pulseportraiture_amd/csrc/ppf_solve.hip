@@ -1090,7 +1090,11 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // has just issued, 5.77 at KU = 4 and 5.91 at KU = 2: no latency to hide.
 // Round 5, with the loads unconditional: KU = 2 / 8 5.61-5.77 / 5.70-5.97
 // vs 5.68-5.83 ms; the first two batches requested before the dphi / cutoff
-// loads, 5.83-5.85 vs 5.61-5.65 ms: not kept)
+// loads, 5.83-5.85 vs 5.61-5.65 ms, and with the mask / dphi / cutoff loads
+// issued together before them (one round trip), 5.56-5.58 vs 5.54-5.55 ms:
+// not kept.  The same one-round-trip prologue for k_pass, and unconditional
+// loads in the scattering-gate and k_tr_init channel loops, measured within
+// the noise at C3 / C5 (profiles/r05/ab_ps1_status.txt, ab_gt1_status.txt))
 #ifndef PPF_MOM_KU
 #define PPF_MOM_KU 4
 #endif

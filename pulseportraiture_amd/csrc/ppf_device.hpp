@@ -135,7 +135,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Sum K values per thread over the whole block; result valid in every thread.
 // scratch must hold kWaves*K doubles.  Contains two __syncthreads().
 // Max of K values per thread over the block (same contract as block_sum).
-template <int K>
+template <int K, int NW = kWaves>
 __device__ __forceinline__ void block_max(double (&v)[K], double *scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -148,13 +148,13 @@ __device__ __forceinline__ void block_max(double (&v)[K], double *scratch) {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         double s = scratch[i];
-        for (int w = 1; w < kWaves; ++w) s = fmax(s, scratch[w * K + i]);
+        for (int w = 1; w < NW; ++w) s = fmax(s, scratch[w * K + i]);
         v[i] = s;
     }
     __syncthreads();
 }
 
-template <int K>
+template <int K, int NW = kWaves>
 __device__ __forceinline__ void block_sum(double (&v)[K], double *scratch) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -167,7 +167,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double *scratch) {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         double s = 0.0;
-        for (int w = 0; w < kWaves; ++w) s += scratch[w * K + i];
+        for (int w = 0; w < NW; ++w) s += scratch[w * K + i];
         v[i] = s;
     }
     __syncthreads();
@@ -181,7 +181,7 @@ __device__ __forceinline__ void blk_sum(double (&v)[K], double *scratch) {
 #pragma unroll
         for (int i = 0; i < K; ++i) v[i] = wave_sum(v[i]);
     } else {
-        block_sum<K>(v, scratch);
+        block_sum<K, TB / 64>(v, scratch);
     }
 }
 template <int K, int TB>
@@ -190,7 +190,7 @@ __device__ __forceinline__ void blk_max(double (&v)[K], double *scratch) {
 #pragma unroll
         for (int i = 0; i < K; ++i) v[i] = wave_max(v[i]);
     } else {
-        block_max<K>(v, scratch);
+        block_max<K, TB / 64>(v, scratch);
     }
 }
 

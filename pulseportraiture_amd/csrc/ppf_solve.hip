@@ -1993,12 +1993,18 @@ hipError_t launch_tr_mom(const SolveArgs &a, hipStream_t st) {
     // the evaluation as a lambda with two call sites raised the spills from
     // 30 to 70 VGPRs, 229-232 ms vs 168 ms per 120 C2 calls (with the test
     // off, the same structure took 209 ms), C4 299-311k vs 330k)
+    // Round 5: 128-thread workgroups (two waves, four channels per thread at
+    // 512 channels; four sub-ints per CU instead of two, so more thread-0
+    // updates overlap other workgroups' evaluation passes): C2 k_tr_mom 163
+    // vs 171 ms per 120 calls, C4 332.8-338.6k vs 322.7-330.6k
+    // archive-iterations/s in one call (profiles/r05/ab_tb1_status.txt)
 #ifdef PPF_TRMOM_TB
     const int tb = PPF_TRMOM_TB;
 #else
-    const int tb = 256;
+    const int tb = 128;
 #endif
     if (tb == 64) hipLaunchKernelGGL(k_tr_mom<64>, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
+    else if (tb == 128) hipLaunchKernelGGL(k_tr_mom<128>, dim3((unsigned)a.nsub), dim3(128), 0, st, a);
     else hipLaunchKernelGGL(k_tr_mom<256>, dim3((unsigned)a.nsub), dim3(256), 0, st, a);
     return hipGetLastError();
 }
@@ -2010,6 +2016,7 @@ hipError_t launch_postfit(const SolveArgs &a, hipStream_t st) {
     const int pb = a.nchan <= 2048 ? 64 : 256;
 #endif
     if (pb == 64) hipLaunchKernelGGL(k_postfit<64>, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
+    else if (pb == 128) hipLaunchKernelGGL(k_postfit<128>, dim3((unsigned)a.nsub), dim3(128), 0, st, a);
     else hipLaunchKernelGGL(k_postfit<256>, dim3((unsigned)a.nsub), dim3(256), 0, st, a);
     return hipGetLastError();
 }

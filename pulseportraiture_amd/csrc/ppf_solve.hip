@@ -2015,8 +2015,9 @@ hipError_t launch_postfit(const SolveArgs &a, hipStream_t st) {
 #else
     const int pb = a.nchan <= 2048 ? 64 : 256;
 #endif
+    // (128 threads measured slower in round 5: C2 285.3-286.5k vs 287.6-288.2k, C3
+    // 145.0-146.5k vs 147.7-148.1k, profiles/r05/ab_pf1_status.txt)
     if (pb == 64) hipLaunchKernelGGL(k_postfit<64>, dim3((unsigned)a.nsub), dim3(64), 0, st, a);
-    else if (pb == 128) hipLaunchKernelGGL(k_postfit<128>, dim3((unsigned)a.nsub), dim3(128), 0, st, a);
     else hipLaunchKernelGGL(k_postfit<256>, dim3((unsigned)a.nsub), dim3(256), 0, st, a);
     return hipGetLastError();
 }

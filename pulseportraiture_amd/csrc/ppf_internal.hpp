@@ -297,8 +297,8 @@ hipError_t launch_gflag(int nsub, int nchan, const uint8_t *needx, const int32_t
                         const int32_t *model_index, int klim, uint8_t *gflag, hipStream_t st);
 hipError_t launch_dsum(const DsumArgs &a, hipStream_t st);
 bool xspec_wave_supported(int log2N, int cb);
-// wave-per-row mixed-radix spectrum pass (k_xspec_wm): nbin / 2 smooth, not
-// a power of two, <= 1024
+// wave-per-row mixed-radix spectrum pass (k_xspec_wm): nbin / 2 not a power
+// of two, <= 1024 (prime factors above 7 on the generic-radix stage)
 bool xspec_wm_supported(int nbin);
 // the spectrum pass accumulates the GetTOAs guess at this FFT size (k_gflag)
 bool xspec_guess_fused_n(int log2N);

@@ -1310,8 +1310,8 @@ void k_xspec_w2(XspecArgs a) {
 }
 
 // ===========================================================================
-// k_xspec_wm: the spectrum pass for nbin / 2 = 2^a 3^b 5^c 7^d not a power
-// of two (1000, 1536, 2000 bins ...), N <= 1024 (round 5).  k_xspec_any gave
+// k_xspec_wm: the spectrum pass for nbin / 2 not a power of two (1000, 1022,
+// 1536, 2000 bins ...), N <= 1024 (round 5).  k_xspec_any gave
 // each row to a 256-thread workgroup (a barrier per FFT stage and per
 // block sum; 2 points per thread at 1000 bins) and wrote X one channel per
 // lane, every harmonic.  Here, as k_xspec_w: a 4-wave workgroup takes a

@@ -239,6 +239,12 @@ void k_xspec_w(XspecArgs a) {
     auto usable = [&](int n) {
         return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
     };
+    // |M|^2 sum and sigma of channel cbase + lane in lane registers, read by
+    // readlane per row (round 5, as k_xspec_w2): their global loads in the
+    // row loop came after the next row's prefetch, and vmcnt counts in order
+    const int nlr = cbase + lane;
+    const double ch_mpow = nlr < cend ? a.Mpow[(int64_t)mi * a.nchan + nlr] : 0.0;
+    const double ch_err = (a.errs && nlr < cend) ? a.errs[(int64_t)s * a.nchan + nlr] : 0.0;
     // fused guess: per-lane channel weight and dedispersion phase of
     // channel cbase + lane; the workgroup sum G[1..NL) after the twiddles
     constexpr int NL = 64 * guess_npl(LOG2N);
@@ -388,7 +394,7 @@ void k_xspec_w(XspecArgs a) {
             pn = wave_sum(pn);
             pd = wave_sum(pd);
             double errs_FT;
-            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            if (a.errs) errs_FT = readlane_d(ch_err, n - cbase) * sqrtN;
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
             if (GS && gon) {
@@ -402,7 +408,7 @@ void k_xspec_w(XspecArgs a) {
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
                 chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+                chan[3] = readlane_d(ch_mpow, n - cbase) * inv_e2;     // S_n at tau = 0
             }
 #else
             preload_m();
@@ -435,7 +441,7 @@ void k_xspec_w(XspecArgs a) {
             pn = wave_sum(pn);
             pd = wave_sum(pd);
             double errs_FT;
-            if (a.errs) errs_FT = a.errs[crow] * sqrtN;
+            if (a.errs) errs_FT = readlane_d(ch_err, n - cbase) * sqrtN;
             else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
 
@@ -502,7 +508,7 @@ void k_xspec_w(XspecArgs a) {
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
                 chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = a.Mpow[(int64_t)mi * a.nchan + n] * inv_e2;   // S_n at tau = 0
+                chan[3] = readlane_d(ch_mpow, n - cbase) * inv_e2;     // S_n at tau = 0
             }
 #endif
         }

@@ -17,9 +17,10 @@
  *   - Return value: PPF_OK (0) or a negative PPF_E* code; ppf_last_error()
  *     gives the message.  Per-sub-integration numerical outcomes are reported
  *     in ppf_result.status, never by aborting the batch.
- *   - nbin: even, 32 <= nbin <= 8192 (nbin/2 not a power of two: the
- *     mixed-radix LDS FFT, a generic-radix stage for prime factors above 7);
- *     odd nbin or nbin > 8192 returns PPF_EUNSUP.  Powers of two
+ *   - nbin: even 32..8192 or odd 33..4095 (nbin/2 not a power of two: the
+ *     mixed-radix LDS FFT, a generic-radix stage for prime factors above 7;
+ *     odd nbin: the row transformed as nbin complex points on the same
+ *     stages); other nbin returns PPF_EUNSUP.  Powers of two
  *     in [256, 2048] take the wave-per-row kernels.
  *   - Threads: ppf_fit_batch / ppf_fit2_batch must not run concurrently on
  *     the same context (they share its profiling event ring and pinned

@@ -67,11 +67,12 @@ bool pow2_in_range(int nbin) {
     return nbin >= 32 && nbin <= 8192 && (nbin & (nbin - 1)) == 0;
 }
 
-// nbin the FFT kernels take: even, 32..8192 (power-of-two nbin on the
-// register / radix-4 paths, the others on the mixed-radix LDS FFT, whose
-// generic-radix stage takes prime factors of nbin / 2 above 7)
+// nbin the FFT kernels take: even 32..8192 and odd 33..4095 (power-of-two
+// nbin on the register / radix-4 paths, the others on the mixed-radix LDS
+// FFT, whose generic-radix stage takes prime factors above 7; odd nbin as a
+// full-length complex transform of the row, ppf::rfft_len)
 bool nbin_supported(int nbin) {
-    return nbin >= 32 && nbin <= 8192 && (nbin & 1) == 0 && ppf::fft_len_supported(nbin / 2);
+    return nbin >= 32 && nbin <= 8192 && ppf::fft_len_supported(ppf::rfft_len(nbin));
 }
 
 // log2 of a power-of-two FFT length, 0 otherwise (the kernels' "not a power
@@ -82,6 +83,9 @@ int fft_log2(int n) {
     while ((1 << l) < n) ++l;
     return l;
 }
+
+// fft_log2 of the real-row transform: 0 (mixed-radix LDS FFT) for odd nbin
+int rfft_log2(int nbin) { return (nbin & 1) ? 0 : fft_log2(nbin / 2); }
 
 int ilog2(int n) {
     int l = 0;
@@ -98,7 +102,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
     std::lock_guard<std::mutex> lock(ctx->tw_mu);
     auto it = ctx->tw.find(nbin);
     if (it == ctx->tw.end()) {
-        const int N = nbin / 2;
+        const int N = ppf::rfft_len(nbin);
         double2 *p = nullptr;
         hipError_t e = hipMalloc(&p, sizeof(double2) * 2 * (size_t)N);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(twiddles)");
@@ -111,7 +115,7 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
         it = ctx->tw.emplace(nbin, p).first;
     }
     *T = it->second;
-    *T2 = it->second + nbin / 2;
+    *T2 = it->second + ppf::rfft_len(nbin);
     return PPF_OK;
 }
 
@@ -138,11 +142,11 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     const size_t nsub = (size_t)d->nsub, nchan = (size_t)d->nchan;
     L.cb = d->nchan < 32 ? d->nchan : 32;
     L.nblk = (d->nchan + L.cb - 1) / L.cb;
-    L.fused = ppf::xspec_wave_supported(fft_log2(d->nbin / 2), L.cb) ? 1 : 0;
+    L.fused = ppf::xspec_wave_supported(rfft_log2(d->nbin), L.cb) ? 1 : 0;
     // moments from X: on request, or by default where the GetTOAs guess is
     // fused into the spectrum pass (1024-point rows): there the X pass
     // replaces both the guess pass (k_dsum) and k_xmom_g's re-FFT
-    const bool mom_auto = d->guess && fft_log2(d->nbin / 2) == 10;
+    const bool mom_auto = d->guess && rfft_log2(d->nbin) == 10;
     L.momx = (L.fused && !(d->options & PPF_OPT_FUSED_MOM) &&
               ((d->options & PPF_OPT_MOM_X) || mom_auto)) ? 1 : 0;
     L.xcap = (L.fused && d->x_subints > 0 && d->x_subints < d->nsub) ? d->x_subints : d->nsub;
@@ -176,7 +180,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
         L.nuref = o; o += align256(sizeof(double) * nsub);
         L.Msum = o; o += align256(sizeof(double2) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nharm);
         if (L.fused) {   // guess spectrum fused into k_xspec_w (k_gflag)
-            const size_t ng = (size_t)ppf::guess_slots(fft_log2(d->nbin / 2));
+            const size_t ng = (size_t)ppf::guess_slots(rfft_log2(d->nbin));
             L.gpart = o; o += align256(sizeof(double2) * nsub * (size_t)L.nblk * ng);
             L.gwx = o;   o += align256(sizeof(double) * nsub * (size_t)L.nblk * 3);
             L.gflag = o; o += align256(nsub);
@@ -191,7 +195,7 @@ int check_fit_desc(ppf_ctx *ctx, const ppf_fit_desc *d) {
     if (d->nsub < 1 || d->nchan < 1) return fail(ctx, PPF_EINVAL, "nsub=%d nchan=%d", d->nsub, d->nchan);
     if (!nbin_supported(d->nbin))
         return fail(ctx, PPF_EUNSUP,
-                    "nbin=%d: must be even, in [32, 8192]", d->nbin);
+                    "nbin=%d: must be even in [32, 8192] or odd in [33, 4095]", d->nbin);
     if (d->data_dtype != PPF_F32 && d->data_dtype != PPF_F64)
         return fail(ctx, PPF_EINVAL, "data_dtype=%d", d->data_dtype);
     if (d->nmodel < 1) return fail(ctx, PPF_EINVAL, "nmodel=%d", d->nmodel);
@@ -417,7 +421,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ctx->ran[slot][2] = d->guess != 0;
     ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
-    ppf::RfftArgs ra{d->nbin, fft_log2(d->nbin / 2), PPF_F64, d->model, T, T2, Mft};
+    ppf::RfftArgs ra{d->nbin, rfft_log2(d->nbin), PPF_F64, d->model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_rfft_rows");
     double *Mpow = (double *)(ws + L.Mpow);
@@ -442,9 +446,9 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // fused guess: the sub-ints k_xspec_w streams whose mean-model cutoff
     // fits its guess harmonics accumulate the guess spectrum there
     uint8_t *gflag = nullptr;
-    if (d->guess && L.fused && ppf::xspec_guess_fused_n(fft_log2(d->nbin / 2))) {
+    if (d->guess && L.fused && ppf::xspec_guess_fused_n(rfft_log2(d->nbin))) {
         gflag = (uint8_t *)(ws + L.gflag);
-        const int klim = 64 * ppf::guess_npl(fft_log2(d->nbin / 2));
+        const int klim = 64 * ppf::guess_npl(rfft_log2(d->nbin));
         if ((e = ppf::launch_gflag(d->nsub, d->nchan, needx, (const int32_t *)(ws + L.KC),
                                    d->model_index, klim, gflag, st)) != hipSuccess)
             return hip_fail(ctx, e, "k_gflag");
@@ -452,7 +456,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     mark(1);
 
     ppf::XspecArgs xa{};
-    xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = fft_log2(d->nbin / 2);
+    xa.nsub = d->nsub; xa.nchan = d->nchan; xa.nbin = d->nbin; xa.log2N = rfft_log2(d->nbin);
     xa.kc = kc; xa.nblk = L.nblk; xa.cb = L.cb; xa.dtype = d->data_dtype;
     // k_xspec_w: channel-block-major (mode 2) when the model spectra
     // outgrow the L2s, sub-int-major otherwise; k_xmom_g stages its model
@@ -518,7 +522,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         if ((e = ppf::launch_model_sum(Mft, d->nchan, nharm, d->nmodel, msum, st)) != hipSuccess)
             return hip_fail(ctx, e, "k_model_sum");
         ppf::GuessArgs ga{};
-        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = fft_log2(d->nbin / 2);
+        ga.nsub = d->nsub; ga.nchan = d->nchan; ga.nbin = d->nbin; ga.log2N = rfft_log2(d->nbin);
         ga.kc = kc; ga.nblkd = L.nblkd; ga.Ns = d->guess_Ns; ga.mask = d->chan_mask;
         ga.guess_ref = d->guess_ref;
         ga.freqs = d->freqs; ga.P = d->P; ga.guess_DM = d->guess_DM; ga.guess_tau = d->guess_tau;
@@ -700,7 +704,7 @@ int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::RotateArgs a{nbin, fft_log2(nbin / 2), in_dtype, in, phases, T, T2, out};
+    ppf::RotateArgs a{nbin, rfft_log2(nbin), in_dtype, in, phases, T, T2, out};
     if ((e = ppf::launch_rotate(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_rotate");
     return PPF_OK;
 }
@@ -732,7 +736,7 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
     ppf::AlignArgs a{};
-    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = in_dtype;
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = rfft_log2(nbin); a.dtype = in_dtype;
     a.ngroup = ppf::align_groups(nsub, nchan);
     a.in = in; a.phases = phases; a.weights = weights; a.T = T; a.T2 = T2;
     char *ws = (char *)workspace;
@@ -761,7 +765,7 @@ int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_d
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::ResidArgs a{nbin, fft_log2(nbin / 2), in_dtype, in, phases, model, model_row, scales, errs,
+    ppf::ResidArgs a{nbin, rfft_log2(nbin), in_dtype, in, phases, model, model_row, scales, errs,
                      dof, T, T2, out};
     if ((e = ppf::launch_resid_chi2(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_resid_chi2");
     return PPF_OK;
@@ -781,7 +785,7 @@ int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::NoiseArgs a{nbin, fft_log2(nbin / 2), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
+    ppf::NoiseArgs a{nbin, rfft_log2(nbin), in_dtype, noise_kc(nbin / 2 + 1, frac), in, T, T2, out};
     if (ppf::noise_wave_supported(a.log2N)) {
         if ((e = ppf::launch_noise_wave(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_noise_w");
     } else if ((e = ppf::launch_noise(a, nrows, st)) != hipSuccess) {
@@ -882,7 +886,7 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
     ppf::PhaseShiftArgs a{};
-    a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
+    a.nbin = nbin; a.log2N = rfft_log2(nbin); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
     a.Ns = Ns; a.lo = lo; a.hi = hi; a.data = data; a.model = model; a.model_index = model_index;
     a.noise = noise; a.T = T; a.T2 = T2; a.out = out;
     if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
@@ -914,10 +918,12 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2);
+    a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = rfft_log2(nbin);
     a.ngauss = ngauss; a.npar = 2 + 6 * ngauss;
     a.params = params; a.scat_index = scattering_index; a.freqs = freqs; a.nu_ref = nu_ref;
     a.T = T; a.T2 = T2; a.out = out;
+    a.Te = T; a.T2e = T2;
+    if ((nbin & 1) && (rc = twiddles(ctx, nbin - 1, st, &a.Te, &a.T2e))) return rc;
     if ((e = ppf::launch_gauss_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_gauss_port");
     return PPF_OK;
 }
@@ -943,7 +949,7 @@ int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_
     ppf::SplineArgs a{};
     a.nport = nport; a.nchan = nchan; a.nbin_model = nbin_model; a.nbin = nbin; a.ncomp = ncomp;
     a.nknots = nknots; a.degree = degree;
-    a.log2N0 = fft_log2(nbin_model / 2); a.log2N1 = fft_log2(nbin / 2);
+    a.log2N0 = fft_log2(nbin_model / 2); a.log2N1 = rfft_log2(nbin);
     a.mean_prof = mean_prof; a.eigvec = eigvec; a.knots = knots; a.coefs = coefs; a.freqs = freqs;
     a.out = out;
     int rc;
@@ -976,10 +982,10 @@ int ppf_synth_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, con
     const size_t nharm = (size_t)nbin / 2 + 1;
     e = hipMallocAsync((void **)&Mft, sizeof(double2) * nchan * nharm, st);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMallocAsync(synth)");
-    ppf::RfftArgs ra{nbin, fft_log2(nbin / 2), PPF_F64, model, T, T2, Mft};
+    ppf::RfftArgs ra{nbin, rfft_log2(nbin), PPF_F64, model, T, T2, Mft};
     if ((e = ppf::launch_rfft_rows(ra, nchan, st)) != hipSuccess) return hip_fail(ctx, e, "k_rfft_rows");
     ppf::SynthArgs a{};
-    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = fft_log2(nbin / 2); a.dtype = out_dtype;
+    a.nsub = nsub; a.nchan = nchan; a.nbin = nbin; a.log2N = rfft_log2(nbin); a.dtype = out_dtype;
     a.Mft = Mft; a.freqs = freqs; a.phi = phi; a.DM = DM; a.P = P; a.nu_ref = nu_ref;
     a.noise = noise; a.seed = seed; a.first = first_sub; a.T = T; a.T2 = T2; a.out = out;
     if ((e = ppf::launch_synth(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_synth");

@@ -307,6 +307,11 @@ __host__ __device__ inline bool fft_len_smooth(int N) {
 }
 __host__ __device__ inline bool fft_len_supported(int N) { return N >= 2 && N <= kMaxFftN; }
 __host__ __device__ inline bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+// Complex FFT length of a real row of nbin samples: even nbin packs
+// z_j = x_2j + i x_2j+1 into nbin / 2 points (rfft_bin / irfft_prebin); odd
+// nbin transforms the row itself, nbin points with zero imaginary parts
+// (X_k = Z_k for k <= nbin / 2, the inverse from the Hermitian-filled buffer)
+__host__ __device__ inline int rfft_len(int nbin) { return (nbin & 1) ? nbin : nbin >> 1; }
 
 // cos / sin (2 pi m / R), m < R, for the odd radices (exact decimal expansions)
 __device__ constexpr double kCos3[3] = {1.0, -0.5, -0.5};

@@ -264,7 +264,8 @@ struct GaussArgs {
     const double *freqs;         // [nport][nchan]
     const double *nu_ref;        // [nport]
     const double2 *T, *T2;
-    double *out;                 // [nport][nchan][nbin]
+    const double2 *Te, *T2e;     // odd nbin: the twiddles of nbin - 1 (the scattered rows' irfft)
+    double *out;                 // [nport][nchan][nbin] (odd nbin, tau != 0: nbin - 1 bins, then 0)
 };
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st);
 

@@ -21,11 +21,22 @@
 namespace ppf {
 
 // ===========================================================================
-// common row loading: z_j = x_{2j} + i x_{2j+1}
+// common row loading: z_j = x_{2j} + i x_{2j+1} (even nbin); z_j = x_j + 0 i
+// (odd nbin, rfft_len)
 // ===========================================================================
 __device__ __forceinline__ void load_row(double2 *buf, const void *src, int dtype, int64_t row,
                                          int nbin) {
     const int N = nbin >> 1;
+    if (nbin & 1) {
+        if (dtype == 0) {
+            const float *s = reinterpret_cast<const float *>(src) + row * (int64_t)nbin;
+            for (int j = threadIdx.x; j < nbin; j += kBlock) buf[j] = cmk((double)s[j], 0.0);
+        } else {
+            const double *s = reinterpret_cast<const double *>(src) + row * (int64_t)nbin;
+            for (int j = threadIdx.x; j < nbin; j += kBlock) buf[j] = cmk(s[j], 0.0);
+        }
+        return;
+    }
     if (dtype == 0) {
         const float2 *s = reinterpret_cast<const float2 *>(src) + row * (int64_t)N;
         for (int j = threadIdx.x; j < N; j += kBlock) {
@@ -36,6 +47,18 @@ __device__ __forceinline__ void load_row(double2 *buf, const void *src, int dtyp
         const double2 *s = reinterpret_cast<const double2 *>(src) + row * (int64_t)N;
         for (int j = threadIdx.x; j < N; j += kBlock) buf[j] = s[j];
     }
+}
+
+// X_k (k <= nbin / 2) of the row load_row + lds_fft_n(rfft_len(nbin)) left in buf
+__device__ __forceinline__ double2 rbin(const double2 *buf, int nbin, const double2 *__restrict__ T2, int k) {
+    return (nbin & 1) ? buf[k] : rfft_bin(buf, nbin >> 1, T2, k);
+}
+// odd nbin: Y_k (k <= nbin / 2) into the Hermitian full-length buffer of the
+// inverse transform, whose real part is then the row (the imaginary part of
+// Y_0 drops out, as numpy.fft.irfft ignores it)
+__device__ __forceinline__ void herm_put(double2 *buf, int nbin, int k, double2 Y) {
+    buf[k] = Y;
+    if (k) buf[nbin - k] = cconj(Y);
 }
 
 // ===========================================================================
@@ -61,9 +84,9 @@ __global__ __launch_bounds__(kBlock) void k_rfft_rows(RfftArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, false);
     double2 *o = a.out + row * (int64_t)(N + 1);
-    for (int k = threadIdx.x; k <= N; k += kBlock) o[k] = rfft_bin(lds, N, a.T2, k);
+    for (int k = threadIdx.x; k <= N; k += kBlock) o[k] = rbin(lds, a.nbin, a.T2, k);
 }
 
 // ===========================================================================
@@ -207,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
     const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double sqrt_half_nbin = sqrt((double)(2 * N) / 2.0);
+    const double sqrt_half_nbin = sqrt((double)a.nbin / 2.0);
     for (int n = c0; n < c1; ++n) {
         const int64_t crow = (int64_t)s * a.nchan + n;
         if (mask && !mask[n]) {
@@ -216,17 +239,17 @@ __global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
         }
         load_row(lds, a.data, DT, crow, a.nbin);
         __syncthreads();
-        lds_fft_n(lds, N, a.T, false);
+        lds_fft_n(lds, rfft_len(a.nbin), a.T, false);
         double acc[2] = {0.0, 0.0};
         for (int k = tid; k <= N; k += kBlock) {
-            const double p2 = cabs2(rfft_bin(lds, N, a.T2, k));
+            const double p2 = cabs2(rbin(lds, a.nbin, a.T2, k));
             if (k >= a.kc) acc[0] += p2;
             if (k >= 1) acc[1] += p2;
         }
         block_sum<2>(acc, red);
         double errs_FT;
         if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
-        else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)(2 * N)) * sqrt_half_nbin;
+        else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)a.nbin) * sqrt_half_nbin;
         const double inv_e2 = 1.0 / (errs_FT * errs_FT);
         double2 *Xrow = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan + n;
         const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
@@ -237,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
             } else {
                 const double2 M = Mrow[k];
                 mpow[0] += cabs2(M);
-                Xrow[(int64_t)k * a.nchan] = cscale(cmulc(rfft_bin(lds, N, a.T2, k), M), inv_e2);
+                Xrow[(int64_t)k * a.nchan] = cscale(cmulc(rbin(lds, a.nbin, a.T2, k), M), inv_e2);
             }
         }
         block_sum<1>(mpow, red);          // (its barriers also end this row's reads)
@@ -766,11 +789,12 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 // ===========================================================================
 template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
-    // lds: z[N] (packed profile, FFT in place) | xm[N+1] | sh[Ns+8]
+    // lds: z[rfft_len] (packed profile, FFT in place) | xm[N+1] | sh[Ns+8]
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const int N = a.nbin >> 1, nharm = N + 1, s = blockIdx.x, tid = threadIdx.x;
-    double2 *z = lds, *xm = lds + N;
+    const bool odd = a.nbin & 1;
+    double2 *z = lds, *xm = lds + rfft_len(a.nbin);
     double *sh = reinterpret_cast<double *>(xm + nharm + 1);
     // fused (k_xspec_w accumulated the guess spectrum of its rows in the
     // Fourier domain): the block partials of the covered harmonics
@@ -795,7 +819,13 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     if (!fused) {
         // weighted dedispersed profile: sum of the k_dsum block partials
         // (fixed order), packed z_j = p_2j + i p_2j+1 for the real FFT
-        for (int j = tid; j < N; j += kBlock) {
+        // (odd nbin: z_j = p_j)
+        for (int j = tid; odd && j < a.nbin; j += kBlock) {
+            double pj = 0.0;
+            for (int b = 0; b < a.nblkd; ++b) pj += a.gP[((int64_t)s * a.nblkd + b) * a.nbin + j];
+            z[j] = cmk(pj, 0.0);
+        }
+        for (int j = tid; !odd && j < N; j += kBlock) {
             double pe = 0.0, po = 0.0;
             for (int b = 0; b < a.nblkd; ++b) {
                 const double *pp = a.gP + ((int64_t)s * a.nblkd + b) * a.nbin;
@@ -807,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     }
     __syncthreads();
     const double wsum = sh[0], cnt = sh[1];
-    if (!fused) lds_fft_n<MX>(z, a.nbin >> 1, a.T, false);
+    if (!fused) lds_fft_n<MX>(z, rfft_len(a.nbin), a.T, false);
     // R_k of the fused partials (k < NL; 0 above: past every channel's cutoff)
     auto fused_bin = [&](int k) {
         double2 r = cmk(0.0, 0.0);
@@ -853,14 +883,14 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
             }
         }
         if (!kv || k >= kloop) continue;
-        double2 R = cscale(fused ? fused_bin(k) : rfft_bin(z, N, a.T2, k), 1.0 / wsum);
+        double2 R = cscale(fused ? fused_bin(k) : rbin(z, a.nbin, a.T2, k), 1.0 / wsum);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
             double u = kTwoPi * (double)k * a.guess_tau[s];
             double dd = 1.0 / fma(u, u, 1.0);
             M = cmul(M, cmk(dd, -u * dd));
         }
-        if (k == N) R.y = 0.0;   // irfft drops the imaginary Nyquist part
+        if (k == N && !odd) R.y = 0.0;   // irfft drops the imaginary Nyquist part
         if (k >= a.kc) pw[0] += cabs2(R);
         xm[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(R, M);
     }
@@ -902,21 +932,23 @@ template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
+    const bool odd = a.nbin & 1;
+    const int KH = odd ? N + 1 : N;        // harmonic slots: k < KH
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
-    // harmonics handled by this thread: k = tid + 256 i, k < N (pre-pass pairs k, N-k)
+    // harmonics handled by this thread: k = tid + 256 i, k < N (pre-pass
+    // pairs k, N-k); odd nbin: k <= N, no pairs
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         int k = threadIdx.x + i * kBlock;
-        if (k < N) {
-            double2 X1 = rfft_bin(lds, N, a.T2, k);
-            double2 X2 = rfft_bin(lds, N, a.T2, N - k);
-            X1 = cmul(X1, cexp2pi((double)k * ph));
-            X2 = cmul(X2, cexp2pi((double)(N - k) * ph));
+        if (k < KH) {
+            double2 X1 = cmul(rbin(lds, a.nbin, a.T2, k), cexp2pi((double)k * ph));
+            double2 X2 = cmk(0.0, 0.0);
+            if (!odd) X2 = cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
             if (k == 0) { X1.y = 0.0; X2.y = 0.0; }   // DC and Nyquist: real parts only
             Xk[i] = X1;
             Xn[i] = X2;
@@ -926,10 +958,19 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         int k = threadIdx.x + i * kBlock;
-        if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        if (k < KH) {
+            if (odd) herm_put(lds, a.nbin, k, Xk[i]);
+            else lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        }
     }
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, true);
+    if (odd) {
+        const double sc = 1.0 / (double)a.nbin;
+        double *o = reinterpret_cast<double *>(a.out) + row * (int64_t)a.nbin;
+        for (int j = threadIdx.x; j < a.nbin; j += kBlock) o[j] = lds[j].x * sc;
+        return;
+    }
     const double sc = 1.0 / (double)N;
     double2 *o = reinterpret_cast<double2 *>(a.out) + row * (int64_t)N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
@@ -946,9 +987,9 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, false);
     double acc[1] = {0.0};
-    for (int k = threadIdx.x + a.kc; k <= N; k += kBlock) acc[0] += cabs2(rfft_bin(lds, N, a.T2, k));
+    for (int k = threadIdx.x + a.kc; k <= N; k += kBlock) acc[0] += cabs2(rbin(lds, a.nbin, a.T2, k));
     block_sum<1>(acc, red);
     if (threadIdx.x == 0) a.out[row] = sqrt(acc[0] / (double)a.nbin / (double)(N + 1 - a.kc));
 }
@@ -958,30 +999,31 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
 // ===========================================================================
 template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];   // [N] fft | [N+1] xm | sh
+    // [rfft_len] fft | [N+1] xm | sh
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
-    const int N = a.nbin >> 1, nharm = N + 1;
-    double *sh = reinterpret_cast<double *>(lds + 2 * N + 2);
+    const int N = a.nbin >> 1, nharm = N + 1, NF = rfft_len(a.nbin);
+    double *sh = reinterpret_cast<double *>(lds + NF + N + 2);
     const int64_t prof = blockIdx.x;
-    double2 *fbuf = lds, *xm = lds + N;
+    double2 *fbuf = lds, *xm = lds + NF;
     // model spectrum first (into xm as M_k)
     const int mi = a.model_index ? a.model_index[prof] : 0;
     load_row(fbuf, a.model, 1, mi, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(fbuf, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(fbuf, NF, a.T, false);
     double pp[1] = {0.0};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
-        double2 M = rfft_bin(fbuf, N, a.T2, k);
+        double2 M = rbin(fbuf, a.nbin, a.T2, k);
         xm[k] = M;
         if (k >= 1) pp[0] += cabs2(M);
     }
     __syncthreads();
     load_row(fbuf, a.data, a.dtype, prof, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(fbuf, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(fbuf, NF, a.T, false);
     double acc[3] = {0.0, 0.0, pp[0]};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
-        double2 D = rfft_bin(fbuf, N, a.T2, k);
+        double2 D = rbin(fbuf, a.nbin, a.T2, k);
         double p2 = cabs2(D);
         if (k >= a.kc) acc[0] += p2;
         if (k >= 1) acc[1] += p2;
@@ -1047,6 +1089,28 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
     // phase of this row: rotate_data(model, -phi, -DM, P, freq, nu_ref)
     const double D = kDconst * (-a.DM[s]) / a.P[s];
     const double ph = -a.phi[s] + D * (pow(a.freqs[n], -2.0) - pow(a.nu_ref, -2.0));
+    const int64_t row = (int64_t)s * a.nchan + n;
+    if (a.nbin & 1) {      // odd nbin: Hermitian full-length inverse, one normal deviate per bin
+        for (int k = threadIdx.x; k <= N; k += kBlock) {
+            double2 X = cmul(Mrow[k], cexp2pi((double)k * ph));
+            if (k == 0) X.y = 0.0;
+            herm_put(lds, a.nbin, k, X);
+        }
+        __syncthreads();
+        lds_fft_n<MX>(lds, a.nbin, a.T, true);
+        const double sc = 1.0 / (double)a.nbin;
+        for (int j = threadIdx.x; j < a.nbin; j += kBlock) {
+            const uint64_t grow = (uint64_t)(a.first + s) * (uint64_t)a.nchan + (uint64_t)n;
+            uint64_t h = splitmix64(a.seed ^ splitmix64(grow * 0x100000001B3ull + (uint64_t)j));
+            double u1 = u01(h), u2 = u01(splitmix64(h));
+            double sn, cs;
+            sincospi(2.0 * u2, &sn, &cs);
+            const double z = lds[j].x * sc + a.noise * sqrt(-2.0 * log(u1)) * cs;
+            if (a.dtype == 0) reinterpret_cast<float *>(a.out)[row * a.nbin + j] = (float)z;
+            else reinterpret_cast<double *>(a.out)[row * a.nbin + j] = z;
+        }
+        return;
+    }
     for (int k = threadIdx.x; k < N; k += kBlock) {
         double2 X1 = cmul(Mrow[k], cexp2pi((double)k * ph));
         double2 X2 = cmul(Mrow[N - k], cexp2pi((double)(N - k) * ph));
@@ -1056,7 +1120,6 @@ __global__ __launch_bounds__(kBlock) void k_synth(SynthArgs a) {
     __syncthreads();
     lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
     const double sc = 1.0 / (double)N;
-    const int64_t row = (int64_t)s * a.nchan + n;
     for (int j = threadIdx.x; j < N; j += kBlock) {
         const uint64_t grow = (uint64_t)(a.first + s) * (uint64_t)a.nchan + (uint64_t)n;
         uint64_t h = splitmix64(a.seed ^ splitmix64(grow * 0x100000001B3ull + (uint64_t)j));
@@ -1176,18 +1239,36 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
     if (tau != 0.0) {
         // taus = (tau / nbin) * (freqs / nu_ref)**alpha; B_k = 1 / (1 + 2 pi i k tau_n)
         const double tn = tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]);
+        const bool odd = nbin & 1;
+        const int KH = odd ? N + 1 : N;
         __syncthreads();
-        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+        if (odd) {
+            // the real row (doubles) -> complex points in place: all reads first
+            double v[2 * KMAX];
+#pragma unroll
+            for (int i = 0; i < 2 * KMAX; ++i) {
+                const int j = threadIdx.x + i * kBlock;
+                if (j < nbin) v[i] = row[j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 2 * KMAX; ++i) {
+                const int j = threadIdx.x + i * kBlock;
+                if (j < nbin) lds[j] = cmk(v[i], 0.0);
+            }
+            __syncthreads();
+        }
+        lds_fft_n<MX>(lds, rfft_len(nbin), a.T, false);
         double2 Xk[KMAX], Xn[KMAX];
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
             const int k = threadIdx.x + i * kBlock;
-            if (k < N) {
-                double2 X1 = rfft_bin(lds, N, a.T2, k);
-                double2 X2 = rfft_bin(lds, N, a.T2, N - k);
+            if (k < KH) {
+                double2 X1 = rbin(lds, nbin, a.T2, k);
+                double2 X2 = odd ? cmk(0.0, 0.0) : rfft_bin(lds, N, a.T2, N - k);
                 if (tn != 0.0) {
                     X1 = cmul(X1, scat_recip((2.0 * kPi * (double)k) * tn));
-                    X2 = cmul(X2, scat_recip((2.0 * kPi * (double)(N - k)) * tn));
+                    if (!odd) X2 = cmul(X2, scat_recip((2.0 * kPi * (double)(N - k)) * tn));
                 }
                 if (k == 0) { X1.y = 0.0; X2.y = 0.0; }   // irfft keeps DC, Nyquist real parts
                 Xk[i] = X1;
@@ -1195,19 +1276,62 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
             }
         }
         __syncthreads();
+        if (odd) {
+            // the reference's irfft takes no length (pplib.py:957): 2 N =
+            // nbin - 1 bins from X_0..X_N, X_N as the Nyquist term (its
+            // imaginary part dropped); the even-length packed inverse with
+            // the nbin - 1 twiddles, the row's last column zero
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) {
+                const int k = threadIdx.x + i * kBlock;
+                if (k < KH) lds[k] = Xk[i];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) {
+                const int k = threadIdx.x + i * kBlock;
+                if (k < N) {
+                    Xk[i] = lds[k];
+                    Xn[i] = lds[N - k];
+                    if (k == 0) Xn[i].y = 0.0;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) {
+                const int k = threadIdx.x + i * kBlock;
+                if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2e[k]);
+            }
+            __syncthreads();
+            lds_fft_n<MX>(lds, N, a.Te, true);
+            const double sc = 1.0 / (double)N;
+            double *o = a.out + (int64_t)blockIdx.x * nbin;
+            for (int j = threadIdx.x; j < N; j += kBlock) {
+                const double2 z = cscale(lds[j], sc);
+                o[2 * j] = z.x;
+                o[2 * j + 1] = z.y;
+            }
+            if (threadIdx.x == 0) o[nbin - 1] = 0.0;
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
             const int k = threadIdx.x + i * kBlock;
-            if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+            if (k < KH) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
         }
         __syncthreads();
-        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
+        lds_fft_n<MX>(lds, rfft_len(nbin), a.T, true);
         const double sc = 1.0 / (double)N;
         double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
         for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
         return;
     }
     __syncthreads();
+    if (nbin & 1) {
+        double *o = a.out + (int64_t)blockIdx.x * nbin;
+        for (int j = threadIdx.x; j < nbin; j += kBlock) o[j] = row[j];
+        return;
+    }
     double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)blockIdx.x * N;
     for (int j = threadIdx.x; j < N; j += kBlock) o[j] = lds[j];
 }
@@ -1241,8 +1365,8 @@ hipError_t launch_twiddles(int N, double2 *T, double2 *T2, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_rfft_rows(const RfftArgs &a, int64_t nrows, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_rfft_rows<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
+    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_rfft_rows<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_rfft_rows<true>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
@@ -1273,7 +1397,7 @@ hipError_t launch_xspec(const XspecArgs &a, hipStream_t st) {
             // wave per row (k_xspec_wm) up to N = 1024; the block kernel above
             if (PPF_XSPEC_WM && xspec_wm_supported(a.nbin) && a.cb <= 64) return launch_xspec_wm(a, st);
             dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(kBlock);
-            const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+            const size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
             if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_any<0>), g, b, lds, st, a);
             else hipLaunchKernelGGL((k_xspec_any<1>), g, b, lds, st, a);
             break;
@@ -1354,16 +1478,17 @@ hipError_t launch_dsum(const DsumArgs &a_in, hipStream_t st) {
 }
 
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
-    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_guess<false>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
+    size_t lds = (size_t)(rfft_len(a.nbin) + a.nbin / 2 + 2) * sizeof(double2) +
+                 (size_t)(a.Ns + 8) * sizeof(double);
+    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_guess<false>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_guess<true>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nport * a.nchan)), b(kBlock);
-    const bool mx = !is_pow2(a.nbin / 2);
-    switch (kmax_pow2(a.nbin / 2)) {
+    const bool mx = !is_pow2(rfft_len(a.nbin));
+    switch (kmax_pow2(a.nbin / 2 + (a.nbin & 1))) {
         case 1: MXL(mx, k_gauss_port, 1, g, b, lds, st, a); break;
         case 2: MXL(mx, k_gauss_port, 2, g, b, lds, st, a); break;
         case 4: MXL(mx, k_gauss_port, 4, g, b, lds, st, a); break;
@@ -1374,10 +1499,10 @@ hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
-    const bool mx = !is_pow2(a.nbin / 2);
-    switch (kmax_pow2(a.nbin / 2)) {
+    const bool mx = !is_pow2(rfft_len(a.nbin));
+    switch (kmax_pow2(a.nbin / 2 + (a.nbin & 1))) {
         case 1: MXL(mx, k_rotate, 1, g, b, lds, st, a); break;
         case 2: MXL(mx, k_rotate, 2, g, b, lds, st, a); break;
         case 4: MXL(mx, k_rotate, 4, g, b, lds, st, a); break;
@@ -1405,6 +1530,8 @@ template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1;
+    const bool odd = a.nbin & 1;
+    const int KH = odd ? N + 1 : N;
     const int n = blockIdx.x % a.nchan, g = blockIdx.x / a.nchan;
     const int per = (a.nsub + a.ngroup - 1) / a.ngroup;
     const int s0 = g * per, s1 = min(a.nsub, s0 + per);
@@ -1420,16 +1547,18 @@ __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
         wtot += w;
         load_row(lds, a.in, a.dtype, row, a.nbin);
         __syncthreads();
-        lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+        lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, false);
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
             const int k = threadIdx.x + i * kBlock;
-            if (k < N) {
-                const double2 X1 = cmul(rfft_bin(lds, N, a.T2, k), cexp2pi((double)k * ph));
-                const double2 X2 =
-                    cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
+            if (k < KH) {
+                const double2 X1 = cmul(rbin(lds, a.nbin, a.T2, k), cexp2pi((double)k * ph));
                 Ak[i] = cadd(Ak[i], cscale(X1, w));
-                An[i] = cadd(An[i], cscale(X2, w));
+                if (!odd) {
+                    const double2 X2 =
+                        cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
+                    An[i] = cadd(An[i], cscale(X2, w));
+                }
             }
         }
         __syncthreads();
@@ -1438,8 +1567,9 @@ __global__ __launch_bounds__(kBlock) void k_align_part(AlignArgs a) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         const int k = threadIdx.x + i * kBlock;
-        if (k < N) {
+        if (k < KH) {
             P[k] = Ak[i];
+            if (odd) continue;
             if (k == 0) P[N] = An[i];               // (k, N - k) = (0, N)
             else P[N - k] = An[i];
         }
@@ -1451,16 +1581,18 @@ template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int N = a.nbin >> 1, n = blockIdx.x;
+    const bool odd = a.nbin & 1;
+    const int KH = odd ? N + 1 : N;
     double2 Xk[KMAX], Xn[KMAX];
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         const int k = threadIdx.x + i * kBlock;
-        if (k < N) {
+        if (k < KH) {
             double2 s1 = cmk(0.0, 0.0), s2 = s1;
             for (int g = 0; g < a.ngroup; ++g) {
                 const double2 *P = a.part + ((int64_t)g * a.nchan + n) * (N + 1);
                 s1 = cadd(s1, P[k]);
-                s2 = cadd(s2, P[N - k]);
+                if (!odd) s2 = cadd(s2, P[N - k]);
             }
             if (k == 0) { s1.y = 0.0; s2.y = 0.0; }  // DC and Nyquist: real parts only
             Xk[i] = s1;
@@ -1470,13 +1602,22 @@ __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         const int k = threadIdx.x + i * kBlock;
-        if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        if (k < KH) {
+            if (odd) herm_put(lds, a.nbin, k, Xk[i]);
+            else lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        }
     }
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
-    const double sc = 1.0 / (double)N;
-    double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)n * N;
-    for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cadd(o[j], cscale(lds[j], sc));
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, true);
+    if (odd) {
+        const double sc = 1.0 / (double)a.nbin;
+        double *o = a.out + (int64_t)n * a.nbin;
+        for (int j = threadIdx.x; j < a.nbin; j += kBlock) o[j] += lds[j].x * sc;
+    } else {
+        const double sc = 1.0 / (double)N;
+        double2 *o = reinterpret_cast<double2 *>(a.out) + (int64_t)n * N;
+        for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cadd(o[j], cscale(lds[j], sc));
+    }
     if (threadIdx.x == 0) {
         double w = 0.0;
         for (int g = 0; g < a.ngroup; ++g) w += a.wpart[(int64_t)g * a.nchan + n];
@@ -1485,7 +1626,7 @@ __global__ __launch_bounds__(kBlock) void k_align_fin(AlignArgs a) {
 }
 
 hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    const size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
     dim3 gp((unsigned)((int64_t)a.ngroup * a.nchan)), gf((unsigned)a.nchan), b(kBlock);
     // wave-per-row partials where the register FFT covers nbin; the
     // block-FFT k_align_part otherwise
@@ -1494,8 +1635,8 @@ hipError_t launch_align(const AlignArgs &a, hipStream_t st) {
         hipError_t e = launch_align_part_w(a, st);
         if (e != hipSuccess) return e;
     }
-    const bool mx = !is_pow2(a.nbin / 2);
-    switch (kmax_pow2(a.nbin / 2)) {
+    const bool mx = !is_pow2(rfft_len(a.nbin));
+    switch (kmax_pow2(a.nbin / 2 + (a.nbin & 1))) {
         case 1: if (!wave) MXL(mx, k_align_part, 1, gp, b, lds, st, a);
                 MXL(mx, k_align_fin, 1, gf, b, lds, st, a); break;
         case 2: if (!wave) MXL(mx, k_align_part, 2, gp, b, lds, st, a);
@@ -1522,18 +1663,21 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const int N = a.nbin >> 1;
+    const bool odd = a.nbin & 1;
+    const int KH = odd ? N + 1 : N;
     const int64_t row = blockIdx.x;
     load_row(lds, a.in, a.dtype, row, a.nbin);
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, false);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, false);
     double2 Xk[KMAX], Xn[KMAX];
     const double ph = a.phases[row];
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         int k = threadIdx.x + i * kBlock;
-        if (k < N) {
-            double2 X1 = cmul(rfft_bin(lds, N, a.T2, k), cexp2pi((double)k * ph));
-            double2 X2 = cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
+        if (k < KH) {
+            double2 X1 = cmul(rbin(lds, a.nbin, a.T2, k), cexp2pi((double)k * ph));
+            double2 X2 = cmk(0.0, 0.0);
+            if (!odd) X2 = cmul(rfft_bin(lds, N, a.T2, N - k), cexp2pi((double)(N - k) * ph));
             if (k == 0) { X1.y = 0.0; X2.y = 0.0; }
             Xk[i] = X1;
             Xn[i] = X2;
@@ -1543,14 +1687,21 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         int k = threadIdx.x + i * kBlock;
-        if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        if (k < KH) {
+            if (odd) herm_put(lds, a.nbin, k, Xk[i]);
+            else lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2[k]);
+        }
     }
     __syncthreads();
-    lds_fft_n<MX>(lds, a.nbin >> 1, a.T, true);
+    lds_fft_n<MX>(lds, rfft_len(a.nbin), a.T, true);
     const double sc = 1.0 / (double)N, s = a.scales[row];
     const double *m = a.model + (int64_t)a.model_row[row] * a.nbin;
     double acc[1] = {0.0};
-    for (int j = threadIdx.x; j < N; j += kBlock) {
+    for (int j = threadIdx.x; odd && j < a.nbin; j += kBlock) {
+        const double r0 = lds[j].x * (1.0 / (double)a.nbin) - s * m[j];
+        acc[0] = fma(r0, r0, acc[0]);
+    }
+    for (int j = threadIdx.x; !odd && j < N; j += kBlock) {
         const double2 x = cscale(lds[j], sc);
         const double r0 = x.x - s * m[2 * j], r1 = x.y - s * m[2 * j + 1];
         acc[0] = fma(r0, r0, fma(r1, r1, acc[0]));
@@ -1563,10 +1714,10 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a) {
 }
 
 hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
     dim3 g((unsigned)nrows), b(kBlock);
-    const bool mx = !is_pow2(a.nbin / 2);
-    switch (kmax_pow2(a.nbin / 2)) {
+    const bool mx = !is_pow2(rfft_len(a.nbin));
+    switch (kmax_pow2(a.nbin / 2 + (a.nbin & 1))) {
         case 1: MXL(mx, k_resid_chi2, 1, g, b, lds, st, a); break;
         case 2: MXL(mx, k_resid_chi2, 2, g, b, lds, st, a); break;
         case 4: MXL(mx, k_resid_chi2, 4, g, b, lds, st, a); break;
@@ -1578,20 +1729,21 @@ hipError_t launch_resid_chi2(const ResidArgs &a, int64_t nrows, hipStream_t st) 
 }
 
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_noise<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
+    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_noise<false>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_noise<true>, dim3((unsigned)nrows), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin + 2) * sizeof(double2) + (size_t)(a.Ns + 8) * sizeof(double);
-    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+    size_t lds = (size_t)(rfft_len(a.nbin) + a.nbin / 2 + 2) * sizeof(double2) +
+                 (size_t)(a.Ns + 8) * sizeof(double);
+    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_phase_shift<true>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }
 hipError_t launch_synth(const SynthArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(a.nbin / 2) * sizeof(double2);
-    if (is_pow2(a.nbin / 2)) hipLaunchKernelGGL(k_synth<false>, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
+    size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
+    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_synth<false>, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_synth<true>, dim3((unsigned)(a.nsub * a.nchan)), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }

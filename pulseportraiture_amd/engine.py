@@ -420,7 +420,7 @@ def _desc_workspace_bytes(lib, d):
     nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
         raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
-                                  " (nbin must be even, in [32, 8192])" %
+                                  " (nbin must be even in [32, 8192] or odd in [33, 4095])" %
                                   (d.nsub, d.nchan, d.nbin))
     return nbytes
 
@@ -572,8 +572,9 @@ def noise_rows(rows, frac=4, dev=None):
 
 
 def noise_len_supported(n):
-    """Row lengths ppf_noise_batch transforms (its LDS FFT): even, 32..8192."""
-    return n % 2 == 0 and 32 <= n <= 8192
+    """Row lengths ppf_noise_batch transforms (its LDS FFT): even 32..8192,
+    odd 33..4095."""
+    return 32 <= n <= (8192 if n % 2 == 0 else 4095)
 
 
 def noise_long(row, frac=4, dev=None):
@@ -699,7 +700,8 @@ def gauss_portraits(model_code, params, scattering_index, freqs, nu_ref, nbin,
     pplib.py:886-963) on the device: params [nport, 2 + 6 ngauss] (DC, tau
     [bin], per component loc, m_loc, wid, m_wid, amp, m_amp),
     scattering_index [nport], freqs [nport, nchan], nu_ref [nport] ->
-    float64 [nport, nchan, nbin]."""
+    float64 [nport, nchan, nbin] (odd nbin with tau != 0: nbin - 1 bins, as
+    the reference's length-less irfft gives, then a zero column)."""
     code = str(model_code)
     if len(code) != 3 or any(c not in "01" for c in code):
         raise KeyError(code)     # evolve_parameter's dictionary lookup

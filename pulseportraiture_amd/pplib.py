@@ -193,7 +193,12 @@ def gen_gaussian_portrait(model_code, params, scattering_index, phases, freqs,
                                  [scattering_index],
                                  np.asarray(freqs, dtype=float)[None, :],
                                  [nu_ref], len(phases))
-    return out[0].cpu().numpy()
+    out = out[0].cpu().numpy()
+    if len(phases) % 2 and params[1] != 0.0:
+        # the reference's scattering irfft takes no length (pplib.py:957):
+        # nbin - 1 bins at odd nbin
+        out = out[:, :-1]
+    return out
 
 
 def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
@@ -343,8 +348,8 @@ def get_noise_PS(data, frac=4, chans=False):
     row = data.ravel()
     if not engine.noise_len_supported(row.size):
         # the flattened portrait (nchan nbin samples; pplib.py:2334-2338) is
-        # longer than the LDS transforms of ppf_noise_batch (even, <= 8192
-        # points) or odd: one library rFFT on the device (rocFFT) instead
+        # longer than the LDS transforms of ppf_noise_batch (even <= 8192,
+        # odd <= 4095 points): one library rFFT on the device (rocFFT) instead
         return engine.noise_long(row, frac)
     return float(engine.noise_rows(row[None, :], frac).cpu().numpy()[0])
 

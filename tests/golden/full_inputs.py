@@ -97,6 +97,12 @@ FITS = [
          seed=112),
     dict(name="pdta_64x2006", nchan=64, nbin=2006, flags=[1, 1, 0, 1, 1],
          seed=113, tau=2e-3),
+    # odd nbin (the row transformed as nbin complex points): 1023 = 3 * 11 *
+    # 31 (radix 3 + generic stages), 1001 = 7 * 11 * 13 with scattering
+    dict(name="pd_128x1023", nchan=128, nbin=1023, flags=[1, 1, 0, 0, 0],
+         seed=114),
+    dict(name="pdta_64x1001", nchan=64, nbin=1001, flags=[1, 1, 0, 1, 1],
+         seed=115, tau=2e-3),
 ]
 
 
@@ -210,6 +216,8 @@ TOAS = [
     dict(name="nb1000", nfile=1, nsub=3, nchan=64, nbin=1000, seed=213),
     # (i) round 5: nbin = 1022 (2 * 7 * 73), the generic-radix FFT stage
     dict(name="nb1022", nfile=1, nsub=3, nchan=64, nbin=1022, seed=214),
+    # (j) odd nbin = 1023 = 3 * 11 * 31 through the whole get_TOAs loop
+    dict(name="nb1023", nfile=1, nsub=3, nchan=64, nbin=1023, seed=215),
 ]
 
 

@@ -19,7 +19,8 @@ SIG, RCHI2 = G.SIGMA_TOL, G.RCHI2_RTOL
                                   "c3_pdta_512x2048", "narrow_pd_512x2048",
                                   "pd_64x4096", "pdta_64x128", "pd_128x1000",
                                   "pdta_128x1536", "pd_128x1022",
-                                  "pdta_64x2006"])
+                                  "pdta_64x2006", "pd_128x1023",
+                                  "pdta_64x1001"])
 def test_fit_inputs_rebuild(name):
     F.fit_case(name)
 
@@ -52,7 +53,8 @@ def _oracle_fit(c, data, model, freqs):
                                   "pd_64x4096", "pdta_64x128",
                                   "lowsnr_pd_512x2048", "lowsnr_pd_64x512",
                                   "pd_128x1000", "pdta_128x1536",
-                                  "pd_128x1022", "pdta_64x2006"])
+                                  "pd_128x1022", "pdta_64x2006",
+                                  "pd_128x1023", "pdta_64x1001"])
 def test_oracle_matches_reference_fullshape_fits(name):
     c, data, model, freqs = F.fit_case(name)
     r = _oracle_fit(c, data, model, freqs)

@@ -35,7 +35,8 @@ def _kept_harmonic_fraction(model):
                                   "lowsnr_pd_512x2048", "lowsnr_pd_64x512",
                                   "lowsnr_all_512x2048", "pd_128x1000",
                                   "pdta_128x1536", "pd_128x1022",
-                                  "pdta_64x2006"])
+                                  "pdta_64x2006", "pd_128x1023",
+                                  "pdta_64x1001"])
 def test_fullshape_fit_matches_reference(name):
     """configs[2]'s fit (phi, DM, GM, tau, alpha) and phi+DM+tau+alpha at
     512 x 2048, a narrow-component template at 512 x 2048 (no harmonic
@@ -44,8 +45,9 @@ def test_fullshape_fit_matches_reference(name):
     the initial DM several bins off at the band edges: the moment path's
     truncation bound is relative to sum_k |Y_k|, loosest when |C_n| is
     small; S/N 133 with all five parameters), nbin = 1000 and 1536 (not
-    powers of two: the mixed-radix LDS FFT), through the drop-in
-    fit_portrait_full."""
+    powers of two: the mixed-radix LDS FFT), 1022 and 2006 (the
+    generic-radix stage), the odd 1023 and 1001 (full-length complex
+    transforms of the rows), through the drop-in fit_portrait_full."""
     from pulseportraiture_amd import pptoaslib
     c, data, model, freqs = F.fit_case(name)
     if int(c["narrow"]):
@@ -211,7 +213,7 @@ def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True,
 
 
 BRANCHES = ["scatgm", "scatfix", "opts", "chan12", "tscr", "tnc", "tncscat",
-            "ncg", "nb1000", "nb1022"]
+            "ncg", "nb1000", "nb1022", "nb1023"]
 
 
 @pytest.mark.timeout(300)

@@ -48,8 +48,18 @@ def test_noise_matches_reference(ppl):
                                axis=-1))
         np.testing.assert_allclose(ppl.get_noise(x, chans=True), want,
                                    rtol=1e-12, err_msg=str(shape))
-    with pytest.raises(NotImplementedError):     # odd nbin
-        ppl.get_noise(np.ones((2, 1001)), chans=True)
+    # odd nbin (the row as nbin complex points): 1001 = 7 x 11 x 13,
+    # 1023 = 3 x 11 x 31, 4093 prime (one generic-radix stage)
+    for shape in ((2, 1001), (3, 1023), (2, 4093), (2, 33)):
+        x = np.random.default_rng(7).normal(size=shape)
+        F = np.fft.rfft(x, axis=-1)
+        p = np.real(F * np.conj(F)) / shape[-1]
+        want = np.sqrt(np.mean(p[:, int((1 - 4 ** -1) * p.shape[-1]):],
+                               axis=-1))
+        np.testing.assert_allclose(ppl.get_noise(x, chans=True), want,
+                                   rtol=1e-12, err_msg=str(shape))
+    with pytest.raises(NotImplementedError):     # odd nbin past 4095
+        ppl.get_noise(np.ones((2, 4097)), chans=True)
     # chans=False ravels the portrait (pplib.py:2334-2338): 64 x 2048 and an
     # odd length go through the device FFT library (no LDS-size cap); the
     # restatement is the reference's own NumPy arithmetic
@@ -100,12 +110,15 @@ def test_rotate_matches_reference(ppl, ppt):
                                  1500., 1600., P0), m["rotf_dmgm"], **tol)
 
 
-@pytest.mark.parametrize("nbin", [1000, 1022, 2006, 4094])
-def test_rotate_any_even_nbin_matches_numpy(ppl, nbin):
+@pytest.mark.parametrize("nbin", [1000, 1022, 2006, 4094, 33, 127, 511,
+                                  1001, 1023, 4095])
+def test_rotate_any_nbin_matches_numpy(ppl, nbin):
     """rotate_data (pplib.py:2427-2480) at nbin/2 not a power of two, on
     the mixed-radix (1000) and generic-radix (1022 = 2 x 7 x 73, 2006 =
-    2 x 17 x 59, 4094 = 2 x 23 x 89) LDS FFTs, against its own NumPy
-    arithmetic: rfft, phasor, irfft."""
+    2 x 17 x 59, 4094 = 2 x 23 x 89) LDS FFTs, and at odd nbin (33, 127
+    prime, 511 = 7 x 73, 1001, 1023, 4095 = 3^2 5 7 13: the row as nbin
+    complex points, Hermitian inverse), against its own NumPy arithmetic:
+    rfft, phasor, irfft."""
     x = np.random.default_rng(nbin).normal(size=(3, nbin))
     ph = 0.2718
     k = np.arange(nbin // 2 + 1)
@@ -560,15 +573,16 @@ def test_chime_shape_16384ch_scattering_fit_properties():
 
 
 # ------------------------------------------------------------- ppalign (C4) --
-def test_align_accum_matches_numpy():
+@pytest.mark.parametrize("nbin", [512, 511])
+def test_align_accum_matches_numpy(nbin):
     """ppf_align_accum: sum_s w rotate(x_s, phi_s) per channel (frequency-
     domain accumulation) equals the time-domain rotate-then-sum of the
-    oracle to rounding."""
+    oracle to rounding (odd nbin: the unpaired harmonic partials)."""
     import torch
     import oracle as O
     from pulseportraiture_amd import engine
     rng = np.random.default_rng(5)
-    nsub, nchan, nbin = 37, 12, 512
+    nsub, nchan = 37, 12
     x = rng.normal(size=(nsub, nchan, nbin)).astype(np.float32)
     ph = rng.uniform(-0.5, 0.5, size=(nsub, nchan))
     w = rng.uniform(0.1, 2.0, size=(nsub, nchan))
@@ -1174,3 +1188,56 @@ def test_lane_trust_region_step_equals_wave_step_multiblock():
     for key in ("results", "scales", "scale_errs", "channel_snrs",
                 "covariance"):
         np.testing.assert_array_equal(small[key], big[key][:k], err_msg=key)
+
+
+@pytest.mark.parametrize("nbin", [511, 1001])
+def test_odd_nbin_block_kernels_match_oracle(ppl, nbin):
+    """The block-FFT kernels at odd nbin (rfft_len: nbin complex points,
+    X_k = Z_k, inverse from the Hermitian-filled buffer) against the
+    oracle's NumPy restatements: fit_phase_shift (pplib.py:2136-2182),
+    the per-channel reduced chi^2 of get_channels_to_zap (pplib.py:754-779),
+    and gen_gaussian_portrait with and without scattering
+    (pplib.py:886-963)."""
+    import oracle as O
+    from pulseportraiture_amd import engine
+    rng = np.random.default_rng(nbin)
+    # fit_phase_shift
+    ph = np.linspace(0, 1, nbin, endpoint=False)
+    model = np.exp(-0.5 * ((ph - 0.4) / 0.03) ** 2) + \
+        0.3 * np.exp(-0.5 * ((ph - 0.55) / 0.05) ** 2)
+    data = np.stack([O.rotate_rows(model[None, :] * 2.5, [-s])[0] +
+                     rng.normal(scale=0.05, size=nbin)
+                     for s in (0.123, -0.31, 0.0)])
+    got = engine.phase_shift_batch(data, model).cpu().numpy()
+    for i in range(len(data)):
+        want = O.fit_phase_shift(data[i], model)
+        assert abs(G.phase_diff(got[i, 0], want["phase"])) < \
+            SIG * want["phase_err"], (i, got[i], want)
+        assert abs(got[i, 1] / want["phase_err"] - 1) < 1e-4
+        assert abs(got[i, 2] / want["scale"] - 1) < 1e-6
+        assert abs(got[i, 4] / want["snr"] - 1) < 1e-6
+    # per-channel reduced chi^2 after rotation
+    rows = rng.normal(size=(6, nbin))
+    mrows = rng.normal(size=(2, nbin))
+    phs = rng.uniform(-0.5, 0.5, 6)
+    mi = np.array([0, 1, 0, 1, 1, 0], dtype=np.int32)
+    sc = rng.uniform(0.5, 2.0, 6)
+    er = rng.uniform(0.5, 1.5, 6)
+    got = engine.resid_chi2_rows(rows, phs, mrows, mi, sc, er, 7.0)
+    want = O.channel_red_chi2s(rows, phs, mrows[mi], sc, er, 7.0)
+    np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-12)
+    # Gaussian portraits: the example template, with and without tau
+    g = G.gauss()
+    c = G.gauss_case(g, "example_64x512")
+    for tau in (0.0, 0.02):
+        prm = np.array(c["params"], dtype=float)
+        prm[1] = tau
+        got = ppl.gen_gaussian_portrait(c["code"], prm, c["alpha"],
+                                        np.zeros(nbin), c["freqs"],
+                                        c["nu_ref"])
+        want = O.gen_gaussian_portrait(c["code"], prm, c["alpha"],
+                                       np.zeros(nbin), c["freqs"],
+                                       c["nu_ref"])
+        # (with tau the reference's length-less irfft returns nbin - 1 bins)
+        assert got.shape == want.shape == (len(c["freqs"]), nbin - (tau != 0))
+        assert np.abs(got - want).max() <= GAUSS_ATOL * np.abs(want).max()

@@ -937,7 +937,10 @@ def main():
         # nbin / 2 not a power of two, <= 1024: the wave-per-row mixed-radix
         # pass k_xspec_wm, which writes X below the cutoffs (like
         # k_xspec_w); longer rows: the block-FFT k_xspec, every harmonic
-        wm = nbin // 2 <= 1024 and (nbin & (nbin - 1)) != 0
+        # (odd nbin < 1024 too, rows as nbin complex points; longer odd rows
+        # on the block-FFT pass)
+        wm = (nbin % 2 == 0 and nbin // 2 <= 1024 and
+              (nbin & (nbin - 1)) != 0) or (nbin % 2 == 1 and nbin < 1024)
         xfull = nchan * nbin * 4 + (xh if wm else nchan * nharm) * 16 + 4 * nchan * 8
         kern["xspec"] = dict(name="k_xspec_wm" if wm else "k_xspec (block FFT)",
                              ms=stage_ms[1], unit=xfull,
@@ -1145,7 +1148,9 @@ def main():
                            if momx_used and wave else (
                                "fused pass (k_xmom_g)" if wave else
                                "cross spectrum (k_xspec_wm + k_moments)"
-                               if nbin // 2 <= 1024 and (nbin & (nbin - 1)) else
+                               if (nbin % 2 == 0 and nbin // 2 <= 1024 and
+                                   (nbin & (nbin - 1))) or
+                               (nbin % 2 == 1 and nbin < 1024) else
                                "cross spectrum (block FFT + k_moments)"),
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],

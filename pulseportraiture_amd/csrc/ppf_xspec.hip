@@ -1400,25 +1400,30 @@ __device__ __forceinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, c
 #ifndef PPF_WM_PRE
 #define PPF_WM_PRE 1
 #endif
-template <int DT, int NMAX>
+// ODD: odd nbin (<= 1023), the row as NF = nbin complex points with zero
+// imaginary parts (rfft_len), X_k = Z_k for k <= nbin / 2: no pair post-pass.
+template <int DT, int NMAX, bool ODD>
 __global__ __launch_bounds__(64 * kWmW) __attribute__((amdgpu_waves_per_eu(NMAX <= 512 ? 3 : 2)))
 void k_xspec_wm(XspecArgs a) {
     const int N = a.nbin >> 1, NH = N + 1;
-    const int SL = N + 2;                      // [0, N]: Z then X; [N + 1]: 1/errs_FT^2
+    const int NF = ODD ? a.nbin : N;           // complex points per row
+    // even: [0, N] Z then X, [N + 1] 1/errs_FT^2; odd: Z in [0, NF), X in
+    // [0, N] and 1/errs_FT^2 in [N + 1] after the post-pass (N + 1 < NF)
+    const int SL = ODD ? NF : N + 2, IE = N + 1;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double2 *buf = lds + wave * SL;
-    double2 *twl = lds + kWmW * SL;            // T[0, N): the stage twiddles
+    double2 *twl = lds + kWmW * SL;            // T[0, NF): the stage twiddles
     int s, cb;
     block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
     if (a.needx && !a.needx[s]) return;
-    for (int i = threadIdx.x; i < N; i += 64 * kWmW) twl[i] = a.T[i];
+    for (int i = threadIdx.x; i < NF; i += 64 * kWmW) twl[i] = a.T[i];
     __syncthreads();
     const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
     const int nround = (a.cb + kWmW - 1) / kWmW;
     const int mi = a.model_index ? a.model_index[s] : 0;
     const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double sqrtN = sqrt((double)N);
+    const double sqrtN = sqrt((double)a.nbin / 2.0);
     double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
     int kw = NH;
     if (a.KC) {
@@ -1432,19 +1437,20 @@ void k_xspec_wm(XspecArgs a) {
     const int nl = cbase + lane;
     const double ch_mpow = nl < cend ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
     const double ch_err = (a.errs && nl < cend) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
-    const bool two0 = (__builtin_ctz((unsigned)N) & 1) != 0;
+    const bool two0 = !ODD && (__builtin_ctz((unsigned)N) & 1) != 0;
 #if PPF_WM_PRE
     // the wave's next row in registers while this one is transformed
     // (unconditional loads of a valid row: the prefetch stays in VGPRs)
-    using LT = typename std::conditional<DT == 0, float2, double2>::type;
+    using ET = typename std::conditional<DT == 0, float, double>::type;
+    using LT = typename std::conditional<ODD, ET, typename std::conditional<DT == 0, float2, double2>::type>::type;
     constexpr int PJ = NMAX / 64;
     LT pre[PJ];
     auto fetch = [&](int m) {
-        const LT *src = reinterpret_cast<const LT *>(a.data) + ((int64_t)s * a.nchan + m) * (int64_t)N;
+        const LT *src = reinterpret_cast<const LT *>(a.data) + ((int64_t)s * a.nchan + m) * (int64_t)NF;
 #pragma unroll
         for (int i = 0; i < PJ; ++i) {
             const int t = lane + 64 * i;
-            pre[i] = src[t < N ? t : N - 1];
+            pre[i] = src[t < NF ? t : NF - 1];
         }
     };
     fetch(min(cbase + wave, cend - 1));
@@ -1457,7 +1463,11 @@ void k_xspec_wm(XspecArgs a) {
 #pragma unroll
             for (int i = 0; i < PJ; ++i) {
                 const int t = lane + 64 * i;
-                if (t < N) buf[t] = cmk((double)pre[i].x, (double)pre[i].y);
+                if constexpr (ODD) {
+                    if (t < NF) buf[t] = cmk((double)pre[i], 0.0);
+                } else {
+                    if (t < N) buf[t] = cmk((double)pre[i].x, (double)pre[i].y);
+                }
             }
         }
         fetch(min(n + kWmW, cend - 1));
@@ -1465,6 +1475,7 @@ void k_xspec_wm(XspecArgs a) {
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
 #if !PPF_WM_PRE
+            static_assert(!ODD, "odd nbin needs PPF_WM_PRE");
             if (DT == 0) {
                 const float2 *src = reinterpret_cast<const float2 *>(a.data) + crow * (int64_t)N;
                 for (int j = lane; j < N; j += 64) {
@@ -1479,7 +1490,7 @@ void k_xspec_wm(XspecArgs a) {
             wfft::wave_sync();
             // the stages in fft_radices' order (one 2 when the power of two
             // is odd, 4s, then the odd primes ascending), wave-uniform
-            int L = 1, rem = N;
+            int L = 1, rem = NF;
             bool two = two0;
             while (rem > 1) {
                 int R;
@@ -1487,11 +1498,11 @@ void k_xspec_wm(XspecArgs a) {
                 else if ((rem & 3) == 0) R = 4;
                 else { R = 3; while (rem % R) R += 2; }
                 switch (R) {
-                    case 2: wmr_stage<2, NMAX>(buf, N, L, twl, lane); break;
-                    case 3: wmr_stage<3, NMAX>(buf, N, L, twl, lane); break;
-                    case 4: wmr_stage<4, NMAX>(buf, N, L, twl, lane); break;
-                    case 5: wmr_stage<5, NMAX>(buf, N, L, twl, lane); break;
-                    default: wmr_stage_g<NMAX>(buf, N, L, R, twl, lane); break;
+                    case 2: wmr_stage<2, NMAX>(buf, NF, L, twl, lane); break;
+                    case 3: wmr_stage<3, NMAX>(buf, NF, L, twl, lane); break;
+                    case 4: wmr_stage<4, NMAX>(buf, NF, L, twl, lane); break;
+                    case 5: wmr_stage<5, NMAX>(buf, NF, L, twl, lane); break;
+                    default: wmr_stage_g<NMAX>(buf, NF, L, R, twl, lane); break;
                 }
                 L *= R;
                 rem /= R;
@@ -1501,7 +1512,15 @@ void k_xspec_wm(XspecArgs a) {
             // slot N); unscaled, the write-out applies 1/errs_FT^2
             const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
             double pn = 0.0, pd = 0.0;
-            for (int k = lane; k <= N / 2; k += 64) {
+            // odd nbin: X_k = Z_k (k <= N), each lane its own slots
+            for (int k = lane; ODD && k <= N; k += 64) {
+                const double2 dk = buf[k];
+                const double p0 = cabs2(dk);
+                if (k >= a.kc) pn += p0;
+                if (k >= 1) pd += p0;
+                if (k < kw) buf[k] = k == 0 ? cmk(0.0, 0.0) : cmulc(dk, Mrow[k]);
+            }
+            for (int k = lane; !ODD && k <= N / 2; k += 64) {
                 const int kn = N - k;
                 const double2 dk = rfft_bin(buf, N, a.T2, k);
                 const double2 dn = rfft_bin(buf, N, a.T2, kn);
@@ -1522,11 +1541,11 @@ void k_xspec_wm(XspecArgs a) {
             const int rr = n - cbase;
             double errs_FT;
             if (a.errs) errs_FT = readlane_d(ch_err, rr) * sqrtN;
-            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
+            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)a.nbin) * sqrtN;
             const double inv_e2 = 1.0 / (errs_FT * errs_FT);
             const double mpow = readlane_d(ch_mpow, rr);
             if (lane == 0) {
-                reinterpret_cast<double *>(buf + N + 1)[0] = inv_e2;
+                reinterpret_cast<double *>(buf + IE)[0] = inv_e2;
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
@@ -1542,7 +1561,7 @@ void k_xspec_wm(XspecArgs a) {
             if (nc < cend) {
                 const bool ok = !mask || mask[nc];
                 const double2 *b = lds + c * SL;
-                const double ie2 = ok ? reinterpret_cast<const double *>(b + N + 1)[0] : 0.0;
+                const double ie2 = ok ? reinterpret_cast<const double *>(b + IE)[0] : 0.0;
                 for (int k = threadIdx.x / kWmW; k < kw; k += 64)
                     Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[k], ie2) : cmk(0.0, 0.0);
             }
@@ -1551,20 +1570,30 @@ void k_xspec_wm(XspecArgs a) {
     }
 }
 
+// nbin / 2 <= 1024 not a power of two; odd nbin < 1024 (NF = nbin points)
 bool xspec_wm_supported(int nbin) {
+    if (nbin & 1) return nbin >= 33 && nbin < kWmMaxN;
     const int N = nbin / 2;
-    return (nbin & 1) == 0 && !is_pow2(N) && N <= kWmMaxN && fft_len_supported(N);
+    return !is_pow2(N) && N <= kWmMaxN && fft_len_supported(N);
 }
 
+#define PPF_WM_LAUNCH(NM, ODD)                                                           \
+    do {                                                                                 \
+        if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wm<0, NM, ODD>), g, b, lds, st, a); \
+        else hipLaunchKernelGGL((k_xspec_wm<1, NM, ODD>), g, b, lds, st, a);              \
+    } while (0)
+
 hipError_t launch_xspec_wm(const XspecArgs &a, hipStream_t st) {
-    const size_t lds = ((size_t)kWmW * (a.nbin / 2 + 2) + a.nbin / 2) * sizeof(double2);
+    const bool odd = a.nbin & 1;
+    const int NF = rfft_len(a.nbin);
+    const size_t lds = ((size_t)kWmW * (odd ? NF : NF + 2) + NF) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kWmW);
-    if (a.nbin / 2 <= 512) {
-        if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wm<0, 512>), g, b, lds, st, a);
-        else hipLaunchKernelGGL((k_xspec_wm<1, 512>), g, b, lds, st, a);
+    if (NF <= 512) {
+        if (odd) PPF_WM_LAUNCH(512, true);
+        else PPF_WM_LAUNCH(512, false);
     } else {
-        if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wm<0, 1024>), g, b, lds, st, a);
-        else hipLaunchKernelGGL((k_xspec_wm<1, 1024>), g, b, lds, st, a);
+        if (odd) PPF_WM_LAUNCH(1024, true);
+        else PPF_WM_LAUNCH(1024, false);
     }
     return hipGetLastError();
 }

@@ -1009,18 +1009,23 @@ def _cut_fraction(model):
     return kc.mean() / mp.shape[1]
 
 
-@pytest.mark.parametrize("flags", [[1, 1, 0, 0, 0], [1, 1, 1, 1, 1]])
-def test_harmonic_cutoff_fits_match_oracle(flags):
+@pytest.mark.parametrize("flags,nbin", [([1, 1, 0, 0, 0], 2048),
+                                        ([1, 1, 1, 1, 1], 2048),
+                                        ([1, 1, 0, 0, 0], 3001),
+                                        ([1, 1, 1, 1, 1], 1001)])
+def test_harmonic_cutoff_fits_match_oracle(flags, nbin):
     """The example template at 1100-1900 MHz x 2048 bins has no model power
     above ~1e-14 of its peak past harmonic ~430, so the device sums stop
     there (k_model_cut; DESIGN.md section 4, deviation 7) while the oracle
     sums all 1025 harmonics: the phase+DM moment path (with the device guess)
     and the full scattering fit agree with the oracle to 0.01 sigma and
-    chi2_red to 1e-8."""
+    chi2_red to 1e-8.  Also at odd nbin (3001, a prime: one generic-radix
+    stage of radix 3001; 1001 = 7 x 11 x 13), whose synthetic rows,
+    guess profile and spectra all take the full-length complex transforms."""
     import oracle as O
     from pulseportraiture_amd import engine, synth, _lib
     from pulseportraiture_amd.pplib import guess_fit_freq, phase_transform
-    nsub, nchan, nbin = 2, 128, 2048
+    nsub, nchan = 2, 128
     scat = flags[3] == 1
     b = synth.make_batch(nsub, nchan, nbin, first=515,
                          tau=2e-3 if scat else 0.0,

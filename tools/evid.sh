@@ -2,7 +2,8 @@
 # Evidence run: the GPU parity suite, then every bench line with its
 # CPU baseline and parity sample (C2 headline, single-call latency, C3 and C5
 # with >= 5 timed steps, C4 ppalign, GetTOAs from 16-bit PSRFITS and from
-# float32 archives, phase+DM at the mixed-radix nbin 1000 and 1536).
+# float32 archives, phase+DM at the mixed-radix nbin 1000 and 1536 and the
+# odd nbin 1023).
 # usage: tools/evid.sh TAG [tests|notests]
 tag=${1:-a}
 mode=${2:-tests}
@@ -30,4 +31,5 @@ run gettoaspsrfits 300 --fit gettoas --psrfits --steps 4 --warmup 1 --timeline g
 run gettoas 300 --fit gettoas --steps 3 --warmup 1
 run c2nb1000 300 --nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
 run c2nb1536 300 --nbin 1536 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
+run c2nb1023 300 --nbin 1023 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8
 echo end >> $st

@@ -263,6 +263,47 @@ def O_DM0():
     return DM0
 
 
+
+def _solver_fp64(fk, parts, nchan, nmom, evaluations, fpath):
+    """The bench line's solver_fp64 object: per solver kernel (key, name,
+    event-timed ms, units or None, launches) its f64 flops from the SQ
+    passes (fp64_summary.json entry fk) over its time, against the fp64
+    peak; k_tr_mom also its memory-side rate (it re-reads the moment set of
+    every channel on every evaluation: nmom complex moments plus the channel
+    scalars and the radius test's dphi / centre residual; the sets outgrow
+    the L2s, re-reads of one sub-int's set within a launch may hit the MALL)."""
+    items = {}
+    tot_fl = tot_ms = 0.0
+    for key, name, ms, units, nl in parts:
+        k = fk.get(key)
+        it = dict(name=name, total_ms=round(float(ms), 3), launches=int(nl))
+        if k is not None and ms > 0:
+            # units: sub-ints (or sub-int evaluations); k_tr_mom and
+            # k_tr_step count per launch in the SQ pass's units, so their
+            # units follow from the profiled run's ratio
+            if units is None:
+                units = k["units"] / max(k["dispatches"], 1) * nl
+            fl = k["flops_per_unit"] * units
+            tf = fl / (ms / 1e3) / 1e12
+            it.update(flops_per_unit=round(k["flops_per_unit"]),
+                      achieved_tflops=round(tf, 3),
+                      frac=round(tf / FP64_PEAK_TF, 4),
+                      valu_active_per_wave=k.get("valu_active_per_wave"))
+            tot_fl += fl
+            tot_ms += ms
+        if key == "tr_mom" and ms > 0:
+            bpe = nchan * (nmom * 16 + 40 + 32)
+            mb = evaluations * bpe
+            it["memory"] = dict(bytes_per_evaluation=bpe,
+                                evaluations=round(evaluations),
+                                achieved_gbs=round(mb / (ms / 1e3) / 1e9, 1),
+                                hbm_frac=round(mb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
+        items[key] = it
+    return dict(bound="fp64", peak=FP64_PEAK_TF, unit="TFLOP/s",
+                achieved=round(tot_fl / max(tot_ms, 1e-9) / 1e9, 3) if tot_ms else None,
+                frac=round(tot_fl / max(tot_ms, 1e-9) / 1e9 / FP64_PEAK_TF, 4) if tot_ms else None,
+                kernels=items, source=os.path.relpath(fpath, ROOT))
+
 def bench_align(args):
     """configs[3]: ppalign.align_archives iterations over --nsub tscrunched
     archives (256 ch x 1024 bin by default).  One step = one iteration: the
@@ -388,6 +429,11 @@ def bench_align(args):
                        gbs=(None if not v["ms"] else
                             round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)))
                for k, v in kern.items()}
+    # solver kernels of the timed calls: [k_tr_mom ms, launches, k_tr_step
+    # ms, launches, k_postfit ms, launches]
+    shist = np.zeros((ncalls, 6))
+    sgot = lib.ppf_solver_ms_history(lctx, ncalls, shist.ctypes.data)
+    solv_ms = shist[:max(sgot, 0)].sum(axis=0)
     fitstats = {}
     lr = R.__dict__.get("_dev_inputs", {}).get("last_results")
     if lr is not None:
@@ -397,6 +443,20 @@ def bench_align(args):
         fitstats = dict(mean_passes_per_fit=round(float(lr[:, I["npass"]].mean()), 3),
                         mean_evals_per_fit=round(float(lr[:, I["nfeval"]].mean()), 3),
                         passes_hist=np.bincount(lr[:, I["npass"]].astype(int)).tolist())
+    # fp64 utilisation of the solver (as the fit modes' solver_fp64): the
+    # moment sets come from the fused pass k_xmom_g (32 moments, priced in
+    # the roofline above), every trust-region evaluation from k_tr_mom
+    solver = None
+    fpath = os.path.join(ROOT, "profiles", "fp64_summary.json")
+    if os.path.exists(fpath) and fitstats:
+        fm = json.load(open(fpath)).get("modes", {}).get("align", {})
+        same = ("%dch x %dbin" % (nchan, nbin)) in str(
+            (fm.get("source") or {}).get("bench", ""))
+        if same:
+            parts = [("tr_mom", "k_tr_mom", solv_ms[0], None, solv_ms[1]),
+                     ("postfit", "k_postfit", solv_ms[4], ncalls * count, solv_ms[5])]
+            solver = _solver_fp64(fm.get("kernels", {}), parts, nchan, 32,
+                                  ncalls * count * fitstats["mean_evals_per_fit"], fpath)
     out = dict(metric="archive fits+aligns/sec (ppalign iteration, %dch×"
                       "%dbin) at 1/2/4/8 MI355X" % (nchan, nbin),
                value=round(value, 2), unit="archive-iterations/s",
@@ -411,7 +471,7 @@ def bench_align(args):
                                                           nbin),
                            nsub_per_gpu=args.nsub, nchan=nchan, nbin=nbin,
                            fit="align", parallelism="dp%d" % world),
-               roofline=roof, kernels=kernels, cpu_baseline=None,
+               roofline=roof, solver_fp64=solver, kernels=kernels, cpu_baseline=None,
                template_peak=float(torch.as_tensor(m).abs().max()), **fitstats)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         out["cpu_baseline"], out["parity"] = _align_cpu_baseline(
@@ -1072,47 +1132,8 @@ def main():
                               steps_subints, ncalls))
         parts.append(("postfit", "k_postfit", solv_ms[4], steps_subints,
                       solv_ms[5]))
-        items = {}
-        tot_fl = tot_ms = 0.0
-        for key, name, ms, units, nl in parts:
-            k = fk.get(key)
-            it = dict(name=name, total_ms=round(float(ms), 3),
-                      launches=int(nl))
-            if k is not None and ms > 0:
-                # units: sub-ints (or sub-int evaluations); k_tr_mom and
-                # k_tr_step count per launch in the SQ pass's units, so
-                # their units follow from the profiled run's ratio
-                if units is None:
-                    units = k["units"] / max(k["dispatches"], 1) * nl
-                fl = k["flops_per_unit"] * units
-                tf = fl / (ms / 1e3) / 1e12
-                it.update(flops_per_unit=round(k["flops_per_unit"]),
-                          achieved_tflops=round(tf, 3),
-                          frac=round(tf / FP64_PEAK_TF, 4),
-                          valu_active_per_wave=k.get("valu_active_per_wave"))
-                tot_fl += fl
-                tot_ms += ms
-            if key == "tr_mom" and ms > 0:
-                # k_tr_mom re-reads the moment set of every channel on every
-                # evaluation (16 complex moments on the X-moment path, up to
-                # 32 otherwise) plus the channel scalars and the radius
-                # test's dphi / centre residual: its memory-side rate against
-                # the HBM peak (the sets outgrow the L2s; re-reads of one
-                # sub-int's set within a launch may hit the MALL)
-                nmom = 16 if (momx_used or not wave) else 32
-                bpe = nchan * (nmom * 16 + 40 + 32)
-                mb = steps_subints * mean_nfev * bpe
-                it["memory"] = dict(bytes_per_evaluation=bpe,
-                                    evaluations=round(steps_subints * mean_nfev),
-                                    achieved_gbs=round(mb / (ms / 1e3) / 1e9, 1),
-                                    hbm_frac=round(mb / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
-            items[key] = it
-        solver = dict(bound="fp64", peak=FP64_PEAK_TF, unit="TFLOP/s",
-                      achieved=round(tot_fl / max(tot_ms, 1e-9) / 1e9, 3)
-                      if tot_ms else None,
-                      frac=round(tot_fl / max(tot_ms, 1e-9) / 1e9 /
-                                 FP64_PEAK_TF, 4) if tot_ms else None,
-                      kernels=items, source=os.path.relpath(fpath, ROOT))
+        solver = _solver_fp64(fk, parts, nchan, 16 if (momx_used or not wave) else 32,
+                              steps_subints * mean_nfev, fpath)
     names = ["model_rfft", "xspec", "guess", "solve"]
     stages = {n: round(float(stage_ms[i]), 3) for i, n in enumerate(names)}
     kernels = {k: dict(name=v["name"], total_ms=round(float(v["ms"]), 3),

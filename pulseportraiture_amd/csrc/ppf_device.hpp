@@ -420,28 +420,44 @@ __device__ void mr_stage(double2 *buf, int N, int L, const double2 *__restrict__
 // One output per thread per pass (NT threads starting at t0), O(N R) work;
 // all of a thread's reads are done before the caller's barrier, its writes
 // after it.
+// Outputs are formed G = 4 at a time with the q loop outside, so a thread
+// has four independent LDS / twiddle read chains in flight instead of one
+// dependent chain per output (the same arithmetic per output, so the same
+// bits); an output past N is computed on a clamped index and dropped.
 template <int QO>
 __device__ __forceinline__ void gr_stage_read(const double2 *buf, int N, int L, int R,
                                               const double2 *__restrict__ T, bool inv, int t0, int NT,
                                               double2 (&y)[QO]) {
     const int nb = N / R, ts = N / (R * L), RL = R * L;
+    constexpr int G = QO >= 4 ? 4 : QO;
+    static_assert(QO % G == 0, "QO must be a multiple of the group size");
 #pragma unroll
-    for (int i = 0; i < QO; ++i) {
-        const int o = t0 + i * NT;
-        if (o < N) {
+    for (int i0 = 0; i0 < QO; i0 += G) {
+        if (t0 + i0 * NT >= N) break;            // no output of this thread from here on
+        int j[G], e[G], idx[G];
+        double2 acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            int o = t0 + (i0 + g) * NT;
+            o = o < N ? o : N - 1;
             const int blk = o / RL, rem = o - blk * RL, m = rem / L, k = rem - m * L;
-            const int j = blk * L + k;
-            int e = k * ts + m * nb;
-            e = e >= N ? e - N : e;
-            double2 acc = buf[j];
-            for (int q = 1, idx = e; q < R; ++q) {
-                const double2 w = twid(T, idx, inv);
-                acc = cadd(acc, cmul(buf[j + q * nb], w));
-                idx += e;
-                idx = idx >= N ? idx - N : idx;
-            }
-            y[i] = acc;
+            j[g] = blk * L + k;
+            const int ee = k * ts + m * nb;
+            e[g] = ee >= N ? ee - N : ee;
+            idx[g] = e[g];
+            acc[g] = buf[j[g]];
         }
+        for (int q = 1; q < R; ++q) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const double2 w = twid(T, idx[g], inv);
+                acc[g] = cadd(acc[g], cmul(buf[j[g] + q * nb], w));
+                idx[g] += e[g];
+                idx[g] = idx[g] >= N ? idx[g] - N : idx[g];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) y[i0 + g] = acc[g];
     }
 }
 template <int QO>

@@ -30,6 +30,7 @@ args_of() {
     nb1000) echo "--nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 0";;
     nb1536) echo "--nbin 1536 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 0";;
     nb1022) echo "--nbin 1022 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 0";;
+    nb1023) echo "--nbin 1023 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 0";;
     *) echo "BAD";;
   esac
 }

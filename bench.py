@@ -1002,7 +1002,8 @@ def main():
         wm = (nbin % 2 == 0 and nbin // 2 <= 1024 and
               (nbin & (nbin - 1)) != 0) or (nbin % 2 == 1 and nbin < 1024)
         xfull = nchan * nbin * 4 + (xh if wm else nchan * nharm) * 16 + 4 * nchan * 8
-        kern["xspec"] = dict(name="k_xspec_wm" if wm else "k_xspec (block FFT)",
+        kern["xspec"] = dict(name=("k_xspec_wo" if nbin % 2 else "k_xspec_wm") if wm
+                             else "k_xspec (block FFT)",
                              ms=stage_ms[1], unit=xfull,
                              bytes=steps_subints * xfull +
                              ncalls * nchan * nharm * 16)
@@ -1168,7 +1169,8 @@ def main():
                            moments="cross spectrum (k_xspec_w + k_moments)"
                            if momx_used and wave else (
                                "fused pass (k_xmom_g)" if wave else
-                               "cross spectrum (k_xspec_wm + k_moments)"
+                               "cross spectrum (k_xspec_w%s + k_moments)" %
+                               ("o" if nbin % 2 else "m")
                                if (nbin % 2 == 0 and nbin // 2 <= 1024 and
                                    (nbin & (nbin - 1))) or
                                (nbin % 2 == 1 and nbin < 1024) else

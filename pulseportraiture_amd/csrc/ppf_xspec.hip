@@ -1570,6 +1570,166 @@ void k_xspec_wm(XspecArgs a) {
     }
 }
 
+// ===========================================================================
+// k_xspec_wo: the spectrum pass for odd nbin < 1024 with TWO real rows per
+// complex transform: row A as the real part, row B as the imaginary part,
+// Z = FFT_NF(a + i b) (NF = nbin points, the stages of k_xspec_wm), then
+// X_A(k) = (Z_k + conj Z_{NF-k}) / 2 and X_B(k) = (Z_k - conj Z_{NF-k}) / 2i
+// for k <= N = nbin / 2: half the transform work per row of the one-row
+// path (k_xspec_wm<ODD>, PPF_XSPEC_WO=0).  A round is 8 rows, two per wave
+// (rows w and w + 4 of the round).  Each pair (k, NF - k) is read and
+// written back by one lane in its own two slots: the unscaled X of row A at
+// slot k, of row B at slot NF - k (k = 1 .. N); the k = 0 positions (X_0 = 0:
+// F0_fact), slot 0 and slot NF, carry the rows' 1/errs_FT^2 for the
+// write-out, which stores 8 channels (128 B) per harmonic.
+// ===========================================================================
+template <int DT, int NMAX>
+__global__ __launch_bounds__(64 * kWmW) __attribute__((amdgpu_waves_per_eu(NMAX <= 512 ? 3 : 2)))
+void k_xspec_wo(XspecArgs a) {
+    const int N = a.nbin >> 1, NH = N + 1, NF = a.nbin;
+    const int SL = NF + 1;                     // = 2 NH
+    constexpr int RW = 2 * kWmW;               // rows per round
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *buf = lds + wave * SL;
+    double2 *twl = lds + kWmW * SL;            // T[0, NF): the stage twiddles
+    int s, cb;
+    block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
+    if (a.needx && !a.needx[s]) return;
+    for (int i = threadIdx.x; i < NF; i += 64 * kWmW) twl[i] = a.T[i];
+    __syncthreads();
+    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
+    const int nround = (a.cb + RW - 1) / RW;
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double sqrtN = sqrt((double)a.nbin / 2.0);
+    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
+    int kw = NH;
+    if (a.KC) {
+        const int nn = (cbase & ~63) + lane;
+        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
+    }
+    const int mlane = (cbase + lane < cend && (!mask || mask[cbase + lane])) ? 1 : 0;
+    auto usable = [&](int n) {
+        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
+    };
+    const int nl = cbase + lane;
+    const double ch_mpow = nl < cend ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
+    const double ch_err = (a.errs && nl < cend) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
+    // the wave's next two rows in registers while these are transformed
+    using ET = typename std::conditional<DT == 0, float, double>::type;
+    constexpr int PJ = NMAX / 64;
+    ET pa[PJ], pb[PJ];
+    auto fetch = [&](ET (&p)[PJ], int m) {
+        const ET *src = reinterpret_cast<const ET *>(a.data) + ((int64_t)s * a.nchan + m) * (int64_t)NF;
+#pragma unroll
+        for (int i = 0; i < PJ; ++i) {
+            const int t = lane + 64 * i;
+            p[i] = src[t < NF ? t : NF - 1];
+        }
+    };
+    fetch(pa, min(cbase + wave, cend - 1));
+    fetch(pb, min(cbase + wave + kWmW, cend - 1));
+    for (int r = 0, nA = cbase + wave; r < nround; ++r, nA += RW) {
+        const int nB = nA + kWmW;
+        const bool liveA = usable(nA), liveB = usable(nB), live = liveA || liveB;
+        if (nA < cend && !liveA && lane < 4) a.chan[((int64_t)s * a.nchan + nA) * 4 + lane] = 0.0;
+        if (nB < cend && !liveB && lane < 4) a.chan[((int64_t)s * a.nchan + nB) * 4 + lane] = 0.0;
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < PJ; ++i) {
+                const int t = lane + 64 * i;
+                if (t < NF) buf[t] = cmk(liveA ? (double)pa[i] : 0.0, liveB ? (double)pb[i] : 0.0);
+            }
+        }
+        fetch(pa, min(nA + RW, cend - 1));
+        fetch(pb, min(nB + RW, cend - 1));
+        if (live) {
+            wfft::wave_sync();
+            int L = 1, rem = NF;
+            while (rem > 1) {
+                int R = 3;
+                while (rem % R) R += 2;
+                switch (R) {
+                    case 3: wmr_stage<3, NMAX>(buf, NF, L, twl, lane); break;
+                    case 5: wmr_stage<5, NMAX>(buf, NF, L, twl, lane); break;
+                    default: wmr_stage_g<NMAX>(buf, NF, L, R, twl, lane); break;
+                }
+                L *= R;
+                rem /= R;
+            }
+            // the pairs (Z_k, Z_{NF-k}), k <= N: each lane reads and
+            // rewrites only its own pairs' two slots
+            const double2 *MA = a.Mft + ((int64_t)mi * a.nchan + min(nA, cend - 1)) * NH;
+            const double2 *MB = a.Mft + ((int64_t)mi * a.nchan + min(nB, cend - 1)) * NH;
+            double pnA = 0.0, pdA = 0.0, pnB = 0.0, pdB = 0.0;
+            for (int k = lane; k <= N; k += 64) {
+                const int kn = k == 0 ? 0 : NF - k;
+                const double2 zk = buf[k], c = cconj(buf[kn]);
+                const double2 xa = cscale(cadd(zk, c), 0.5);
+                const double2 d = csub(zk, c);
+                const double2 xb = cmk(0.5 * d.y, -0.5 * d.x);       // d / 2i
+                const double qa = cabs2(xa), qb = cabs2(xb);
+                if (k >= a.kc) { pnA += qa; pnB += qb; }
+                if (k >= 1) { pdA += qa; pdB += qb; }
+                if (k >= 1 && k < kw) {
+                    buf[k] = cmulc(xa, MA[k]);
+                    buf[kn] = cmulc(xb, MB[k]);
+                }
+            }
+            pnA = wave_sum(pnA);
+            pdA = wave_sum(pdA);
+            pnB = wave_sum(pnB);
+            pdB = wave_sum(pdB);
+            const int rA = nA - cbase, rB = min(nB - cbase, 63);
+            double eA, eB;
+            if (a.errs) {
+                eA = readlane_d(ch_err, rA) * sqrtN;
+                eB = readlane_d(ch_err, rB) * sqrtN;
+            } else {
+                eA = sqrt(pnA / (double)(NH - a.kc) / (double)a.nbin) * sqrtN;
+                eB = sqrt(pnB / (double)(NH - a.kc) / (double)a.nbin) * sqrtN;
+            }
+            const double ieA = 1.0 / (eA * eA), ieB = 1.0 / (eB * eB);
+            const double mpA = readlane_d(ch_mpow, rA), mpB = readlane_d(ch_mpow, rB);
+            if (lane == 0) {
+                buf[0] = cmk(ieA, 0.0);
+                buf[NF] = cmk(ieB, 0.0);
+                if (liveA) {
+                    double *chan = a.chan + ((int64_t)s * a.nchan + nA) * 4;
+                    chan[0] = eA;
+                    chan[1] = ieA;
+                    chan[2] = pdA * ieA;          // Sd_n
+                    chan[3] = mpA * ieA;          // S_n at tau = 0
+                }
+                if (liveB) {
+                    double *chan = a.chan + ((int64_t)s * a.nchan + nB) * 4;
+                    chan[0] = eB;
+                    chan[1] = ieB;
+                    chan[2] = pdB * ieB;
+                    chan[3] = mpB * ieB;
+                }
+            }
+        }
+        __syncthreads();
+        // write-out: thread t -> channel c = t % 8 of the round, harmonics
+        // k = t / 8 + 32 j (X_0 = 0; slot 0 holds the row's 1/errs_FT^2)
+        {
+            const int c = threadIdx.x % RW, nc = cbase + r * RW + c;
+            if (nc < cend) {
+                const bool ok = !mask || mask[nc];
+                // row A: X_k at slot k; row B: at slot NF - k (k = 0: 1/errs_FT^2)
+                const double2 *b = lds + (c % kWmW) * SL;
+                const int o0 = c < kWmW ? 0 : NF, st = c < kWmW ? 1 : -1;
+                const double ie2 = ok ? b[o0].x : 0.0;
+                for (int k = threadIdx.x / RW; k < kw; k += 64 * kWmW / RW)
+                    Xs[(int64_t)k * a.nchan + nc] = (ok && k) ? cscale(b[o0 + st * k], ie2) : cmk(0.0, 0.0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // nbin / 2 <= 1024 not a power of two; odd nbin < 1024 (NF = nbin points)
 bool xspec_wm_supported(int nbin) {
     if (nbin & 1) return nbin >= 33 && nbin < kWmMaxN;
@@ -1583,9 +1743,31 @@ bool xspec_wm_supported(int nbin) {
         else hipLaunchKernelGGL((k_xspec_wm<1, NM, ODD>), g, b, lds, st, a);              \
     } while (0)
 
+// odd nbin: two rows per transform (k_xspec_wo) unless PPF_XSPEC_WO=0
+// (environment, read once: the one-row k_xspec_wm<ODD>)
+static bool use_xspec_wo() {
+    static const bool on = [] {
+        const char *e = getenv("PPF_XSPEC_WO");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
 hipError_t launch_xspec_wm(const XspecArgs &a, hipStream_t st) {
     const bool odd = a.nbin & 1;
     const int NF = rfft_len(a.nbin);
+    if (odd && use_xspec_wo()) {
+        const size_t lds = ((size_t)kWmW * (NF + 1) + NF) * sizeof(double2);
+        dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kWmW);
+        if (NF <= 512) {
+            if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wo<0, 512>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_xspec_wo<1, 512>), g, b, lds, st, a);
+        } else {
+            if (a.dtype == 0) hipLaunchKernelGGL((k_xspec_wo<0, 1024>), g, b, lds, st, a);
+            else hipLaunchKernelGGL((k_xspec_wo<1, 1024>), g, b, lds, st, a);
+        }
+        return hipGetLastError();
+    }
     const size_t lds = ((size_t)kWmW * (odd ? NF : NF + 2) + NF) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kWmW);
     if (NF <= 512) {

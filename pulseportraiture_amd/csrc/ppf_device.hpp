@@ -420,12 +420,40 @@ __device__ void mr_stage(double2 *buf, int N, int L, const double2 *__restrict__
 // One output per thread per pass (NT threads starting at t0), O(N R) work;
 // all of a thread's reads are done before the caller's barrier, its writes
 // after it.
-// Outputs are formed G = 4 at a time with the q loop outside, so a thread
-// has four independent LDS / twiddle read chains in flight instead of one
-// dependent chain per output (the same arithmetic per output, so the same
-// bits); an output past N is computed on a clamped index and dropped.
 template <int QO>
 __device__ __forceinline__ void gr_stage_read(const double2 *buf, int N, int L, int R,
+                                              const double2 *__restrict__ T, bool inv, int t0, int NT,
+                                              double2 (&y)[QO]) {
+    const int nb = N / R, ts = N / (R * L), RL = R * L;
+#pragma unroll
+    for (int i = 0; i < QO; ++i) {
+        const int o = t0 + i * NT;
+        if (o < N) {
+            const int blk = o / RL, rem = o - blk * RL, m = rem / L, k = rem - m * L;
+            const int j = blk * L + k;
+            int e = k * ts + m * nb;
+            e = e >= N ? e - N : e;
+            double2 acc = buf[j];
+            for (int q = 1, idx = e; q < R; ++q) {
+                const double2 w = twid(T, idx, inv);
+                acc = cadd(acc, cmul(buf[j + q * nb], w));
+                idx += e;
+                idx = idx >= N ? idx - N : idx;
+            }
+            y[i] = acc;
+        }
+    }
+}
+// gr_stage_read with the outputs formed G = 4 at a time and the q loop
+// outside, so a lane has four independent LDS read chains in flight instead
+// of one dependent chain per output (the same arithmetic per output, so the
+// same bits); an output past N is computed on a clamped index and dropped.
+// The wave-per-row kernels take it (k_xspec_wm / k_xspec_wo: nbin 1022 and
+// 1023 +3-4 %); in the block-FFT kernels its registers cost more than it
+// gains (k_guess at nbin 1000 / 1536: 152 -> 185 / 248 -> 278 ms per 72
+// calls, profiles/r05/ab_r5g_status.txt), so they keep the loop above.
+template <int QO>
+__device__ __forceinline__ void gr_stage_read4(const double2 *buf, int N, int L, int R,
                                               const double2 *__restrict__ T, bool inv, int t0, int NT,
                                               double2 (&y)[QO]) {
     const int nb = N / R, ts = N / (R * L), RL = R * L;

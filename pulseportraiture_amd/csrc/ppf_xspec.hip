@@ -1385,7 +1385,7 @@ __device__ __forceinline__ void wmr_stage(double2 *buf, int N, int L, const doub
 template <int NMAX>
 __device__ __forceinline__ void wmr_stage_g(double2 *buf, int N, int L, int R, const double2 *tw, int lane) {
     double2 y[NMAX / 64];
-    gr_stage_read<NMAX / 64>(buf, N, L, R, tw, false, lane, 64, y);
+    gr_stage_read4<NMAX / 64>(buf, N, L, R, tw, false, lane, 64, y);
     wfft::wave_sync();
     gr_stage_write<NMAX / 64>(buf, N, lane, 64, y);
     wfft::wave_sync();

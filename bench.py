@@ -14,6 +14,11 @@ the result records when N > 1 (weak scaling: N_sub per GPU is fixed).
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher (WORLD_SIZE unset), bench.py starts its N
+ranks itself (one child process per GPU, dist.launch_local) and forwards
+rank 0's JSON line; under torchrun / torch.distributed.run each process is
+one rank.
+
 Rank 0 prints ONE JSON line.  It carries `roofline` for the dominant kernel
 (algorithmic bytes from HIP events around each kernel on the launch stream)
 and `cpu_baseline` (the NumPy/SciPy oracle on a bounded sample, 1 core).
@@ -37,6 +42,11 @@ FP64_PEAK_TF = 78.6            # MI355X spec: FP64 vector = FP64 matrix = 78.6 T
 
 
 MOMX = {"auto": None, "x": True, "fused": False}
+# who started the ranks: "bench-self" (bench.py --gpus N started its own),
+# "env" (WORLD_SIZE came from the environment: torchrun / torch.distributed.run),
+# or "none" (N = 1)
+LAUNCHER = os.environ.get("PPF_LAUNCHER") or (
+    "env" if "WORLD_SIZE" in os.environ else "none")
 
 
 def parse():
@@ -470,7 +480,7 @@ def bench_align(args):
                            "weighted rotate-and-sum)" % (args.nsub, nchan,
                                                           nbin),
                            nsub_per_gpu=args.nsub, nchan=nchan, nbin=nbin,
-                           fit="align", parallelism="dp%d" % world),
+                           fit="align", parallelism="dp%d" % world, launcher=LAUNCHER),
                roofline=roof, solver_fp64=solver, kernels=kernels, cpu_baseline=None,
                template_peak=float(torch.as_tensor(m).abs().max()), **fitstats)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -712,7 +722,7 @@ def bench_gettoas(args):
                            % (nfile, per, nchan, nbin), nfile=nfile,
                            host_memory="pinned" if args.pinned else "pageable",
                            nsub_per_archive=per, nchan=nchan, nbin=nbin,
-                           fit="gettoas", parallelism="dp%d" % world,
+                           fit="gettoas", parallelism="dp%d" % world, launcher=LAUNCHER,
                            sharding="archives" if nfile >= world and
                            world > 1 else "sub-ints" if world > 1 else None,
                            load_data="PSRFITS fast path (psrfits.load_data:"
@@ -817,8 +827,30 @@ def bench_single(args):
     print(json.dumps(out), flush=True)
 
 
+def self_launch(args):
+    """`python bench.py --gpus N` (N > 1) with no launcher: start the N ranks
+    here (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, dist.launch_local) and return their exit status; rank 0's
+    JSON line is forwarded.  This parent never touches the GPU (counting
+    devices does not initialise HIP) and never re-execs.  With fewer visible
+    devices than ranks (the one-GPU gloo rehearsal) ranks share devices
+    round-robin; RCCL needs one device per rank, so that raises for nccl."""
+    import torch
+    from pulseportraiture_amd import dist
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus and args.dist_backend == "nccl":
+        print("error: --gpus %d with %d visible devices (RCCL needs one "
+              "device per rank)" % (args.gpus, ndev), file=sys.stderr)
+        return 2
+    local = (lambda r: r % ndev) if 0 < ndev < args.gpus else None
+    return dist.launch_local(os.path.abspath(__file__), sys.argv[1:],
+                             args.gpus, local_ranks=local)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     if args.fit == "single":
         return bench_single(args)
     if args.fit == "align":
@@ -1177,7 +1209,7 @@ def main():
                                "cross spectrum (block FFT + k_moments)"),
                            zap_frac=args.zap_frac,
                            fit=args.fit, fit_flags=FIT["flags"],
-                           parallelism="dp%d" % world),
+                           parallelism="dp%d" % world, launcher=LAUNCHER),
                roofline=roof, fp64_roofline=fp64, solver_fp64=solver,
                stage_ms=stages, kernels=kernels,
                # algorithmic HBM bytes of the priced kernels per fit (the

@@ -45,7 +45,8 @@ extern "C" {
  * ppf_copy_from_pinned (added in round 4 without a bump), and
  * ppf_kernel_ms_history slot 0 = the first moment pass of either kind;
  * ppf_solver_ms_history, ppf_host_copy. */
-#define PPF_ABI_VERSION 4
+/* ABI 5 (round 6): ppf_rotate_batch_ref. */
+#define PPF_ABI_VERSION 5
 
 enum ppf_error {
     PPF_OK = 0,
@@ -281,6 +282,17 @@ int ppf_fit2_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream);
 int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
                      int32_t in_dtype, const void *in, const double *phases,
                      double *out, void *stream);
+
+/* ppf_rotate_batch with the reference's output length (ABI 5): the public
+ * rotate routines call numpy's irfft WITHOUT a length (pplib.py:2466,
+ * 2508-2512, 2550, 2652; pptoaslib.py:89), which at odd nbin returns
+ * nbin - 1 samples: the inverse of length nbin - 1 of X_0..X_{nbin/2}, the
+ * last harmonic taken as the Nyquist term (its imaginary part dropped).
+ * out: [nrows][nbin] at even nbin (identical to ppf_rotate_batch),
+ * [nrows][nbin - 1] at odd nbin. */
+int ppf_rotate_batch_ref(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
+                         int32_t in_dtype, const void *in, const double *phases,
+                         double *out, void *stream);
 
 /* ppalign.align_archives accumulation (ppalign.py:236-247, the inner
  * "aligned_port += weights * rotate_data(...)" / "total_weights += weights"

@@ -119,6 +119,12 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
     return PPF_OK;
 }
 
+// 16-moment sets on the non-power-of-two shapes too (their moments always
+// come from X): nbin 1000 278-280k -> 293-294k, 1536 178-179k -> 183k fits/s
+// in one call (profiles/r05/ab_m16_status.txt)
+#ifndef PPF_MOM16_BLOCK
+#define PPF_MOM16_BLOCK 1
+#endif
 struct FitLayout {
     size_t M, X, chan, stats, x0, gP, gw, nuref, Msum, gpart, gwx, gflag, state, partials, active, mom, dphi,
         mres, hcen, Mpow, MP, KC, needx, xslot, rclist, Bt, total;
@@ -128,14 +134,19 @@ struct FitLayout {
     int xcap;     // X slots
 };
 
+// 16 moments about each wave's band centre where the moments come from a
+// stored X and that was measured to pay (ab_m16_status.txt): the wave
+// shapes' MOM_X path and (PPF_MOM16_BLOCK) the non-power-of-two nbin.
+// Power-of-two nbin off the wave shapes (32-128, 4096, 8192) and block sizes
+// the wave kernels refuse keep 32 moments about the global centre (radius
+// 4.5 instead of 0.73, so fewer re-centring passes).
+static bool mom16_layout(const FitLayout &L, int nbin) {
+    return L.momx || (!L.fused && PPF_MOM16_BLOCK && !ppf::is_pow2(ppf::rfft_len(nbin)));
+}
+
+
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// 16-moment sets on the non-power-of-two shapes too (their moments always
-// come from X): nbin 1000 278-280k -> 293-294k, 1536 178-179k -> 183k fits/s
-// in one call (profiles/r05/ab_m16_status.txt)
-#ifndef PPF_MOM16_BLOCK
-#define PPF_MOM16_BLOCK 1
-#endif
 FitLayout fit_layout(const ppf_fit_desc *d) {
     FitLayout L{};
     const size_t nharm = (size_t)d->nbin / 2 + 1;
@@ -166,7 +177,7 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
     L.mom = o;   o += align256(sizeof(double2) * nsub * 2 * nchan * (size_t)ppf::kMoments);
     L.dphi = o;  o += align256(sizeof(double) * nsub * nchan * 2);
     L.mres = o;  o += align256(sizeof(double) * nsub * 2 * nchan);
-    L.hcen = o;  o += (L.momx || (!L.fused && PPF_MOM16_BLOCK)) ? align256(sizeof(double) * nsub * 2 * nchan) : 0;
+    L.hcen = o;  o += mom16_layout(L, d->nbin) ? align256(sizeof(double) * nsub * 2 * nchan) : 0;
     L.Mpow = o;  o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
     L.MP = o;    o += align256(sizeof(double) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan * nharm);
     L.KC = o;    o += align256(sizeof(int32_t) * (size_t)(d->nmodel > 0 ? d->nmodel : 1) * nchan);
@@ -245,6 +256,11 @@ void ppf_destroy(ppf_ctx *ctx) {
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
     for (auto &v : ctx->pass_ev)
+        for (auto &pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    for (auto &v : ctx->solv_ev)
         for (auto &pr : v) {
             (void)hipEventDestroy(pr.first);
             (void)hipEventDestroy(pr.second);
@@ -405,8 +421,11 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         auto &kv = ctx->solv_kind[slot];
         if ((int)v.size() <= ctx->nsolv[slot]) {
             std::pair<hipEvent_t, hipEvent_t> pr{};
-            if (hipEventCreate(&pr.first) != hipSuccess || hipEventCreate(&pr.second) != hipSuccess)
+            if (hipEventCreate(&pr.first) != hipSuccess) return nullptr;
+            if (hipEventCreate(&pr.second) != hipSuccess) {
+                (void)hipEventDestroy(pr.first);
                 return nullptr;
+            }
             v.push_back(pr);
             kv.push_back(0);
         }
@@ -569,10 +588,8 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     sa.mom = (double2 *)(ws + L.mom);
     sa.dphi = (double *)(ws + L.dphi);
     sa.mres = (double *)(ws + L.mres);
-    // 16 moments about each wave's band centre wherever the moments come
-    // from a stored X: the wave shapes' MOM_X path and (PPF_MOM16_BLOCK) the
-    // non-power-of-two shapes
-    const bool m16 = L.momx || (!L.fused && PPF_MOM16_BLOCK);
+    // 16 moments about each wave's band centre (mom16_layout)
+    const bool m16 = mom16_layout(L, d->nbin);
     sa.mom16 = m16;
     sa.hcen = m16 ? (double *)(ws + L.hcen) : nullptr;
     sa.xslot = xslot;
@@ -618,9 +635,12 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
                     auto &v = ctx->pass_ev[slot];
                     if ((int)v.size() <= ctx->npass[slot]) {
                         std::pair<hipEvent_t, hipEvent_t> pr{};
-                        if ((e = hipEventCreate(&pr.first)) != hipSuccess ||
-                            (e = hipEventCreate(&pr.second)) != hipSuccess)
+                        if ((e = hipEventCreate(&pr.first)) != hipSuccess)
                             return hip_fail(ctx, e, "hipEventCreate");
+                        if ((e = hipEventCreate(&pr.second)) != hipSuccess) {
+                            (void)hipEventDestroy(pr.first);
+                            return hip_fail(ctx, e, "hipEventCreate");
+                        }
                         v.push_back(pr);
                     }
                     pe = &v[ctx->npass[slot]++];
@@ -690,8 +710,8 @@ int ppf_fit2_batch(ppf_ctx *ctx, const ppf_fit_desc *desc, void *stream) {
     return ppf_fit_batch(ctx, &d, stream);
 }
 
-int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
-                     const double *phases, double *out, void *stream) {
+static int rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
+                        const double *phases, double *out, void *stream, bool ref_len) {
     if (!ctx) return PPF_EINVAL;
     if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nrows < 0 || (nrows > 0 && (!in || !phases || !out)))
@@ -704,9 +724,23 @@ int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype
     const double2 *T, *T2;
     int rc = twiddles(ctx, nbin, st, &T, &T2);
     if (rc) return rc;
-    ppf::RotateArgs a{nbin, rfft_log2(nbin), in_dtype, in, phases, T, T2, out};
+    ppf::RotateArgs a{nbin, rfft_log2(nbin), in_dtype, in, phases, T, T2, out, 0, T, T2};
+    if (ref_len && (nbin & 1)) {
+        a.ref_len = 1;
+        if ((rc = twiddles(ctx, nbin - 1, st, &a.Te, &a.T2e))) return rc;
+    }
     if ((e = ppf::launch_rotate(a, nrows, st)) != hipSuccess) return hip_fail(ctx, e, "k_rotate");
     return PPF_OK;
+}
+
+int ppf_rotate_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
+                     const double *phases, double *out, void *stream) {
+    return rotate_batch(ctx, nrows, nbin, in_dtype, in, phases, out, stream, false);
+}
+
+int ppf_rotate_batch_ref(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype, const void *in,
+                         const double *phases, double *out, void *stream) {
+    return rotate_batch(ctx, nrows, nbin, in_dtype, in, phases, out, stream, true);
 }
 
 size_t ppf_align_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin) {

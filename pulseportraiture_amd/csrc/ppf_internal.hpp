@@ -155,6 +155,12 @@ struct RotateArgs {
     const double *phases;
     const double2 *T, *T2;
     double *out;
+    // ref_len (odd nbin only): the reference's length-less irfft
+    // (pplib.py:2466, 2508-2512, 2550, 2652): nbin - 1 samples per row from
+    // X_0..X_{nbin/2}, the last as the Nyquist term; out rows of nbin - 1;
+    // Te / T2e the twiddles of nbin - 1
+    int ref_len;
+    const double2 *Te, *T2e;
 };
 
 // ppalign accumulation (ppalign.py:236-247): per channel, sum_s w_sn *

@@ -955,6 +955,39 @@ __global__ __launch_bounds__(kBlock) void k_rotate(RotateArgs a) {
         }
     }
     __syncthreads();
+    if (odd && a.ref_len) {
+        // the reference's irfft without a length: 2 N = nbin - 1 samples
+        // from X_0..X_N, X_N as the Nyquist term (imaginary part dropped):
+        // the even-length packed inverse with the nbin - 1 twiddles (as
+        // k_gauss_port's scattered rows)
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < KH) lds[k] = Xk[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < N) {
+                Xk[i] = lds[k];
+                Xn[i] = lds[N - k];
+                if (k == 0) Xn[i].y = 0.0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+            const int k = threadIdx.x + i * kBlock;
+            if (k < N) lds[k] = irfft_prebin(Xk[i], Xn[i], a.T2e[k]);
+        }
+        __syncthreads();
+        lds_fft_n<MX>(lds, N, a.Te, true);
+        const double sc = 1.0 / (double)N;
+        double2 *o = reinterpret_cast<double2 *>(a.out) + row * (int64_t)N;
+        for (int j = threadIdx.x; j < N; j += kBlock) o[j] = cscale(lds[j], sc);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
         int k = threadIdx.x + i * kBlock;

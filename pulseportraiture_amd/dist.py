@@ -135,3 +135,77 @@ def raise_if_any_failed(err, device=None):
 def backend():
     """The process group's backend ('nccl' = RCCL, 'gloo'), or None."""
     return dist.get_backend() if dist.is_initialized() else None
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_local(script, argv, nproc, local_ranks=None, poll_s=0.2):
+    """Start `nproc` ranks of `script` on this node and wait for them: the
+    launcher `bench.py --gpus N` uses when nothing set WORLD_SIZE (as
+    ``torch.distributed.run --nnodes 1 --nproc-per-node N`` would).
+
+    This process never touches a GPU and never re-execs: each rank is a child
+    process (``sys.executable script argv``) with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR (127.0.0.1) / MASTER_PORT set.  LOCAL_RANK is
+    the rank (one GPU per rank) unless `local_ranks` maps it (the one-GPU
+    gloo rehearsal puts every rank on device 0).  Rank 0's stdout is
+    forwarded to this process's stdout line by line (it carries the bench
+    JSON line); the other ranks' stdout goes to stderr with a rank prefix.
+    If any rank fails, the others are terminated (by their own PIDs) so none
+    waits forever in a collective.  Returns 0, or the first failing rank's
+    exit code (1 if that was a signal)."""
+    import subprocess
+    import sys
+    import threading
+    import time
+    port = free_port()
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_RANK=str(local_ranks(r) if local_ranks else r),
+                   LOCAL_WORLD_SIZE=str(nproc), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PPF_LAUNCHER="bench-self")
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv),
+                                      env=env, stdout=subprocess.PIPE,
+                                      text=True, bufsize=1))
+
+    def pump(r, p):
+        dst = sys.stdout if r == 0 else sys.stderr
+        for ln in p.stdout:
+            dst.write(ln if r == 0 else "[rank %d] %s" % (r, ln))
+            dst.flush()
+
+    pumps = [threading.Thread(target=pump, args=(r, p), daemon=True)
+             for r, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    rc = 0
+    t_term = None
+    live = list(range(nproc))
+    while live:
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print("[launcher] rank %d exited with %d; stopping the "
+                      "others" % (r, c), file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].terminate()
+                t_term = time.monotonic()
+        if live and t_term is not None and time.monotonic() - t_term > 30.0:
+            for q in live:                  # ignored SIGTERM (e.g. in a collective)
+                procs[q].kill()
+        if live:
+            time.sleep(poll_s)
+    for t in pumps:
+        t.join(timeout=10)
+    return rc

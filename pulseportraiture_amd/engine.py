@@ -467,9 +467,11 @@ def _fit_slice(lib, dev, per_sub, c0, c1, n_x, cfg, workspace, d=None,
                 workspace=workspace, _keep=keep, _flat=flat)
 
 
-def rotate_rows(rows, phases, dev=None):
+def rotate_rows(rows, phases, dev=None, ref_len=False):
     """irfft(rfft(row) * exp(2 pi i k phase)) for each row of rows [..., nbin]
-    (float64 output, same leading shape)."""
+    (float64 output, same leading shape).  ref_len: the reference's public
+    rotate routines' length-less irfft (ppf_rotate_batch_ref): nbin - 1
+    samples per row at odd nbin; otherwise (internal callers) nbin."""
     dev = device(dev)
     r = to_dev(rows, dev, _data_dtype(rows)) if isinstance(rows, torch.Tensor) \
         else host_to_dev(rows, dev, _data_dtype(rows))
@@ -479,14 +481,16 @@ def rotate_rows(rows, phases, dev=None):
     ph = to_dev(phases, dev, torch.float64).reshape(-1).contiguous()
     if ph.numel() != r2.shape[0]:
         raise ValueError("need one phase per row")
-    out = torch.empty((r2.shape[0], nbin), dtype=torch.float64, device=dev)
+    nout = nbin - 1 if (ref_len and nbin % 2) else nbin
+    out = torch.empty((r2.shape[0], nout), dtype=torch.float64, device=dev)
     ctx = _lib.context(dev.index)
-    rc = _lib.load().ppf_rotate_batch(
-        ctx, r2.shape[0], nbin,
-        _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
-        _p(r2), _p(ph), _p(out), _stream(dev))
+    lib = _lib.load()
+    fn = lib.ppf_rotate_batch_ref if ref_len else lib.ppf_rotate_batch
+    rc = fn(ctx, r2.shape[0], nbin,
+            _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
+            _p(r2), _p(ph), _p(out), _stream(dev))
     _lib.check(rc, ctx)
-    return out.reshape(shape)
+    return out.reshape(tuple(shape[:-1]) + (nout,))
 
 
 def align_accum(data, phases, weights, out, wsum, dev=None):
@@ -571,10 +575,31 @@ def noise_rows(rows, frac=4, dev=None):
     return out.reshape(shape[:-1])
 
 
+# largest prime factor of the transform length the LDS path takes for
+# get_noise_PS of a single flattened row: the generic-radix stage costs
+# O(N R) per row (R the prime), so a length like 8186 = 2 x 4093 would be a
+# 4093-point direct DFT inside one workgroup; rocFFT's Bluestein is faster
+NOISE_MAX_PRIME = 61
+
+
+def _max_prime_factor(n):
+    p, m, f = 2, n, 1
+    while p * p <= m:
+        while m % p == 0:
+            f, m = p, m // p
+        p += 1
+    return max(f, m) if m > 1 else f
+
+
 def noise_len_supported(n):
-    """Row lengths ppf_noise_batch transforms (its LDS FFT): even 32..8192,
-    odd 33..4095."""
-    return 32 <= n <= (8192 if n % 2 == 0 else 4095)
+    """Row lengths get_noise_PS(chans=False) sends to ppf_noise_batch (its LDS
+    FFT): even 32..8192 or odd 33..4095 (every length ppf_noise_batch
+    accepts) whose transform length -- n / 2 complex points at even n, n at
+    odd n -- has no prime factor above NOISE_MAX_PRIME; the rest go to the
+    device FFT library (noise_long)."""
+    if not 32 <= n <= (8192 if n % 2 == 0 else 4095):
+        return False
+    return _max_prime_factor(n // 2 if n % 2 == 0 else n) <= NOISE_MAX_PRIME
 
 
 def noise_long(row, frac=4, dev=None):

@@ -383,8 +383,8 @@ def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
     if DM == 0.0:
         nrows = int(np.prod(shape[:-1])) if ndim > 1 else 1
         out = engine.rotate_rows(data.reshape(nrows, nbin),
-                                 np.full(nrows, float(phase)))
-        return engine.dev_to_host(out).reshape(shape)
+                                 np.full(nrows, float(phase)), ref_len=True)
+        return engine.dev_to_host(out).reshape(shape[:-1] + (out.shape[-1],))
     d4 = data                       # only read: the result is a new array
     while d4.ndim != 4:
         d4 = d4[None]
@@ -418,8 +418,9 @@ def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
         return 0
     ph = phase + D[:, None] * fterm
     ph = np.broadcast_to(ph[:, None, :], (nsub, npol, nchan))
-    out = engine.rotate_rows(d4.reshape(-1, nbin), ph.reshape(-1))
-    out = engine.dev_to_host(out).reshape(d4.shape)
+    out = engine.rotate_rows(d4.reshape(-1, nbin), ph.reshape(-1),
+                             ref_len=True)
+    out = engine.dev_to_host(out).reshape(d4.shape[:3] + (out.shape[-1],))
     if ndim == 1:
         return out[0, 0, 0]
     if ndim == 2:
@@ -438,13 +439,14 @@ def rotate_portrait(port, phase=0.0, DM=None, P=None, freqs=None,
         D = Dconst * DM / P
         ph = phase + D * (np.asarray(freqs, dtype=float) ** -2.0 -
                           nu_ref ** -2.0)
-    return engine.rotate_rows(port, ph).cpu().numpy()
+    return engine.rotate_rows(port, ph, ref_len=True).cpu().numpy()
 
 
 def rotate_profile(profile, phase=0.0):
     """pplib.py:2641-2652."""
     profile = np.asarray(profile)
-    return engine.rotate_rows(profile[None, :], [phase]).cpu().numpy()[0]
+    return engine.rotate_rows(profile[None, :], [phase],
+                              ref_len=True).cpu().numpy()[0]
 
 
 def fit_phase_shift(data, model, noise=None, bounds=[-0.5, 0.5], Ns=100):

@@ -393,6 +393,16 @@ class GetTOAs(object):
         if not prms:
             return np.zeros((0, len(d.freqs[0]), nbin)), \
                 np.zeros(0, dtype=np.int32)
+        if nbin % 2 and any(p[1] != 0.0 for p in prms):
+            # the reference's scattered model is the length-less irfft of
+            # gen_gaussian_portrait (pplib.py:957): nbin - 1 bins at odd nbin,
+            # then fitted against nbin-bin data (a transform of another
+            # length); the batched fit takes one nbin for both, so refuse
+            # rather than fit a zero-padded model
+            raise NotImplementedError(
+                "GetTOAs with a scattered Gaussian model (TAU != 0) at odd "
+                "nbin = %d: the reference fits an nbin - 1 bin model there" %
+                nbin)
         ck = (bool(fit_scat), nbin, tuple(cache))
         models = mc.get(ck)
         if models is None:

@@ -68,7 +68,7 @@ def rotate_portrait_full(port, phi, DM, GM, freqs, nu_DM=np.inf,
                       nu_GM, P, False)
     port = np.asarray(port)
     ph = np.broadcast_to(np.asarray(ph, dtype=float), (port.shape[0],))
-    return engine.rotate_rows(port, ph).cpu().numpy()
+    return engine.rotate_rows(port, ph, ref_len=True).cpu().numpy()
 
 
 def _status_message(rc, sub_id):

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_struct_layouts_match():
     lib = _lib.load()
-    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 5
     assert lib.ppf_sizeof_fit_desc() == ctypes.sizeof(_lib.FitDesc)
     assert lib.ppf_sizeof_result() == 8 * _lib.RESULT_DOUBLES == 256
 

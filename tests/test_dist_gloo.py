@@ -486,3 +486,52 @@ def test_gettoas_scattering_fits_sharded_equal_serial(mode, nfile):
         for k in serial:
             if k != "fit_durations":            # wall-clock times
                 assert repr(got[r][k]) == repr(serial[k]), (r, k)
+
+
+# ---- the bench.py self-launcher (dist.launch_local), CPU / gloo ----------
+
+def _launch(argv, nproc, timeout=180):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = os.path.join(root, "tests", "launch_probe.py")
+    code = ("import sys; sys.path.insert(0, %r); "
+            "from pulseportraiture_amd import dist; "
+            "sys.exit(dist.launch_local(%r, %r, %d, "
+            "local_ranks=lambda r: 0))" % (root, probe, argv, nproc))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True,
+                         text=True, timeout=timeout, env=env)
+    lines = [json.loads(ln) for ln in out.stdout.splitlines()
+             if ln.startswith("{")]
+    return out.returncode, lines, out.stdout, out.stderr
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_self_launcher_starts_ranks_and_forwards_rank0(nproc):
+    """bench.py --gpus N without torchrun: N child ranks, each with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, gathered rows in global order,
+    exactly one JSON line (rank 0's) on the launcher's stdout."""
+    rc, lines, so, se = _launch(["11"], nproc)
+    assert rc == 0, se
+    assert len(lines) == 1, so
+    d = lines[0]
+    assert d["world"] == nproc and d["rank"] == 0 and d["local_rank"] == 0
+    assert d["launcher"] == "bench-self" and d["master"] == "127.0.0.1"
+    assert d["first_col"] == [float(i) for i in range(11)]
+    for r in range(1, nproc):
+        assert "[rank %d] rank %d local 0 done" % (r, r) in se
+
+
+def test_self_launcher_fails_when_a_rank_fails():
+    """A rank that exits non-zero fails the launch (its exit code), and the
+    ranks left waiting in the all-gather are stopped, not left hanging."""
+    import time
+    t0 = time.monotonic()
+    rc, lines, so, se = _launch(["11", "1"], 2, timeout=120)
+    assert rc == 3, (so, se)
+    assert lines == []
+    assert "rank 1 exited with 3" in se
+    assert time.monotonic() - t0 < 100

@@ -161,3 +161,25 @@ def test_bench_two_ranks_rehearsal(fit):
         assert d["results_sha256"] == one["results_sha256"]
     if fit == "gettoas":
         assert d["toas"] == 48 and d["config"]["sharding"] == "archives"
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher (WORLD_SIZE unset) starts
+    its own two ranks (here both on the box's one GPU, over gloo) and prints
+    rank 0's line: n_gpus 2, the gathered records equal to one rank fitting
+    every sub-int."""
+    common = ["--nchan", "64", "--nbin", "512", "--steps", "1", "--warmup",
+              "1", "--passes", "1", "--cpu-sample", "0"]
+    env_keys = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")
+    saved = {k: os.environ.pop(k) for k in env_keys if k in os.environ}
+    try:
+        d = _bench_one(["--gpus", "2", "--dist-backend", "gloo", "--nsub",
+                        "48"] + common)
+    finally:
+        os.environ.update(saved)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["launcher"] == "bench-self"
+    assert d["fits_converged_frac"] == 1.0
+    one = _bench_one(["--nsub", "96"] + common)
+    assert one["n_gpus"] == 1 and one["config"]["launcher"] == "none"
+    assert d["results_sha256"] == one["results_sha256"]

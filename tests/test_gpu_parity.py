@@ -63,7 +63,7 @@ def test_noise_matches_reference(ppl):
     # chans=False ravels the portrait (pplib.py:2334-2338): 64 x 2048 and an
     # odd length go through the device FFT library (no LDS-size cap); the
     # restatement is the reference's own NumPy arithmetic
-    for shape in ((64, 2048), (3, 1001), (1002,)):
+    for shape in ((64, 2048), (3, 1001), (1002,), (8186,), (1022,), (1000,)):
         x = np.random.default_rng(4).normal(size=shape)
         F = np.fft.rfft(x.ravel())
         p = np.real(F * np.conj(F)) / x.size
@@ -118,13 +118,36 @@ def test_rotate_any_nbin_matches_numpy(ppl, nbin):
     2 x 17 x 59, 4094 = 2 x 23 x 89) LDS FFTs, and at odd nbin (33, 127
     prime, 511 = 7 x 73, 1001, 1023, 4095 = 3^2 5 7 13: the row as nbin
     complex points, Hermitian inverse), against its own NumPy arithmetic:
-    rfft, phasor, irfft."""
+    rfft, phasor, irfft -- the irfft WITHOUT a length, as the reference calls
+    it (pplib.py:2466, 2508-2512, 2550, 2652; pptoaslib.py:89): at odd nbin
+    the public routines return nbin - 1 samples.  The internal full-length
+    rotation (engine.rotate_rows, used by the PSRFITS dedispersion) keeps
+    nbin samples: irfft(..., n=nbin)."""
+    from pulseportraiture_amd import engine, pptoaslib
     x = np.random.default_rng(nbin).normal(size=(3, nbin))
     ph = 0.2718
     k = np.arange(nbin // 2 + 1)
-    want = np.fft.irfft(np.fft.rfft(x, axis=-1) *
-                        np.exp(2j * np.pi * k * ph), n=nbin, axis=-1)
+    X = np.fft.rfft(x, axis=-1) * np.exp(2j * np.pi * k * ph)
+    want = np.fft.irfft(X, axis=-1)
+    assert want.shape[-1] == nbin - (nbin % 2)
     np.testing.assert_allclose(ppl.rotate_data(x, ph), want, atol=1e-11)
+    np.testing.assert_allclose(ppl.rotate_data(x[0], ph), want[0], atol=1e-11)
+    np.testing.assert_allclose(ppl.rotate_portrait(x, ph), want, atol=1e-11)
+    np.testing.assert_allclose(ppl.rotate_profile(x[1], ph), want[1],
+                               atol=1e-11)
+    # DM != 0 (4-D branch, pplib.py:2467-2512) and rotate_portrait_full
+    P0, f = 1.0 / 345.67890123456789, np.array([1300.0, 1400.0, 1500.0])
+    phs = ph + ppl.Dconst * 12.5 / P0 * (f ** -2.0 - 1450.0 ** -2.0)
+    Xd = np.fft.rfft(x, axis=-1) * np.exp(2j * np.pi * np.outer(phs, k))
+    np.testing.assert_allclose(ppl.rotate_data(x, ph, 12.5, P0, f, 1450.0),
+                               np.fft.irfft(Xd, axis=-1), atol=1e-10)
+    np.testing.assert_allclose(
+        pptoaslib.rotate_portrait_full(x, ph, 12.5, 0.0, f, 1450.0, np.inf,
+                                       P0), np.fft.irfft(Xd, axis=-1),
+        atol=1e-10)
+    full = engine.rotate_rows(x, np.full(3, ph)).cpu().numpy()
+    np.testing.assert_allclose(full, np.fft.irfft(X, n=nbin, axis=-1),
+                               atol=1e-11)
 
 
 def test_rotate_round_trip_and_bad_shapes(ppl, capsys):

@@ -192,3 +192,17 @@ def test_substituted_epoch_type_takes_the_object_path(monkeypatch):
                         False, ok_common="all")
     assert [repr(t.MJD) for t in fast.TOA_list] == \
         [repr(t.MJD) for t in obj.TOA_list]
+
+
+def test_noise_length_rule():
+    """get_noise_PS(chans=False) sends a flattened row to the LDS FFT only
+    when its transform length has no prime factor above NOISE_MAX_PRIME
+    (8186 = 2 x 4093 was a 4093-point direct DFT per row); the
+    rest take the device FFT library."""
+    from pulseportraiture_amd import engine
+    ok = [2048, 1000, 1536, 4096, 8192, 1023, 4095, 33, 2006]
+    lib = [8186, 1022, 4094, 127, 1002, 30, 8194, 4097]
+    assert all(engine.noise_len_supported(n) for n in ok)
+    assert not any(engine.noise_len_supported(n) for n in lib)
+    assert engine._max_prime_factor(2 * 3 * 167) == 167
+    assert engine._max_prime_factor(1) == 1

@@ -1098,6 +1098,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef PPF_MOM_KU
 #define PPF_MOM_KU 4
 #endif
+#ifndef PPF_MOM_ILP
+#define PPF_MOM_ILP 1
+#endif
 // M16: the call's moment count (a.mom16: 16 on the moments-from-X path, 32
 // otherwise), a template argument so the MFMA loop carries no branch
 template <bool M16>
@@ -1145,6 +1148,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_MOM_
     // batches of 4 K-steps (16 harmonics), software-pipelined: the next
     // batch's loads are in flight while this one's MFMAs run
     constexpr int KU = PPF_MOM_KU;
+#if PPF_MOM_ILP
+    // Round 6: no serial chains through a batch.  The K-step phasors are
+    // Eb W4^t from the batch's base phasor Eb (one product each, all
+    // independent; Eb itself advances by W4^KU once per batch), and the
+    // m < 16 contraction runs on two accumulator pairs (even / odd K-steps,
+    // summed at the end), so consecutive MFMAs do not wait for each other:
+    // the kernel waited on instruction dependencies 63 % of its wave cycles
+    // (profiles/r05/sq_c2_r5a.txt) at half the HBM rate
+    double2 Wt[KU];
+    Wt[0] = cmk(1.0, 0.0);
+#pragma unroll
+    for (int t = 1; t < KU; ++t) Wt[t] = cmul(Wt[t - 1], W4);
+    const double2 WB = cmul(Wt[KU - 1], W4);
+    f64x4 dre0b = dre0, dim0b = dre0;
+#endif
     double2 xa[KU], xb[KU];
     // The loads are unconditional (clamped to a valid harmonic; values past
     // the cutoff or of a masked channel are replaced by 0 after the load):
@@ -1162,21 +1180,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_MOM_
     };
     auto keep = [&](int k) { return valid && k < kend; };
     auto mm = [&](const double2 (&xv)[KU], int kb) {
+#if PPF_MOM_ILP
+        // base phasor of the batch (k = kb + kk), re-seeded exactly every
+        // 64 harmonics (kb is a multiple of 4 KU)
+        if ((kb & 63) == 0) E = cexp2pi((double)(kb + kk) * phin);
+        else E = cmul(E, WB);
+#endif
 #pragma unroll
         for (int t = 0; t < KU; ++t) {
             const int k = kb + 4 * t + kk;
+#if PPF_MOM_ILP
+            const double2 Et = t == 0 ? E : cmul(E, Wt[t]);
+#else
             // phasor by recurrence, re-seeded exactly every 64 harmonics
             // (kb is a multiple of 16: only t = 0 can re-seed)
             if (t == 0 && (kb & 63) == 0) E = cexp2pi((double)k * phin);
             else E = cmul(E, W4);
+            const double2 Et = E;
+#endif
             const double2 xk = keep(k) ? xv[t] : cmk(0.0, 0.0);
-            const double2 y = cmul(xk, E);
+            const double2 y = cmul(xk, Et);
             const double u = ((double)k - hw) * ihw;
             const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4, u16 = u8 * u8;
             const double uj = ((ci & 1) ? u : 1.0) * ((ci & 2) ? u2 : 1.0) *
                               ((ci & 4) ? u4 : 1.0) * ((ci & 8) ? u8 : 1.0);
-            dre0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, uj, dre0, 0, 0, 0);
-            dim0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, uj, dim0, 0, 0, 0);
+#if PPF_MOM_ILP
+            // (32 moments: dre1 / dim1 already make four chains)
+            if (m16 && (t & 1)) {
+                dre0b = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, uj, dre0b, 0, 0, 0);
+                dim0b = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, uj, dim0b, 0, 0, 0);
+            } else
+#endif
+            {
+                dre0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, uj, dre0, 0, 0, 0);
+                dim0 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.y, uj, dim0, 0, 0, 0);
+            }
             if constexpr (!m16) {
                 const double ujh = uj * u16;
                 dre1 = __builtin_amdgcn_mfma_f64_16x16x4f64(y.x, ujh, dre1, 0, 0, 0);
@@ -1194,6 +1232,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_MOM_
         if (kb + 4 * KU < kend) mm(xb, kb + 4 * KU);    // (uniform)
         ld(xb, kb + 12 * KU);
     }
+#if PPF_MOM_ILP
+    if constexpr (m16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            dre0[r] += dre0b[r];
+            dim0[r] += dim0b[r];
+        }
+    }
+#endif
     // D[row][col]: col = lane & 15 = moment, row = (lane >> 4) + 4 r = channel
     double2 *M = a.mom + ((int64_t)s * 2 + q) * a.nchan * kMoments;
 #pragma unroll

@@ -1029,6 +1029,9 @@ __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 
 #ifndef PPF_X2_LATEPF
 #define PPF_X2_LATEPF 0
 #endif
+#ifndef PPF_X2_EW
+#define PPF_X2_EW 1
+#endif
 
 template <int DT, bool GS>
 __global__ __launch_bounds__(64 * kX2W) __attribute__((amdgpu_waves_per_eu(2)))
@@ -1037,7 +1040,10 @@ void k_xspec_w2(XspecArgs a) {
     constexpr int MD = PPF_X2_MD;
     using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane0 = threadIdx.x & 63;
+    // (wave-uniform: the row pointers built from it stay in SGPRs, so the
+    // loads take the scalar-base + 32-bit-offset form)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double2 *buf = lds + wave * kX2SL;
 
     int s, cb;
@@ -1114,20 +1120,57 @@ void k_xspec_w2(XspecArgs a) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) zr[q] = src[lane0 + 64 * q];
     };
+#if PPF_X2_EW
+    // Round 6: the next row's load is unconditional (a row past the block,
+    // or a masked one, is replaced by the block's last row: a valid address
+    // whose values are ignored), so the row registers carry no phi between
+    // loop paths (that cost two sets of 16 v_mov_b64 per row), and the wait
+    // for it is forced at the END of the round (rows_ready), before the
+    // round's X stores.  vmcnt counts loads and stores in issue order on
+    // gfx950: waited at the top of the next round, as the compiler placed
+    // it, the prefetch's wait included every X store of the write-out just
+    // issued -- vmcnt(0) on the store acknowledgements once per row.
+    auto fetch_c = [&](int m) { fetch(m < cend ? m : cend - 1); };
+    auto rows_ready = [&]() {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(zr[q].x), "v"(zr[q].y));
+    };
+    int n = cbase + wave;
+    fetch_c(n);
+    rows_ready();
+#else
     int n = cbase + wave;
     if (usable(n)) fetch(n);
+#endif
     XP_INIT();
     for (int r = 0; r < nround; ++r, n += kX2W) {
         const bool live = usable(n);
+#if PPF_X2_EW
+        if (n < cend && !live && lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
+        double2 x[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+            // (pinned here: sunk into the live branch below, the conversion
+            // kept the old row registers alive past the next load, which
+            // then took other registers and a copy per row)
+            asm volatile("" : "+v"(x[q].x), "+v"(x[q].y));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        fetch_c(n + kX2W);                       // next row in flight during this FFT
+#else
         if (n < cend && !live) {
             if (lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
             if (usable(n + kX2W)) fetch(n + kX2W);
         }
+#endif
         if (live) {
             const int64_t crow = (int64_t)s * a.nchan + n;
+#if !PPF_X2_EW
             double2 x[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
+#endif
             const int rr = n - cbase;
             // per-lane indices re-derived every row from an opaque lane
             // (hoisted out of the round loop they would hold VGPRs for good)
@@ -1150,15 +1193,16 @@ void k_xspec_w2(XspecArgs a) {
             double2 Mq[MD > 0 ? MD : 1];
             auto mpre = [&]() {
 #pragma unroll
-                for (int i = 0; i < MD; ++i) Mq[i] = Mrow[hl0 + hstep * i];
+                for (int i = 0; i < MD; ++i) Mq[i] = Mrow[(unsigned)(hl0 + hstep * i)];
             };
             if (PPF_X2_MEARLY) mpre();
-            if (!PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
+            if (!PPF_X2_EW && !PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
             XP(0);
             wf2::fft1024(x, buf, lane, sd);
             XP(1);
+            if (PPF_X2_EW) __builtin_amdgcn_sched_barrier(0);
             if (!PPF_X2_MEARLY) mpre();
-            if (PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);
+            if (!PPF_X2_EW && PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);
             double2 zm = cmk(0.0, 0.0);
             wf2::pairs(x, buf + wf2::kXSlots, lane, zm);
             XP(2);
@@ -1207,13 +1251,14 @@ void k_xspec_w2(XspecArgs a) {
                 double2 Ml;
                 if constexpr (MD > 0) {
                     Ml = Mq[i % MD];
-                    if (i + MD < 8) Mq[i % MD] = Mrow[hl + hstep * MD];
+                    if (i + MD < 8) Mq[i % MD] = Mrow[(unsigned)(hl + hstep * MD)];
                 } else {
-                    Ml = Mrow[hl];
+                    Ml = Mrow[(unsigned)hl];
                 }
                 // 2 x the unscaled X of the low harmonic (the write-out
                 // applies 1/(2 sigma~^2)); k = 0 zeroed (F0_fact = 0)
-                if (hl < kw) buf[x2slot(hl)] = hl == 0 ? cmk(0.0, 0.0) : cmulc(Dl, Ml);
+                // (k = 0 -- lane 0, slot 0 only -- is zeroed after the loop)
+                if (hl < kw) buf[x2slot(hl)] = cmulc(Dl, Ml);
                 if (GS && gon) {
                     // 2 x the row's guess term of harmonic hl, in the slot
                     // of N - hl (past X's cutoff: kw <= NL < N/2)
@@ -1223,11 +1268,12 @@ void k_xspec_w2(XspecArgs a) {
                     // the group's cutoff passes N/2: the high harmonic too
                     // (2 D_{N - hl} = (vx, -sg vy))
                     const int hh = N - hl;
-                    if (hh < kw) buf[x2slot(hh)] = cmulc(cmk(vx, -sg * vy), Mrow[hh]);
+                    if (hh < kw) buf[x2slot(hh)] = cmulc(cmk(vx, -sg * vy), Mrow[(unsigned)hh]);
                 }
             }
             XP(3);
             if (lane == 0) {
+                buf[x2slot(0)] = cmk(0.0, 0.0);       // k = 0 (F0_fact = 0)
                 // D_{N/2} (pairs: zm = Z_{N/2}), doubled like the rest
                 const double2 Dm = cmk(2.0 * zm.x, -2.0 * zm.y);
                 const double p = cabs2(Dm);
@@ -1259,6 +1305,9 @@ void k_xspec_w2(XspecArgs a) {
                 chan[3] = mpow * inv_e2;                                // S_n at tau = 0
             }
         }
+#if PPF_X2_EW
+        rows_ready();
+#endif
         XP(4);
         __syncthreads();
         XP(5);

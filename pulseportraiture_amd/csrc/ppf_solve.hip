@@ -1075,6 +1075,13 @@ constexpr double kX24 = 2.3;
 // 16 moments (mom16): x^14 / 14! < 1.6e-13 for |x| <= 0.73, with x = 2 pi h_n
 // Delta and h_n the centre of the channel band's harmonics (k_moments)
 constexpr double kX16 = 0.73;
+// fewer of the 16 (k_tr_mom, PPF_TRMOM_ADAPT): x^10 / 10! and x^6 / 6! <
+// 1.6e-13 for |x| <= 0.2368 (12 moments) and 0.0220 (8)
+constexpr double kX12 = 0.2368;
+constexpr double kX8 = 0.0220;
+#ifndef PPF_TRMOM_ADAPT
+#define PPF_TRMOM_ADAPT 1
+#endif
 constexpr int kMomChans = 64;                    // channels per k_moments workgroup
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -1275,10 +1282,10 @@ __device__ __forceinline__ void taylor_acc(const double2 *mu, double x, double r
     }
 }
 
-// moments [M, M1) from registers (mu[m - M0]); the window r0..r2 and the
-// partial sums carry over between segments
-template <int M, int M1, int M0>
-__device__ __forceinline__ void taylor_seg(const double2 (&mu)[M1 - M0], double x, double &r0,
+// moments [M, M1) from registers (mu[m - M0], SZ >= M1 - M0); the window
+// r0..r2 and the partial sums carry over between segments
+template <int M, int M1, int M0, int SZ>
+__device__ __forceinline__ void taylor_seg(const double2 (&mu)[SZ], double x, double &r0,
                                            double &r1, double &r2, double2 &G0, double2 &G1,
                                            double2 &G2) {
     if constexpr (M < M1) {
@@ -1289,7 +1296,7 @@ __device__ __forceinline__ void taylor_seg(const double2 (&mu)[M1 - M0], double 
         r2 = r1;
         r1 = r0;
         r0 = r0 * x * (1.0 / (double)(M + 1));
-        taylor_seg<M + 1, M1, M0>(mu, x, r0, r1, r2, G0, G1, G2);
+        taylor_seg<M + 1, M1, M0, SZ>(mu, x, r0, r1, r2, G0, G1, G2);
     }
 }
 
@@ -1428,18 +1435,38 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
             c_ok = mk[n];
         };
         const bool q4 = !m16 && xsel > kX24;   // uniform: all 32 moments needed
+#if PPF_TRMOM_ADAPT
+        // mom16 (round 6): only the moments the step needs.  The second
+        // derivative's series truncated after M moments errs by at most
+        // x^(M-2) / (M-2)! of sum |Y| (|u| <= 1), so with x = max_n 2 pi h_n
+        // |Delta_n| (xsel): M = 8 for x <= kX8 -- every fit's first
+        // evaluation, at the centre itself (x = 0) --, 12 for x <= kX12,
+        // else 16: the same 1.6e-13 bound as kX16, 128 / 192 instead of 256
+        // B of moments per channel read per evaluation
+        const int mq = !m16 ? 2 : (xsel <= kX8 ? 0 : (xsel <= kX12 ? 1 : 2));
+        auto ldq4 = [&](int i, double2 (&b)[KQ]) {
+            const int n = min(tid + TB * i, a.nchan - 1);
+            const double2 *p = Mq + (int64_t)n * kMoments + KQ;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) b[m] = p[m];
+        };
+#else
+        constexpr int mq = 2;
+        auto ldq4 = [&](int, double2 (&)[KQ]) {};
+#endif
         ldq(0, 0, qa);
         ldc(0);
         for (int i = 0; i < nit; ++i) {
             const int n = tid + TB * i;
-            ldq(i, 1, qb);
+            if (mq == 2) ldq(i, 1, qb);
+            else if (mq == 1) ldq4(i, qb);
             const bool valid = n < a.nchan && (!use_mask || c_ok != 0);
             const double d1 = c_d1, d2 = c_d2, Sn = c_S, hn_ = c_h;
             const double del = e0 + e1 * d1 + e2 * d2 + c_rq;
             const double x = kTwoPi * hn_ * del;
             double2 G0 = cmk(0.0, 0.0), G1 = G0, G2 = G0;
             double r0 = 1.0, r1 = 0.0, r2 = 0.0;
-            taylor_seg<0, KQ, 0>(qa, x, r0, r1, r2, G0, G1, G2);
+            taylor_seg<0, KQ, 0, KQ>(qa, x, r0, r1, r2, G0, G1, G2);
             if (m16) {
                 // 16 moments: the next channel's first quarter is in flight
                 // while the second is summed
@@ -1447,17 +1474,18 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
                     ldq(i + 1, 0, qa);
                     ldc(i + 1);
                 }
-                taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+                if (mq == 2) taylor_seg<KQ, 2 * KQ, KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+                else if (mq == 1) taylor_seg<KQ, KQ + 4, KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
             } else {
                 ldq(i, 2, qa);
-                taylor_seg<KQ, 2 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+                taylor_seg<KQ, 2 * KQ, KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
                 if (q4) ldq(i, 3, qb);
-                taylor_seg<2 * KQ, 3 * KQ, 2 * KQ>(qa, x, r0, r1, r2, G0, G1, G2);
+                taylor_seg<2 * KQ, 3 * KQ, 2 * KQ, KQ>(qa, x, r0, r1, r2, G0, G1, G2);
                 if (i + 1 < nit) {
                     ldq(i + 1, 0, qa);
                     ldc(i + 1);
                 }
-                if (q4) taylor_seg<3 * KQ, kMoments, 3 * KQ>(qb, x, r0, r1, r2, G0, G1, G2);
+                if (q4) taylor_seg<3 * KQ, kMoments, 3 * KQ, KQ>(qb, x, r0, r1, r2, G0, G1, G2);
             }
             if (!valid) continue;
             const double2 eix = cexp2pi(hn_ * del);

@@ -1105,8 +1105,12 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #ifndef PPF_MOM_KU
 #define PPF_MOM_KU 4
 #endif
+// PPF_MOM_ILP (round 6, measured and not kept): the batch's phasors from
+// its base phasor and two accumulator pairs -- k_moments 5.83 vs 5.72-5.76
+// ms per 10k at C2 (profiles/r06/ab_r6a_status.txt): the kernel is not
+// bound by its dependency chains, and the 164 VGPRs cost a wave per SIMD
 #ifndef PPF_MOM_ILP
-#define PPF_MOM_ILP 1
+#define PPF_MOM_ILP 0
 #endif
 // M16: the call's moment count (a.mom16: 16 on the moments-from-X path, 32
 // otherwise), a template argument so the MFMA loop carries no branch

@@ -1243,10 +1243,13 @@ def main():
         out["alpha_pull_rms"] = round(float(np.sqrt(np.mean(
             ((pr[:, 4] - synth.GMODEL_ALPHA) / pe[:, 4]) ** 2))), 3)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        # scattering fits take ~10x longer on the CPU: a 24x smaller sample
+        # scattering fits take ~10x longer on the CPU: a 12x smaller sample
+        # (C5's 16384-channel fits ~30 s each: 48x smaller); the default
+        # --cpu-sample 48 gives C3 4 and C5 1 one-core sub-ints, 192 gives
+        # 16 and 4 (the evidence runs, tools/evid.sh)
         nsamp = min(args.cpu_sample if not scat_fit else
                     (max(4, args.cpu_sample // 12) if nchan * nbin <= 1 << 20
-                     else 1), count)
+                     else max(1, args.cpu_sample // 48)), count)
         out["cpu_baseline"], oref = cpu_baseline(
             batch, nsamp, nchan, nbin, args.cpu_workers, mode=args.fit,
             flags=FIT["flags"], per_worker=4 if not scat_fit else 1)

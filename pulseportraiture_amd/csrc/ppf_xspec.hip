@@ -1032,8 +1032,11 @@ __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 
 #ifndef PPF_X2_EW
 #define PPF_X2_EW 1
 #endif
-#ifndef PPF_X2D_MD
-#define PPF_X2D_MD 4
+// PPF_X2_DIAG (timing-only builds, results wrong): 1 no X stores, 2 every
+// model load from the first model row (L2 hits), 4 no FFT (the row values go
+// straight to the post-pass)
+#ifndef PPF_X2_DIAG
+#define PPF_X2_DIAG 0
 #endif
 
 template <int DT, bool GS>
@@ -1184,7 +1187,8 @@ void k_xspec_w2(XspecArgs a) {
             const bool lo = lane <= 32;
             const int kA = wf2::pair_k0(lane);
             const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
-            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            const double2 *Mrow0 = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+            const double2 *Mrow = Mrow0;
             // the first MD slots' model values.  PPF_X2_MEARLY: issued before
             // the next row's prefetch (so their wait does not include it),
             // held through the FFT; else after the FFT.  PPF_X2_LATEPF: the
@@ -1198,10 +1202,16 @@ void k_xspec_w2(XspecArgs a) {
 #pragma unroll
                 for (int i = 0; i < MD; ++i) Mq[i] = Mrow[(unsigned)(hl0 + hstep * i)];
             };
+#if PPF_X2_DIAG & 2
+            // (timing-only build: the model row read once per row, one value)
+            Mrow = a.Mft;
+#endif
             if (PPF_X2_MEARLY) mpre();
             if (!PPF_X2_EW && !PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
             XP(0);
+#if !(PPF_X2_DIAG & 4)
             wf2::fft1024(x, buf, lane, sd);
+#endif
             XP(1);
             if (PPF_X2_EW) __builtin_amdgcn_sched_barrier(0);
             if (!PPF_X2_MEARLY) mpre();
@@ -1323,8 +1333,12 @@ void k_xspec_w2(XspecArgs a) {
                 const bool ok = !mask || mask[nc];
                 const double2 *b = lds + c * kX2SL;
                 const double ie2 = ok ? reinterpret_cast<const double *>(b + kX2IE)[0] : 0.0;
-                for (int k = threadIdx.x / kX2W; k < kw; k += 64)
+                for (int k = threadIdx.x / kX2W; k < kw; k += 64) {
+#if PPF_X2_DIAG & 1
+                    if (ie2 == 12345.0)            // (timing-only build: no X stores)
+#endif
                     Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[x2slot(k)], ie2) : cmk(0.0, 0.0);
+                }
             }
         }
         if (GS && gon) {
@@ -1358,304 +1372,6 @@ void k_xspec_w2(XspecArgs a) {
             if (threadIdx.x == 0) {
                 double acc = 0.0;
                 for (int w2 = 0; w2 < kX2W; ++w2) acc += reinterpret_cast<const double *>(lds + w2 * kX2SL)[0];
-                double *o = a.gw + ((int64_t)s * a.nblk + cb) * 3;
-                o[0] = wsum;
-                o[1] = cnt;
-                o[2] = acc;
-            }
-        }
-    }
-}
-
-// ===========================================================================
-// k_xspec_w2d: k_xspec_w2 with no per-round staging (round 6, default; the
-// environment PPF_XSPEC2D=0 selects k_xspec_w2).  k_xspec_w2 staged each
-// round's four X rows in LDS and wrote them out after a workgroup barrier
-// (two barriers per round of four rows: the waves ran in lock-step).  Here
-// every wave is independent of the others from the prologue to the guess
-// reduction at the end:
-//   - a lane keeps the X values of its eight slots (the low harmonic, and
-//     the high one when the group's cutoff passes N/2) in the registers the
-//     transform frees, scales them once the row's noise is known and stores
-//     them straight to X[k][n] (the same product in the same order as the
-//     staged write-out: X bit-identical);
-//   - the GetTOAs guess terms accumulate in eight complex registers per lane
-//     (the lane's slots hold the same harmonics for every row of the wave),
-//     summed over the workgroup's waves in wave order after the last row.
-// ===========================================================================
-template <int DT, bool GS>
-__global__ __launch_bounds__(64 * kX2W) __attribute__((amdgpu_waves_per_eu(2)))
-void k_xspec_w2d(XspecArgs a) {
-    constexpr int N = 1024, NH = N + 1;
-    constexpr int MD = PPF_X2D_MD;
-    using RowT = typename std::conditional<DT == 0, vf2, vd2>::type;
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const int lane0 = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    double2 *buf = lds + wave * kX2SL;
-
-    int s, cb;
-    block_map(a.xcd_swizzle, a.nblk, s, cb, a.nsub);
-    if (a.needx && !a.needx[s]) return;               // uniform: moment-mode sub-int (or no slot)
-    const int cbase = cb * a.cb, cend = min(a.nchan, cbase + a.cb);
-    const int nround = (a.cb + kX2W - 1) / kX2W;
-    const int mi = a.model_index ? a.model_index[s] : 0;
-    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
-    const double sqrtN = sqrt((double)N);
-    const RowT *rows = reinterpret_cast<const RowT *>(a.data);
-    // per-lane constants in a workgroup LDS table read once per row (held
-    // in registers for the whole row loop they took 14 VGPRs): the FFT seeds
-    // and the post-pass twiddle e^{-i pi k / N} of the lane's first pair
-    double2 *ltab = lds + kX2W * kX2SL;                         // [64][3]
-    if (threadIdx.x < 64) {
-        const wf2::Seeds sd0 = wf2::make_seeds(lane0);
-        double sn, cs;
-        sincospi(-(double)wf2::pair_k0(lane0) / (double)N, &sn, &cs);
-        ltab[lane0 * 3 + 0] = sd0.w1;
-        ltab[lane0 * 3 + 1] = sd0.v1;
-        ltab[lane0 * 3 + 2] = cmk(cs, sn);
-    }
-    double2 wstep;
-    {
-        double sn, cs;
-        sincospi(-64.0 / (double)N, &sn, &cs);     // (uniform: kept in SGPRs)
-        wstep = cmk(readlane_d(cs, 0), readlane_d(sn, 0));
-    }
-    double2 *Xs = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan;
-    const unsigned xrow = (unsigned)a.nchan * (unsigned)sizeof(double2);   // bytes per harmonic of X
-    int kw = NH;
-    if (a.KC) {
-        const int nn = (cbase & ~63) + lane0;
-        kw = (int)wave_max(nn < a.nchan ? (double)a.KC[(int64_t)mi * a.nchan + nn] : 1.0);
-    }
-    const int mlane = (cbase + lane0 < cend && (!mask || mask[cbase + lane0])) ? 1 : 0;
-    auto usable = [&](int n) {
-        return n < cend && __builtin_amdgcn_readlane(mlane, n - cbase) != 0;
-    };
-    constexpr int NL = 64 * guess_npl(10);
-    bool gon = false;
-    double g_Dg = 0.0, g_nrm2 = 0.0, g_w2e2 = 0.0;
-    if constexpr (GS) {
-        gon = a.gflag[s] != 0;                         // uniform
-        if (gon) {
-            const double *fr = a.freqs + (int64_t)s * a.nchan;
-            double v0 = 0.0, v1 = 0.0;
-            for (int nn = lane0; nn < a.nchan; nn += 64)
-                if (!mask || mask[nn]) { v0 += fr[nn]; v1 += 1.0; }
-            v0 = wave_sum(v0);
-            v1 = wave_sum(v1);
-            const double mu = v0 / v1;
-            double nu_ref_m2 = 1.0 / (mu * mu);
-            if (a.guess_ref) {
-                const double nf = a.nu_fits[(int64_t)s * 3];
-                if (nf == nf) nu_ref_m2 = 1.0 / (nf * nf);
-            }
-            g_Dg = readlane_d(kDconst * a.guess_DM[s] / a.P[s], 0);
-            g_nrm2 = readlane_d(nu_ref_m2, 0);
-        }
-    }
-    // the block's per-channel scalars (|M|^2 sum, errs, guess weight and
-    // dispersion phase) in LDS, read per row as a broadcast (in lane
-    // registers, as k_xspec_w2 keeps them, they held 8 VGPRs for good)
-    double *chs = reinterpret_cast<double *>(ltab + 64 * 3);      // [cb][4]
-    if (threadIdx.x < 64) {
-        const int nl = cbase + lane0;
-        const bool lin = nl < cend && lane0 < a.cb;
-        double ch_wn = 0.0, ch_dg = 0.0;
-        if (GS && gon && lin) {
-            ch_wn = a.guess_weights[(int64_t)s * a.nchan + nl];
-            const double f = a.freqs[(int64_t)s * a.nchan + nl];
-            ch_dg = g_Dg * (1.0 / (f * f) - g_nrm2);
-        }
-        if (lane0 < a.cb) {
-            chs[lane0 * 4 + 0] = lin ? a.Mpow[(int64_t)mi * a.nchan + nl] : 0.0;
-            chs[lane0 * 4 + 1] = (a.errs && lin) ? a.errs[(int64_t)s * a.nchan + nl] : 0.0;
-            chs[lane0 * 4 + 2] = ch_wn;
-            chs[lane0 * 4 + 3] = ch_dg;
-        }
-    }
-    __syncthreads();
-    // slot i of a lane: harmonics hl = hl0 + hstep i (the lower one, < N/2)
-    // and N - hl (lanes <= 32: k = kA + 64 i, the others N - k)
-    const bool lo0 = lane0 <= 32;
-    const int hl00 = lo0 ? wf2::pair_k0(lane0) : N - wf2::pair_k0(lane0);
-    const int hst0 = lo0 ? 64 : -64;
-    double2 gsum[GS ? 8 : 1];
-#pragma unroll
-    for (int i = 0; i < (GS ? 8 : 1); ++i) gsum[i] = cmk(0.0, 0.0);
-    RowT zr[16];
-    auto fetch = [&](int n) {
-        const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) zr[q] = src[lane0 + 64 * q];
-    };
-    // the next row's load unconditional and waited for at the end of the
-    // row, before its X stores (see k_xspec_w2, PPF_X2_EW)
-    auto fetch_c = [&](int m) { fetch(m < cend ? m : cend - 1); };
-    auto rows_ready = [&]() {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(zr[q].x), "v"(zr[q].y));
-    };
-    int n = cbase + wave;
-    fetch_c(n);
-    rows_ready();
-    for (int r = 0; r < nround; ++r, n += kX2W) {
-        const bool live = usable(n);
-        double2 x[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            x[q] = cmk((double)zr[q].x, (double)zr[q].y);
-            asm volatile("" : "+v"(x[q].x), "+v"(x[q].y));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        fetch_c(n + kX2W);                       // next row in flight during this FFT
-        // X column of this channel: byte offset k * xrow from Xn
-        char *Xn = reinterpret_cast<char *>(Xs + n);
-        if (n < cend && !live) {
-            // a zapped channel: chan scalars and X below the cutoff are zero
-            if (lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
-            for (int k = lane0; k < kw; k += 64)
-                *reinterpret_cast<double2 *>(Xn + (unsigned)k * xrow) = cmk(0.0, 0.0);
-        }
-        if (live) {
-            const int64_t crow = (int64_t)s * a.nchan + n;
-            const int rr = n - cbase;
-            int lane = lane0;
-            asm volatile("" : "+v"(lane));
-            const bool lo = lane <= 32;
-            const int kA = wf2::pair_k0(lane);
-            const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
-            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-            double2 Mq[MD > 0 ? MD : 1];
-            auto mpre = [&]() {
-#pragma unroll
-                for (int i = 0; i < MD; ++i) Mq[i] = Mrow[(unsigned)(hl0 + hstep * i)];
-            };
-            wf2::Seeds sd;
-            sd.w1 = ltab[lane * 3 + 0];
-            sd.v1 = ltab[lane * 3 + 1];
-            wf2::fft1024(x, buf, lane, sd);
-            __builtin_amdgcn_sched_barrier(0);
-            mpre();
-            double2 zm = cmk(0.0, 0.0);
-            wf2::pairs(x, buf + wf2::kXSlots, lane, zm);
-            double2 El = cmk(0.0, 0.0), Est = El;
-            if (GS && gon) {
-                const double dg = chs[rr * 4 + 3];
-                const double2 E1 = cexp2pi((double)hl0 * dg);
-                El = cscale(E1, chs[rr * 4 + 2]);
-                Est = cmk(readlane_d(E1.x, 1), readlane_d(E1.y, 1));
-#pragma unroll
-                for (int q = 0; q < 6; ++q) Est = cmul(Est, Est);
-                if (!lo) Est = cconj(Est);
-            }
-            // the post-pass of k_xspec_w2 (doubled values); slot i's X of
-            // the low harmonic replaces x[i], of the high one x[i + 8]
-            const double sg = lo ? 1.0 : -1.0;
-            const int hcut = N - a.kc;
-            const bool hiX = !(GS && gon) && kw > N / 2;   // uniform
-            double pn = 0.0, pd = 0.0;
-            // (opaque: the eight slot twiddles hoisted out of the row loop
-            // held 32 VGPRs, which the guess sums need)
-            double2 w = ltab[lane * 3 + 2];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const double2 zk = x[i], zn = x[i + 8];
-                const double ex = zk.x + zn.x, ey = zk.y - zn.y;
-                const double ox = zk.x - zn.x, oy = zk.y + zn.y;
-                const double wox = fma(w.x, ox, -w.y * oy), woy = fma(w.x, oy, w.y * ox);
-                w = cmul(w, wstep);
-                const double ux = fma(sg, woy, ex), uy = fma(-sg, wox, ey);
-                const double vx = fma(-sg, woy, ex), vy = fma(sg, wox, ey);
-                const double2 Dl = cmk(ux, sg * uy);
-                const double ph = fma(vx, vx, vy * vy), pl = fma(ux, ux, uy * uy);
-                const int hl = hl0 + hstep * i;
-                if (hl <= hcut) pn += ph;
-                if (i == 0) pd += lane == 0 ? ph : pl + ph;
-                else pd += pl + ph;
-                double2 Ml;
-                if constexpr (MD > 0) {
-                    Ml = Mq[i % MD];
-                    if (i + MD < 8) Mq[i % MD] = Mrow[(unsigned)(hl + hstep * MD)];
-                } else {
-                    Ml = Mrow[(unsigned)hl];
-                }
-                // 2 x the unscaled X of hl, parked in the wave's own buffer
-                // (free after the transform) until the row's noise is known
-                if (hl < kw) buf[x2slot(hl)] = cmulc(Dl, Ml);
-                if (GS && gon) {
-                    if (hl >= 1 && hl < NL) gsum[i] = cadd(gsum[i], cmul(Dl, El));
-                    El = cmul(El, Est);
-                } else if (hiX) {
-                    const int hh = N - hl;
-                    if (hh < kw) buf[x2slot(hh)] = cmulc(cmk(vx, -sg * vy), Mrow[(unsigned)hh]);
-                }
-            }
-            if (lane == 0) {
-                const double2 Dm = cmk(2.0 * zm.x, -2.0 * zm.y);
-                const double p = cabs2(Dm);
-                if (N / 2 >= a.kc) pn += p;
-                pd += p;
-                if (N / 2 < kw) buf[x2slot(N / 2)] = cmulc(Dm, Mrow[N / 2]);
-            }
-            pn *= 0.25;
-            pd *= 0.25;
-            pn = wave_sum(pn);
-            pd = wave_sum(pd);
-            double errs_FT;
-            if (a.errs) errs_FT = chs[rr * 4 + 1] * sqrtN;
-            else errs_FT = sqrt(pn / (double)(NH - a.kc) / (double)(2 * N)) * sqrtN;
-            const double inv_e2 = 1.0 / (errs_FT * errs_FT);
-            if (GS && gon) {
-                const double wn = chs[rr * 4 + 2];
-                g_w2e2 += wn * wn * errs_FT * errs_FT;
-            }
-            const double mpow = chs[rr * 4 + 0];
-            if (lane == 0) {
-                double *chan = a.chan + crow * 4;
-                chan[0] = errs_FT;
-                chan[1] = inv_e2;
-                chan[2] = pd * inv_e2;                                  // Sd_n
-                chan[3] = mpow * inv_e2;                                // S_n at tau = 0
-            }
-            // X = D conj(M) / sigma~^2 (the parked products are doubled),
-            // stored by the wave straight to its channel's column: harmonic
-            // k = lane + 64 j of the column, k = 0 zeroed (F0_fact = 0)
-            const double ie2 = 0.5 * inv_e2;
-            // the next row has arrived long since: wait for it here, before
-            // this row's stores, not after them (vmcnt counts both in order)
-            rows_ready();
-            wfft::wave_sync();
-            for (int k = lane; k < kw; k += 64)
-                *reinterpret_cast<double2 *>(Xn + (unsigned)k * xrow) =
-                    k == 0 ? cmk(0.0, 0.0) : cscale(buf[x2slot(k)], ie2);
-            wfft::wave_sync();                  // (the next row's transform reuses buf)
-        }
-        rows_ready();
-    }
-    if constexpr (GS) {
-        if (gon) {
-            // the waves' guess sums by harmonic (every harmonic < N/2 is in
-            // exactly one slot of one lane), then added in wave order
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int hl = hl00 + hst0 * i;
-                if (hl < NL) buf[hl] = hl == 0 ? cmk(0.0, 0.0) : gsum[i];
-            }
-            if (lane0 == 0) reinterpret_cast<double *>(buf + NL)[0] = g_w2e2;
-            __syncthreads();
-            double2 *gp = a.gpart + ((int64_t)s * a.nblk + cb) * NL;
-            for (int t = threadIdx.x; t < NL; t += 64 * kX2W) {
-                double2 acc = lds[t];
-#pragma unroll
-                for (int w2 = 1; w2 < kX2W; ++w2) acc = cadd(acc, lds[w2 * kX2SL + t]);
-                gp[t] = cscale(acc, 0.5);              // (the terms are doubled: exact)
-            }
-            const double gwl = mlane ? a.guess_weights[(int64_t)s * a.nchan + cbase + lane0] : 0.0;
-            const double wsum = wave_sum(gwl), cnt = wave_sum(mlane ? 1.0 : 0.0);
-            if (threadIdx.x == 0) {
-                double acc = 0.0;
-                for (int w2 = 0; w2 < kX2W; ++w2) acc += reinterpret_cast<const double *>(lds + w2 * kX2SL + NL)[0];
                 double *o = a.gw + ((int64_t)s * a.nblk + cb) * 3;
                 o[0] = wsum;
                 o[1] = cnt;
@@ -2139,18 +1855,6 @@ static bool use_xspec2() {
     return on;
 }
 
-// k_xspec_w2d (no per-round staging) unless PPF_XSPEC2D=0 (environment)
-#ifndef PPF_XSPEC2D
-#define PPF_XSPEC2D 1
-#endif
-static bool use_xspec2d() {
-    static const bool on = [] {
-        const char *e = getenv("PPF_XSPEC2D");
-        return e ? atoi(e) != 0 : (PPF_XSPEC2D != 0);
-    }();
-    return on;
-}
-
 // ===========================================================================
 // launchers
 // ===========================================================================
@@ -2160,12 +1864,6 @@ static void launch_w(const XspecArgs &a, hipStream_t st) {
         if (use_xspec2()) {
             const size_t lds = (size_t)kX2W * kX2SL * sizeof(double2);
             dim3 g((unsigned)((int64_t)a.nsub * a.nblk)), b(64 * kX2W);
-            if (use_xspec2d()) {
-                const size_t ldsd = lds + 64 * 3 * sizeof(double2) + (size_t)a.cb * 4 * sizeof(double);
-                if (a.gflag) hipLaunchKernelGGL((k_xspec_w2d<DT, true>), g, b, ldsd, st, a);
-                else hipLaunchKernelGGL((k_xspec_w2d<DT, false>), g, b, ldsd, st, a);
-                return;
-            }
             if (a.gflag)
                 hipLaunchKernelGGL((k_xspec_w2<DT, true>), g, b, lds + (size_t)guess_slots(10) * sizeof(double2),
                                    st, a);

@@ -1013,7 +1013,13 @@ __global__ __launch_bounds__(256) void k_model_sum(const double2 *Mft, int nchan
 // (GS, pptoas.py:461-464) as k_xspec_w, its terms in the slots of N - k.
 // PPF_XSPEC2=0 (environment) selects k_xspec_w instead.
 // ===========================================================================
-constexpr int kX2W = 4;                                   // waves per workgroup
+// waves per workgroup (= rows per round, channels per X line written:
+// 4 -> 64-B segments of the 128-B lines, two workgroups per CU; 8 -> whole
+// lines, one workgroup per CU)
+#ifndef PPF_X2W
+#define PPF_X2W 4
+#endif
+constexpr int kX2W = PPF_X2W;
 constexpr int kX2SL = wf2::kXSlots + wf2::kSpSlots;       // 1072 slots per wave
 constexpr int kX2IE = 1041;                               // the row's 1/errs_FT^2 (.x)
 __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 1024 -> <= 1040
@@ -1037,6 +1043,9 @@ __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 
 // straight to the post-pass)
 #ifndef PPF_X2_DIAG
 #define PPF_X2_DIAG 0
+#endif
+#ifndef PPF_X2_WR
+#define PPF_X2_WR 0
 #endif
 
 template <int DT, bool GS>
@@ -1152,7 +1161,7 @@ void k_xspec_w2(XspecArgs a) {
     for (int r = 0; r < nround; ++r, n += kX2W) {
         const bool live = usable(n);
 #if PPF_X2_EW
-        if (n < cend && !live && lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
+        if (!PPF_X2_WR && n < cend && !live && lane0 < 4) a.chan[((int64_t)s * a.nchan + n) * 4 + lane0] = 0.0;
         double2 x[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -1162,6 +1171,32 @@ void k_xspec_w2(XspecArgs a) {
             // then took other registers and a copy per row)
             asm volatile("" : "+v"(x[q].x), "+v"(x[q].y));
         }
+        // slot i: harmonics k = kA + 64 i and N - k; hl = the lower one
+        // (lanes <= 32: k, the others: N - k), D of it in Dl.  Per-lane
+        // indices re-derived every row from an opaque lane (hoisted out of
+        // the round loop they would hold VGPRs for good)
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const bool lo = lane <= 32;
+        const int kA = wf2::pair_k0(lane);
+        const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
+        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + (n < cend ? n : cend - 1)) * NH;
+#if PPF_X2_DIAG & 2
+        Mrow = a.Mft;       // (timing-only build: every model load from the first row, L2 hits)
+#endif
+        // the first MD slots' model values: PPF_X2_MEARLY issues them here,
+        // before the next row's prefetch, so that the post-pass's wait for
+        // them (vmcnt is in order) does not include the prefetch; else
+        // after the FFT.  The loads are unconditional (hl < N/2 is always a
+        // valid index): under a lane-divergent branch the compiler cannot
+        // count the loads in flight and waits for all of them (vmcnt(0),
+        // the next row's prefetch included) at every slot.
+        double2 Mq[MD > 0 ? MD : 1];
+        auto mpre = [&]() {
+#pragma unroll
+            for (int i = 0; i < MD; ++i) Mq[i] = Mrow[(unsigned)(hl0 + hstep * i)];
+        };
+        if (PPF_X2_MEARLY && live) mpre();
         __builtin_amdgcn_sched_barrier(0);
         fetch_c(n + kX2W);                       // next row in flight during this FFT
 #else
@@ -1178,36 +1213,21 @@ void k_xspec_w2(XspecArgs a) {
             for (int q = 0; q < 16; ++q) x[q] = cmk((double)zr[q].x, (double)zr[q].y);
 #endif
             const int rr = n - cbase;
-            // per-lane indices re-derived every row from an opaque lane
-            // (hoisted out of the round loop they would hold VGPRs for good)
+#if !PPF_X2_EW
             int lane = lane0;
             asm volatile("" : "+v"(lane));
-            // slot i: harmonics k = kA + 64 i and N - k; hl = the lower one
-            // (lanes <= 32: k, the others: N - k), D of it in Dl
             const bool lo = lane <= 32;
             const int kA = wf2::pair_k0(lane);
             const int hl0 = lo ? kA : N - kA, hstep = lo ? 64 : -64;
-            const double2 *Mrow0 = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
-            const double2 *Mrow = Mrow0;
-            // the first MD slots' model values.  PPF_X2_MEARLY: issued before
-            // the next row's prefetch (so their wait does not include it),
-            // held through the FFT; else after the FFT.  PPF_X2_LATEPF: the
-            // prefetch is issued after the FFT and the model loads.
-            // The loads are unconditional (hl < N/2 is always a valid
-            // index): under a lane-divergent branch the compiler cannot
-            // count the loads in flight and waits for all of them (vmcnt(0),
-            // the next row's prefetch included) at every slot.
+            const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
             double2 Mq[MD > 0 ? MD : 1];
             auto mpre = [&]() {
 #pragma unroll
                 for (int i = 0; i < MD; ++i) Mq[i] = Mrow[(unsigned)(hl0 + hstep * i)];
             };
-#if PPF_X2_DIAG & 2
-            // (timing-only build: the model row read once per row, one value)
-            Mrow = a.Mft;
-#endif
             if (PPF_X2_MEARLY) mpre();
-            if (!PPF_X2_EW && !PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
+            if (!PPF_X2_LATEPF && usable(n + kX2W)) fetch(n + kX2W);   // next row in flight during this FFT
+#endif
             XP(0);
 #if !(PPF_X2_DIAG & 4)
             wf2::fft1024(x, buf, lane, sd);
@@ -1311,11 +1331,18 @@ void k_xspec_w2(XspecArgs a) {
             if (lane == 0) {
                 // for the write-out: the staged X are doubled
                 reinterpret_cast<double *>(buf + kX2IE)[0] = 0.5 * inv_e2;
+#if PPF_X2_WR
+                // the channel scalars go out with the round's write-out
+                buf[kX2IE + 1] = cmk(errs_FT, inv_e2);
+                buf[kX2IE + 2] = cmk(pd * inv_e2, mpow * inv_e2);    // Sd_n, S_n at tau = 0
+                (void)crow;
+#else
                 double *chan = a.chan + crow * 4;
                 chan[0] = errs_FT;
                 chan[1] = inv_e2;
                 chan[2] = pd * inv_e2;                                  // Sd_n
                 chan[3] = mpow * inv_e2;                                // S_n at tau = 0
+#endif
             }
         }
 #if PPF_X2_EW
@@ -1324,6 +1351,34 @@ void k_xspec_w2(XspecArgs a) {
         XP(4);
         __syncthreads();
         XP(5);
+#if PPF_X2_WR
+        // write-out by ONE wave per round (wave r mod 4, rotating): vmcnt
+        // counts stores and loads in issue order, so a wave that stores
+        // waits for the acknowledgements at its next load wait; here three
+        // of four waves issue no global store in a round.  Lane l: channel
+        // l % 4 of the round, harmonics l / 4 + 16 j; lanes < 16 also the
+        // round's channel scalars (zero for a zapped channel)
+        if (wave == r % kX2W) {
+            const int c = lane0 % kX2W, n0 = cbase + r * kX2W;
+            const int nc = n0 + c;
+            if (nc < cend) {
+                const bool ok = !mask || mask[nc];
+                const double2 *b = lds + c * kX2SL;
+                const double ie2 = ok ? reinterpret_cast<const double *>(b + kX2IE)[0] : 0.0;
+                for (int k = lane0 / kX2W; k < kw; k += 64 / kX2W)
+                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[x2slot(k)], ie2) : cmk(0.0, 0.0);
+            }
+            if (lane0 < 4 * kX2W) {
+                const int cc = lane0 >> 2, comp = lane0 & 3, ncc = n0 + cc;
+                if (ncc < cend) {
+                    const bool okc = !mask || mask[ncc];
+                    const double v = reinterpret_cast<const double *>(lds + cc * kX2SL + kX2IE + 1)[comp];
+                    a.chan[((int64_t)s * a.nchan + ncc) * 4 + comp] = okc ? v : 0.0;
+                }
+            }
+        }
+        if (false)
+#endif
         // write-out: thread t -> channel c = t % 4 of the round, harmonics
         // k = t / 4 + 64 j
         {

@@ -7,7 +7,7 @@
 round=${1:-r05}; tag=${2:-a}
 cd "$(dirname "$0")/.."
 mkdir -p profiles/$round
-for c in c2 c3 c5 c4 nb1000 nb1536; do
+for c in c2 c3 c5 c4 nb1000 nb1536 nb1023; do
   d=gpurun_out/prof_${tag}_$c
   [ -d $d ] || continue
   ks=$(ls $d/ks/*kernel_stats.csv 2>/dev/null | head -1)

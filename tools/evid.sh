@@ -1,5 +1,5 @@
 #!/bin/bash
-# Evidence run: the GPU parity suite, then every bench line with its
+# Evidence run: the GPU parity suite and smoke(), then every bench line with its
 # CPU baseline and parity sample (C2 headline, single-call latency, C3 and C5
 # with >= 5 timed steps, C4 ppalign, GetTOAs from 16-bit PSRFITS and from
 # float32 archives, phase+DM at the mixed-radix nbin 1000 and 1536 and the
@@ -22,11 +22,18 @@ run() {
   echo "$name rc=$rc $(python tools/show.py gpurun_out/bench_${name}_$tag.log | head -1)" >> $st
   [ $rc -eq 0 ] || exit $rc
 }
+if [ "$mode" = tests ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.txt 2>&1
+  rc=$?; echo "smoke rc=$rc $(tail -1 gpurun_out/smoke_$tag.txt)" >> $st
+  [ $rc -eq 0 ] || exit $rc
+fi
 run c2 300
 run single 200 --fit single --cpu-sample 1
-run c3 300 --fit full --nsub 10000 --steps 5 --warmup 1
-run c5 300 --fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 5 --warmup 1
-run c4 300 --fit align --nsub 1000 --nchan 256 --nbin 1024 --steps 5 --warmup 2
+# C3 / C5: 16 / 4 one-core oracle sub-ints for the line's own parity
+run c3 500 --fit full --nsub 10000 --steps 5 --warmup 1 --cpu-sample 192
+run c5 600 --fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 5 --warmup 1 --cpu-sample 192
+# C4: 50 timed steps (a 5-step region of ~3-ms steps is host-jitter bound)
+run c4 300 --fit align --nsub 1000 --nchan 256 --nbin 1024 --steps 50 --warmup 5
 run gettoaspsrfits 300 --fit gettoas --psrfits --steps 4 --warmup 1 --timeline gpurun_out/gettoas_psrfits_timeline_$tag.json
 run gettoas 300 --fit gettoas --steps 3 --warmup 1
 run c2nb1000 300 --nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 8

@@ -1669,17 +1669,20 @@ class GetTOAs(object):
         if tau != 0.0:
             (model_name, model_code, model_nu_ref, ngauss, gparams, _mff,
              _ma, _mfa) = read_model(self.modelfile, quiet=quiet)
-            gparams = np.copy(gparams)
-            gparams[1] = 0.0
-            model = gen_gaussian_portrait(model_code, gparams, 0.0,
-                                          data.phases, freqs, model_nu_ref)
             if self.log10_tau:
                 tau = 10 ** tau
             nu_ref_tau = self.nu_refs[ifile][isub][2]
-            model = np.fft.irfft(scattering_portrait_FT(
-                scattering_times(tau, self.alphas[ifile][isub], freqs,
-                                 nu_ref_tau), data.nbin) *
-                np.fft.rfft(model, axis=1), axis=1)
+            alpha = self.alphas[ifile][isub]
+            # the reference convolves the un-scattered portrait with the
+            # fitted scattering kernel on the host, irfft(B(tau (nu /
+            # nu_ref_tau)^alpha) rfft(model)) (pptoas.py:1455-1459); the same
+            # portrait is gen_gaussian_portrait's own scattered branch
+            # (pplib.py:948-953) with tau at the model's reference frequency,
+            # built on the device (k_gauss_port: one LDS FFT per channel)
+            gparams = np.copy(gparams)
+            gparams[1] = tau * data.nbin * (model_nu_ref / nu_ref_tau) ** alpha
+            model = gen_gaussian_portrait(model_code, gparams, alpha,
+                                          data.phases, freqs, model_nu_ref)
         elif cache is not None:
             cache[key] = (model_name, model)
         return model_name, model

@@ -1269,3 +1269,45 @@ def test_odd_nbin_block_kernels_match_oracle(ppl, nbin):
         # (with tau the reference's length-less irfft returns nbin - 1 bins)
         assert got.shape == want.shape == (len(c["freqs"]), nbin - (tau != 0))
         assert np.abs(got - want).max() <= GAUSS_ATOL * np.abs(want).max()
+
+
+@pytest.mark.parametrize("nbin,log10_tau", [(512, True), (1024, False)])
+def test_show_fit_scattered_model_on_device(nbin, log10_tau):
+    """show_fit / get_channels_to_zap's model for a fit with scattering
+    (pptoas.py:1455-1459): the reference convolves the un-scattered portrait
+    with the fitted kernel on the host, irfft(B(tau (nu / nu_ref_tau)^alpha)
+    rfft(model)); the drop-in builds the same portrait on the device as
+    gen_gaussian_portrait's scattered branch with tau moved to the model's
+    reference frequency.  Checked against that host arithmetic (the zap
+    goldens hold no scattering fit: parity of this branch is against the
+    reference's formula, not a reference run)."""
+    import os
+    from pulseportraiture_amd import pptoas, pplib
+    from pulseportraiture_amd.pplib import DataBunch
+    gm = os.path.join(os.path.dirname(__file__), "golden", "example.gmodel")
+    nchan = 48
+    freqs = np.linspace(1150.0, 1850.0, nchan)
+    P = 1.0 / 345.67890123456789
+    gt = pptoas.GetTOAs.__new__(pptoas.GetTOAs)
+    gt.modelfile, gt.is_FITS_model = gm, False
+    gt.add_instrumental_response = False
+    gt.ird = {"DM": 0.0, "wids": [], "irf_types": []}
+    gt.log10_tau = log10_tau
+    tau_rot, alpha, nu_tau = 3.1e-3, -3.7, 1432.5
+    gt.taus = [[np.log10(tau_rot) if log10_tau else tau_rot]]
+    gt.alphas = [[alpha]]
+    gt.nu_refs = [[(1400.0, 1400.0, nu_tau)]]
+    data = DataBunch(freqs=freqs[None, :], phases=pplib.get_bin_centers(nbin),
+                     Ps=np.array([P]), nbin=nbin)
+    _, got = gt._fit_model(data, 0, 0, quiet=True)
+    (_, code, nu_ref, _, gparams, _, _, _) = pplib.read_model(gm, quiet=True)
+    g0 = np.copy(gparams)
+    g0[1] = 0.0
+    base = pplib.gen_gaussian_portrait(code, g0, 0.0, data.phases, freqs,
+                                       nu_ref)
+    want = np.fft.irfft(pplib.scattering_portrait_FT(
+        pplib.scattering_times(tau_rot, alpha, freqs, nu_tau), nbin) *
+        np.fft.rfft(base, axis=1), axis=1)
+    assert got.shape == want.shape
+    np.testing.assert_allclose(got, want, atol=1e-11 * np.abs(want).max(),
+                               rtol=0)

@@ -28,6 +28,40 @@ constexpr int kMaxBfly = 4;                  // radix-4 butterflies / thread / p
 __host__ __device__ __forceinline__ double2 cmk(double r, double i) {
     double2 z; z.x = r; z.y = i; return z;
 }
+// Streaming accesses (round 6): data rows are read once and the cross
+// spectrum X is written once per pass, so they are issued nontemporal and
+// do not evict what IS re-read from the XCD's L2 (model rows, |M|^2, twiddle
+// and moment tables).  C2: k_xspec_w2 24.09 vs 24.83 ms per 10k, 302.4k vs
+// 294.3k fits/s; C3 / C5 +1-2 % (profiles/r06/ab_nt_status.txt).
+#ifndef PPF_NT
+#define PPF_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+#if PPF_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float2 ld_stream(const float2 *p) {
+    typedef float v2 __attribute__((ext_vector_type(2)));
+    const v2 v = ld_stream(reinterpret_cast<const v2 *>(p));
+    return float2(v.x, v.y);
+}
+__device__ __forceinline__ double2 ld_stream(const double2 *p) {
+    typedef double v2 __attribute__((ext_vector_type(2)));
+    const v2 v = ld_stream(reinterpret_cast<const v2 *>(p));
+    return cmk(v.x, v.y);
+}
+__device__ __forceinline__ void st_stream(double2 *p, double2 v) {
+#if PPF_NT
+    typedef double v2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(v2{v.x, v.y}, reinterpret_cast<v2 *>(p));
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return cmk(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return cmk(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return cmk(a.x * s, a.y * s); }

@@ -568,7 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_w(DsumArgs a) {
         // unconditional (a valid row when past the block): keeps p in VGPRs
         const VecT *src = rows + (int64_t)(m < c1 ? m : c1 - 1) * (NB / VW);
 #pragma unroll
-        for (int i = 0; i < NL; ++i) p[i] = src[lane + 64 * i];
+        for (int i = 0; i < NL; ++i) p[i] = ld_stream(src + lane + 64 * i);
     };
     auto row = [&](VecT (&p)[NL], int m, int m2) {
         wave_lds_sync();                      // the previous row's reads are issued

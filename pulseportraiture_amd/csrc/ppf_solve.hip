@@ -374,6 +374,9 @@ constexpr int kPassChans = kBlock;             // channels per workgroup
 #ifndef PPF_PASS_SPLIT
 #define PPF_PASS_SPLIT 1
 #endif
+#ifndef PPF_PASS_NT
+#define PPF_PASS_NT PPF_NT
+#endif
 template <bool SCAT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS_WPE))) void k_pass(SolveArgs a) {
     __shared__ double red[kWaves * 21];
@@ -479,7 +482,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
                 const int k = min(kb + u, kend - 1);
+#if PPF_PASS_NT
+                // X streamed past the L2, which keeps |M|^2 (ld_stream)
+                xo[u] = ld_stream(Xc + k * xs);
+#else
                 xo[u] = Xc[k * xs];
+#endif
                 if (SCAT) po[u] = Pc[k * xs];
             }
         };
@@ -1186,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_MOM_
             const int k = kb + 4 * t + kk;
             // (past the end: the last needed harmonic again, an L2 hit)
             const int kc = k < kend ? k : kend - 1;
-            xv[t] = Xr[(int64_t)kc * a.nchan];
+            xv[t] = ld_stream(Xr + (int64_t)kc * a.nchan);
         }
     };
     auto keep = [&](int k) { return valid && k < kend; };

@@ -288,7 +288,7 @@ void k_xspec_w(XspecArgs a) {
     auto fetch = [&](int n) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
 #pragma unroll
-        for (int q = 0; q < R; ++q) zr[q] = src[lane + 64 * q];
+        for (int q = 0; q < R; ++q) zr[q] = ld_stream(src + lane + 64 * q);
     };
     int n = cbase + wave;
     if (usable(n)) fetch(n);
@@ -528,9 +528,9 @@ void k_xspec_w(XspecArgs a) {
                     const int slot = k == N ? wfft::pad<LOG2N>(N / 2)
                                             : (k == N / 2 ? XNYQ : wfft::pad<LOG2N>(k));
 #if PPF_XS_ONEPASS
-                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[slot], ie2) : cmk(0.0, 0.0);
+                    st_stream(Xs + (int64_t)k * a.nchan + nc, ok ? cscale(b[slot], ie2) : cmk(0.0, 0.0));
 #else
-                    Xs[(int64_t)k * a.nchan + nc] = ok ? b[slot] : cmk(0.0, 0.0);
+                    st_stream(Xs + (int64_t)k * a.nchan + nc, ok ? b[slot] : cmk(0.0, 0.0));
 #endif
                 }
             }
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         asm volatile("" : "+v"(off));
 #pragma unroll
         for (int c = 0; c < NLD; ++c)
-            zr[c] = *reinterpret_cast<const VecT *>(x + off + 1024u * (unsigned)c);
+            zr[c] = ld_stream(reinterpret_cast<const VecT *>(x + off + 1024u * (unsigned)c));
     };
     auto usable = [&](int n) {
         return act && n < cend && __builtin_amdgcn_readlane(ch_use, n - cbase) != 0;
@@ -1029,6 +1029,9 @@ __device__ __forceinline__ int x2slot(int k) { return k + (k >> 6); }   // k <= 
 #ifndef PPF_XSPEC2
 #define PPF_XSPEC2 1
 #endif
+#ifndef PPF_X2_NT
+#define PPF_X2_NT (PPF_NT ? 3 : 0)   // nontemporal row loads (1), X stores (2): ld/st_stream
+#endif
 #ifndef PPF_X2_MEARLY
 #define PPF_X2_MEARLY 0
 #endif
@@ -1133,7 +1136,13 @@ void k_xspec_w2(XspecArgs a) {
     auto fetch = [&](int n) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) zr[q] = src[lane0 + 64 * q];
+        for (int q = 0; q < 16; ++q) {
+#if PPF_X2_NT & 1
+            zr[q] = __builtin_nontemporal_load(src + lane0 + 64 * q);
+#else
+            zr[q] = src[lane0 + 64 * q];
+#endif
+        }
     };
 #if PPF_X2_EW
     // Round 6: the next row's load is unconditional (a row past the block,
@@ -1392,7 +1401,14 @@ void k_xspec_w2(XspecArgs a) {
 #if PPF_X2_DIAG & 1
                     if (ie2 == 12345.0)            // (timing-only build: no X stores)
 #endif
+                    {
+#if PPF_X2_NT & 2
+                    const double2 v = ok ? cscale(b[x2slot(k)], ie2) : cmk(0.0, 0.0);
+                    __builtin_nontemporal_store(vd2{v.x, v.y}, reinterpret_cast<vd2 *>(Xs + (int64_t)k * a.nchan + nc));
+#else
                     Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[x2slot(k)], ie2) : cmk(0.0, 0.0);
+#endif
+                    }
                 }
             }
         }
@@ -1571,7 +1587,7 @@ void k_xspec_wm(XspecArgs a) {
 #pragma unroll
         for (int i = 0; i < PJ; ++i) {
             const int t = lane + 64 * i;
-            pre[i] = src[t < NF ? t : NF - 1];
+            pre[i] = ld_stream(src + (t < NF ? t : NF - 1));
         }
     };
     fetch(min(cbase + wave, cend - 1));
@@ -1684,7 +1700,7 @@ void k_xspec_wm(XspecArgs a) {
                 const double2 *b = lds + c * SL;
                 const double ie2 = ok ? reinterpret_cast<const double *>(b + IE)[0] : 0.0;
                 for (int k = threadIdx.x / kWmW; k < kw; k += 64)
-                    Xs[(int64_t)k * a.nchan + nc] = ok ? cscale(b[k], ie2) : cmk(0.0, 0.0);
+                    st_stream(Xs + (int64_t)k * a.nchan + nc, ok ? cscale(b[k], ie2) : cmk(0.0, 0.0));
             }
         }
         __syncthreads();
@@ -1746,7 +1762,7 @@ void k_xspec_wo(XspecArgs a) {
 #pragma unroll
         for (int i = 0; i < PJ; ++i) {
             const int t = lane + 64 * i;
-            p[i] = src[t < NF ? t : NF - 1];
+            p[i] = ld_stream(src + (t < NF ? t : NF - 1));
         }
     };
     fetch(pa, min(cbase + wave, cend - 1));
@@ -1844,7 +1860,7 @@ void k_xspec_wo(XspecArgs a) {
                 const int o0 = c < kWmW ? 0 : NF, st = c < kWmW ? 1 : -1;
                 const double ie2 = ok ? b[o0].x : 0.0;
                 for (int k = threadIdx.x / RW; k < kw; k += 64 * kWmW / RW)
-                    Xs[(int64_t)k * a.nchan + nc] = (ok && k) ? cscale(b[o0 + st * k], ie2) : cmk(0.0, 0.0);
+                    st_stream(Xs + (int64_t)k * a.nchan + nc, (ok && k) ? cscale(b[o0 + st * k], ie2) : cmk(0.0, 0.0));
             }
         }
         __syncthreads();
@@ -2190,7 +2206,7 @@ __global__ __launch_bounds__(64 * kXW) void k_align_part_w(AlignArgs a) {
     auto fetch = [&](int s) {
         const RowT *src = rows + ((int64_t)s * a.nchan + n) * N;
 #pragma unroll
-        for (int q = 0; q < R; ++q) zr[q] = src[lane + 64 * q];
+        for (int q = 0; q < R; ++q) zr[q] = ld_stream(src + lane + 64 * q);
     };
     int s = next_live(s0 + wave);
     if (s < s1) fetch(s);

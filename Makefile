@@ -3,16 +3,19 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := pulseportraiture_amd/csrc
 OUT := pulseportraiture_amd/lib/libppfit.so
-SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_xspec.hip $(CSRC)/ppf_solve.hip $(CSRC)/ppf_psrfits.hip $(CSRC)/ppf_api.cpp $(CSRC)/ppf_io.cpp
+SRCS := $(CSRC)/ppf_kernels.hip $(CSRC)/ppf_longfft.hip $(CSRC)/ppf_xspec.hip $(CSRC)/ppf_solve.hip $(CSRC)/ppf_psrfits.hip $(CSRC)/ppf_api.cpp $(CSRC)/ppf_io.cpp
 HDRS := $(CSRC)/ppf_device.hpp $(CSRC)/ppf_state.hpp $(CSRC)/ppf_wfft.hpp $(CSRC)/ppf_wfft2.hpp $(CSRC)/ppf_internal.hpp include/ppfit.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed \
             -ffp-contract=fast -munsafe-fp-atomics
 
-OBJS := $(CSRC)/ppf_kernels.o $(CSRC)/ppf_xspec.o $(CSRC)/ppf_solve.o $(CSRC)/ppf_psrfits.o $(CSRC)/ppf_api.o $(CSRC)/ppf_io.o
+OBJS := $(CSRC)/ppf_kernels.o $(CSRC)/ppf_longfft.o $(CSRC)/ppf_xspec.o $(CSRC)/ppf_solve.o $(CSRC)/ppf_psrfits.o $(CSRC)/ppf_api.o $(CSRC)/ppf_io.o
 
 all: $(OUT)
 
 $(CSRC)/ppf_kernels.o: $(CSRC)/ppf_kernels.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/ppf_longfft.o: $(CSRC)/ppf_longfft.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/ppf_xspec.o: $(CSRC)/ppf_xspec.hip $(HDRS)

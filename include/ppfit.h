@@ -46,7 +46,7 @@ extern "C" {
  * ppf_kernel_ms_history slot 0 = the first moment pass of either kind;
  * ppf_solver_ms_history, ppf_host_copy. */
 /* ABI 5 (round 6): ppf_rotate_batch_ref. */
-#define PPF_ABI_VERSION 5
+#define PPF_ABI_VERSION 6
 
 enum ppf_error {
     PPF_OK = 0,
@@ -327,6 +327,22 @@ int ppf_resid_chi2_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_d
 int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin,
                     int32_t in_dtype, const void *in, int32_t frac,
                     double *out, void *stream);
+
+/* Power-spectrum noise of rows of ANY length (round 6, ABI 6):
+ * pplib.get_noise_PS (pplib.py:2312-2338) where ppf_noise_batch's LDS
+ * transforms do not reach -- chans=False ravels a whole portrait into one
+ * row of nchan * nbin samples (2^20 at 512 x 2048), and rows past 8192 (even)
+ * / 4095 (odd) samples.  The rFFT is a four-step transform of block LDS FFTs
+ * (transform length a power of two) or Bluestein's chirp z-transform on one
+ * (any other length), up to 2^24 complex points (2^25 samples for a
+ * power-of-two row, 2^24 otherwise; PPF_EUNSUP past that).
+ * in: [nrows][nbin] (in_dtype); out: [nrows] device doubles; workspace:
+ * device scratch of ppf_noise_long_workspace_bytes(nrows, nbin) bytes
+ * (0: nbin unsupported). */
+size_t ppf_noise_long_workspace_bytes(int64_t nrows, int64_t nbin);
+int ppf_noise_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype,
+                   const void *in, int32_t frac, double *out, void *workspace,
+                   size_t workspace_bytes, void *stream);
 
 /* Batched 1-D FFTFIT: pplib.fit_phase_shift (pplib.py:2136-2182): brute
  * force over Ns points of [lo, hi] then Nelder-Mead (scipy fmin) polish.

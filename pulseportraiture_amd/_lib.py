@@ -25,7 +25,7 @@ OPT_NO_X = 2
 OPT_SCIPY_TR = 4          # scattering fits follow scipy's trust-ncg path
 OPT_MOM_X = 8             # phase/DM/GM fits: moments from the stored cross spectrum
 OPT_FUSED_MOM = 16        # ... from the fused k_xmom_g pass (no X)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # ppf_result: 32 doubles (include/ppfit.h)
 RESULT_FIELDS = (
@@ -93,6 +93,11 @@ SIGNATURES = {
                                             _vp, _vp, _vp, _vp]),
     "ppf_noise_batch": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _i32, _vp,
                                        _i32, _vp, _vp]),
+    "ppf_noise_long_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64,
+                                                         ctypes.c_int64]),
+    "ppf_noise_long": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64,
+                                      _i32, _vp, _i32, _vp, _vp,
+                                      ctypes.c_size_t, _vp]),
     "ppf_resid_chi2_batch": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _i32,
                                             _vp, _vp, _vp, _vp, _vp, _vp,
                                             ctypes.c_double, _vp, _vp]),

@@ -837,6 +837,92 @@ int ppf_noise_batch(ppf_ctx *ctx, int64_t nrows, int32_t nbin, int32_t in_dtype,
     return PPF_OK;
 }
 
+// ppf_noise_long's plan and workspace (ppf_longfft.hip): rows in chunks of
+// at most 256 MB of complex work buffers
+namespace {
+struct LongPlan {
+    ppf::LongNoiseArgs a;
+    int64_t rows_c;
+    size_t off_A, off_Y, off_part, bytes;
+};
+bool long_plan(int64_t nrows, int64_t nbin, int frac, LongPlan &p) {
+    if (nrows < 0 || nbin < 1 || frac < 1) return false;
+    ppf::LongNoiseArgs &a = p.a;
+    a = ppf::LongNoiseArgs{};
+    a.nbin = nbin;
+    a.packed = (nbin % 2 == 0) ? 1 : 0;
+    a.n = a.packed ? nbin / 2 : nbin;
+    a.nharm = nbin / 2 + 1;
+    a.kc = (int64_t)((1.0 - std::pow((double)frac, -1.0)) * (double)a.nharm);
+    const bool pow2 = (a.n & (a.n - 1)) == 0;
+    a.bluestein = (pow2 && a.n >= 64) ? 0 : 1;
+    int64_t M = 64;
+    const int64_t need = a.bluestein ? 2 * a.n - 1 : a.n;
+    while (M < need) M *= 2;
+    int m = 0;
+    while (((int64_t)1 << m) < M) ++m;
+    if (m > 24) return false;             // M1, M2 <= 4096 (the block LDS FFT)
+    a.M = M;
+    a.log2M = m;
+    a.log2M1 = (m + 1) / 2;
+    a.M1 = (int64_t)1 << a.log2M1;
+    a.M2 = M / a.M1;
+    const size_t row_b = (size_t)M * sizeof(double2);
+    int64_t rc = (int64_t)((size_t)(256u << 20) / (2 * row_b));
+    if (rc < 1) rc = 1;
+    p.rows_c = nrows < rc ? (nrows > 0 ? nrows : 1) : rc;
+    size_t off = a.bluestein ? align256(2 * row_b) : 0;
+    p.off_A = off;
+    off += align256((size_t)p.rows_c * row_b);
+    p.off_Y = off;
+    off += align256((size_t)p.rows_c * row_b);
+    p.off_part = off;
+    off += align256((size_t)p.rows_c * 256 * sizeof(double));
+    p.bytes = off;
+    return true;
+}
+}  // namespace
+
+size_t ppf_noise_long_workspace_bytes(int64_t nrows, int64_t nbin) {
+    LongPlan p;
+    return long_plan(nrows, nbin, 4, p) ? p.bytes : 0;
+}
+
+int ppf_noise_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype, const void *in,
+                   int32_t frac, double *out, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nrows < 0 || nbin < 1 || frac < 1 || (nrows > 0 && (!in || !out)))
+        return fail(ctx, PPF_EINVAL, "bad noise arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    LongPlan p;
+    if (!long_plan(nrows, nbin, frac, p))
+        return fail(ctx, PPF_EUNSUP, "nbin=%lld: transform longer than 2^24 points", (long long)nbin);
+    if (nrows == 0) return PPF_OK;
+    if (!workspace || workspace_bytes < p.bytes)
+        return fail(ctx, PPF_EINVAL, "workspace %zu < %zu bytes", workspace_bytes, p.bytes);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T1, *T2, *unused;
+    int rc = twiddles(ctx, (int)(2 * p.a.M1), st, &T1, &unused);
+    if (rc) return rc;
+    if ((rc = twiddles(ctx, (int)(2 * p.a.M2), st, &T2, &unused))) return rc;
+    char *ws = (char *)workspace;
+    double2 *Bf = (double2 *)ws;
+    if (p.a.bluestein && (e = ppf::launch_chirp_ft(p.a, Bf, Bf + p.a.M, T1, T2, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_lf_chirp");
+    p.a.in_dtype = in_dtype;
+    p.a.in = in;
+    for (int64_t r0 = 0; r0 < nrows; r0 += p.rows_c) {
+        p.a.row0 = r0;
+        const int64_t nr = nrows - r0 < p.rows_c ? nrows - r0 : p.rows_c;
+        e = ppf::launch_noise_long(p.a, nr, (double2 *)(ws + p.off_A), (double2 *)(ws + p.off_Y), Bf,
+                                   (double *)(ws + p.off_part), out, T1, T2, st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "k_lf");
+    }
+    return PPF_OK;
+}
+
 int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, const double *D,
                      const double *M, const int32_t *model_index, const double *errs_FT,
                      const double *params, const double *P, const double *freqs, const double *nus,

@@ -203,6 +203,29 @@ struct NoiseArgs {
     double *out;
 };
 
+// get_noise_PS of long rows (ppf_longfft.hip): the plan of one call
+struct LongNoiseArgs {
+    int64_t nbin;               // real samples per row
+    int64_t n;                  // complex transform length (rfft_len)
+    int64_t M, M1, M2;          // four-step size M = M1 M2 (powers of two)
+    int log2M, log2M1;
+    int packed;                 // even nbin: two samples per complex point
+    int bluestein;              // n not a power of two >= 64: chirp z-transform
+    int64_t nharm, kc;          // rfft bins nbin / 2 + 1, noise cut
+    int in_dtype;
+    const void *in;
+    int64_t row0;               // first row of this launch
+};
+struct LongPassArgs {
+    int64_t nbatch;
+    int len, log2len;
+    int64_t in_stride, in_bstride, out_stride, out_bstride, row_elems, M;
+    int twiddle, inverse;
+    const double2 *in;
+    double2 *out;
+    const double2 *T;
+};
+
 struct PhaseShiftArgs {
     int nbin, log2N, dtype, kc, Ns;
     double lo, hi;
@@ -340,6 +363,12 @@ size_t tr_state_bytes();
 int pass_blocks(int nchan);
 hipError_t launch_rotate(const RotateArgs &a, int64_t nrows, hipStream_t st);
 hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
+int lf_pow_blocks(const LongNoiseArgs &a);
+hipError_t launch_chirp_ft(const LongNoiseArgs &a, double2 *Bf, double2 *Bs, const double2 *T1,
+                           const double2 *T2, hipStream_t st);
+hipError_t launch_noise_long(const LongNoiseArgs &a, int64_t nrows, double2 *A, double2 *Y,
+                             const double2 *Bf, double *part, double *out, const double2 *T1,
+                             const double2 *T2, hipStream_t st);
 // wave-per-row noise (k_noise_w) for N = nbin/2 = 128..1024
 bool noise_wave_supported(int log2N);
 hipError_t launch_noise_wave(const NoiseArgs &a, int64_t nrows, hipStream_t st);

@@ -559,12 +559,20 @@ def pinned_host_array(shape, dtype=np.float32):
     return t.numpy()
 
 
+def _noise_batch_len_ok(nbin):
+    """Row lengths ppf_noise_batch's LDS transforms take (nbin_supported)."""
+    return 32 <= nbin <= 8192 and (nbin % 2 == 0 or nbin <= 4095)
+
+
 def noise_rows(rows, frac=4, dev=None):
-    """get_noise_PS per row of rows [..., nbin] -> [...] float64."""
+    """get_noise_PS per row of rows [..., nbin] -> [...] float64 (rows past
+    the LDS transforms: ppf_noise_long)."""
     dev = device(dev)
     r = to_dev(rows, dev, _data_dtype(rows))
     shape = r.shape
     r2 = r.reshape(-1, shape[-1]).contiguous()
+    if not _noise_batch_len_ok(shape[-1]):
+        return noise_rows_long(r2, frac, dev).reshape(shape[:-1])
     out = torch.empty(r2.shape[0], dtype=torch.float64, device=dev)
     ctx = _lib.context(dev.index)
     rc = _lib.load().ppf_noise_batch(
@@ -578,7 +586,8 @@ def noise_rows(rows, frac=4, dev=None):
 # largest prime factor of the transform length the LDS path takes for
 # get_noise_PS of a single flattened row: the generic-radix stage costs
 # O(N R) per row (R the prime), so a length like 8186 = 2 x 4093 would be a
-# 4093-point direct DFT inside one workgroup; rocFFT's Bluestein is faster
+# 4093-point direct DFT inside one workgroup; ppf_noise_long's Bluestein
+# transform is faster
 NOISE_MAX_PRIME = 61
 
 
@@ -595,24 +604,46 @@ def noise_len_supported(n):
     """Row lengths get_noise_PS(chans=False) sends to ppf_noise_batch (its LDS
     FFT): even 32..8192 or odd 33..4095 (every length ppf_noise_batch
     accepts) whose transform length -- n / 2 complex points at even n, n at
-    odd n -- has no prime factor above NOISE_MAX_PRIME; the rest go to the
-    device FFT library (noise_long)."""
+    odd n -- has no prime factor above NOISE_MAX_PRIME; the rest go to
+    ppf_noise_long (noise_long)."""
     if not 32 <= n <= (8192 if n % 2 == 0 else 4095):
         return False
     return _max_prime_factor(n // 2 if n % 2 == 0 else n) <= NOISE_MAX_PRIME
 
 
-def noise_long(row, frac=4, dev=None):
-    """get_noise_PS of ONE row of any length (pplib.py:2334-2338): the mean
-    power of the top 1/frac of the rFFT, the transform by the device FFT
-    library (torch.fft -> rocFFT), float64."""
+def noise_rows_long(rows, frac=4, dev=None):
+    """get_noise_PS of rows [nrows, nbin] of any length (pplib.py:2312-2338)
+    on ppf_noise_long: a four-step rFFT of block LDS transforms, or
+    Bluestein's chirp z-transform on one, up to 2^24 complex points ->
+    [nrows] float64 on the device."""
     dev = device(dev)
-    x = to_dev(row, dev, torch.float64).reshape(-1)
-    n = x.numel()
-    F = torch.fft.rfft(x)
-    pows = (F.real * F.real + F.imag * F.imag) / n
-    kc = int((1 - frac ** -1) * pows.numel())
-    return float(torch.sqrt(pows[kc:].mean()))
+    r = to_dev(rows, dev, _data_dtype(rows))
+    r2 = r.reshape(-1, r.shape[-1]).contiguous()
+    nrows, nbin = r2.shape
+    lib = _lib.load()
+    nb = lib.ppf_noise_long_workspace_bytes(nrows, nbin)
+    if nb == 0:
+        raise NotImplementedError(
+            "get_noise_PS of %d-sample rows: past the 2^24-point transform"
+            % nbin)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    out = torch.empty(nrows, dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = lib.ppf_noise_long(
+        ctx, nrows, nbin,
+        _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
+        _p(r2), int(frac), _p(out), _p(ws), nb, _stream(dev))
+    _lib.check(rc, ctx)
+    return out
+
+
+def noise_long(row, frac=4, dev=None):
+    """get_noise_PS of ONE row of any length (pplib.py:2334-2338: the
+    flattened portrait of get_noise(chans=False)): the mean power of the top
+    1/frac of the rFFT, float64 (ppf_noise_long)."""
+    x = to_dev(row, device(dev), None if isinstance(row, torch.Tensor)
+               else torch.float64)
+    return float(noise_rows_long(x.reshape(1, -1), frac, dev).cpu()[0])
 
 
 def unpack_psrfits(raw, elem, npol, nchan, nbin, scl, offs, wts=None,

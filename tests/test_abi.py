@@ -31,7 +31,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_struct_layouts_match():
     lib = _lib.load()
-    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.ppf_abi_version() == _lib.ABI_VERSION == 6
     assert lib.ppf_sizeof_fit_desc() == ctypes.sizeof(_lib.FitDesc)
     assert lib.ppf_sizeof_result() == 8 * _lib.RESULT_DOUBLES == 256
 
@@ -84,6 +84,17 @@ def test_workspace_query_and_validation_without_gpu():
     d.options, d.guess = 0, 0
     # a NULL context is rejected before touching the device
     assert lib.ppf_fit_batch(None, ctypes.byref(d), None) == _lib.PPF_EINVAL
+    # get_noise_PS of long rows: any length up to 2^24 transform points
+    # (2^25 samples for a power-of-two row), workspace in 256-MB row chunks
+    for nb in (1, 2, 33, 8186, 1 << 20, 511 * 1023, 512 * 1000, 1 << 25):
+        assert lib.ppf_noise_long_workspace_bytes(3, nb) > 0, nb
+    assert lib.ppf_noise_long_workspace_bytes(3, (1 << 25) + 2) == 0
+    assert lib.ppf_noise_long_workspace_bytes(1, 0) == 0
+    # a power-of-two row needs no chirp buffers: 2 x 2^19 x 16 B per row
+    assert lib.ppf_noise_long_workspace_bytes(1, 1 << 20) == \
+        2 * (1 << 19) * 16 + 256 * 8
+    assert lib.ppf_noise_long(None, 1, 1 << 20, _lib.PPF_F64, None, 4, None,
+                              None, 0, None) == _lib.PPF_EINVAL
 
 
 @pytest.mark.parametrize("seed", range(40))

@@ -58,17 +58,61 @@ def test_noise_matches_reference(ppl):
                                axis=-1))
         np.testing.assert_allclose(ppl.get_noise(x, chans=True), want,
                                    rtol=1e-12, err_msg=str(shape))
-    with pytest.raises(NotImplementedError):     # odd nbin past 4095
-        ppl.get_noise(np.ones((2, 4097)), chans=True)
-    # chans=False ravels the portrait (pplib.py:2334-2338): 64 x 2048 and an
-    # odd length go through the device FFT library (no LDS-size cap); the
+    # rows past the LDS transforms (odd > 4095, even > 8192): ppf_noise_long
+    # per row -- 4097 and 16382 = 2 x 8191 on the chirp z-transform, 16384
+    # on the four-step
+    for shape in ((2, 4097), (2, 16382), (3, 16384)):
+        x = np.random.default_rng(8).normal(size=shape)
+        F = np.fft.rfft(x, axis=-1)
+        p = np.real(F * np.conj(F)) / shape[-1]
+        want = np.sqrt(np.mean(p[:, int((1 - 4 ** -1) * p.shape[-1]):],
+                               axis=-1))
+        np.testing.assert_allclose(ppl.get_noise(x, chans=True), want,
+                                   rtol=1e-11, err_msg=str(shape))
+    # chans=False ravels the portrait (pplib.py:2334-2338) into one row of
+    # nchan x nbin samples: ppf_noise_long (four-step for a power-of-two
+    # transform, chirp z-transform otherwise; no LDS-size cap).  The
     # restatement is the reference's own NumPy arithmetic
-    for shape in ((64, 2048), (3, 1001), (1002,), (8186,), (1022,), (1000,)):
+    for shape in ((64, 2048), (512, 2048), (3, 1001), (511, 1023),
+                  (512, 1000), (1002,), (8186,), (1022,), (1000,), (2, 3),
+                  (5,), (1,)):
         x = np.random.default_rng(4).normal(size=shape)
         F = np.fft.rfft(x.ravel())
         p = np.real(F * np.conj(F)) / x.size
         want = np.sqrt(np.mean(p[int((1 - 4 ** -1) * len(p)):]))
-        assert abs(ppl.get_noise(x) / want - 1) < 1e-12, shape
+        assert abs(ppl.get_noise(x) / want - 1) < 1e-11, shape
+
+
+def test_noise_long_rows_match_numpy():
+    """ppf_noise_long against NumPy's rFFT at lengths that exercise each
+    plan: power-of-two transforms at the four-step's smallest and largest
+    splits, chirp z-transforms of prime, odd-composite and even lengths, f32
+    input (converted exactly), frac != 4, and several 256-MB row chunks."""
+    from pulseportraiture_amd import engine
+    rng = np.random.default_rng(9)
+
+    def want(x, frac=4):
+        F = np.fft.rfft(x, axis=-1)
+        p = np.real(F * np.conj(F)) / x.shape[-1]
+        return np.sqrt(np.mean(p[..., int((1 - frac ** -1) * p.shape[-1]):],
+                               axis=-1))
+    for nrows, nbin in ((3, 128), (2, 1 << 22), (2, 65537), (2, 3 * 5 * 7 * 11 * 13),
+                        (4, 2 * 4099), (1, 1 << 25)):
+        x = rng.normal(size=(nrows, nbin))
+        got = engine.noise_rows_long(x).cpu().numpy()
+        np.testing.assert_allclose(got, want(x), rtol=1e-11,
+                                   err_msg=str((nrows, nbin)))
+    x = rng.normal(size=(2, 3000)).astype(np.float32)
+    np.testing.assert_array_equal(
+        engine.noise_rows_long(x).cpu().numpy(),
+        engine.noise_rows_long(x.astype(np.float64)).cpu().numpy())
+    np.testing.assert_allclose(engine.noise_rows_long(x, frac=3).cpu().numpy(),
+                               want(x.astype(np.float64), 3), rtol=1e-11)
+    # 40 rows of 2^21 samples: 2^20-point transforms, 16 MB per work row,
+    # 8 rows per 256-MB chunk -> five chunks
+    x = rng.normal(size=(40, 1 << 21)).astype(np.float32)
+    np.testing.assert_allclose(engine.noise_rows_long(x).cpu().numpy(),
+                               want(x.astype(np.float64)), rtol=1e-11)
 
 
 def test_noise_fp32_input_equals_fp64(ppl):

@@ -299,7 +299,12 @@ __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int 
                              double hi, double *sh /*LDS >= 2*Ns+8*/, double *fval, int *nfev) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double step = (Ns != 1) ? (hi - lo) / (double)(Ns - 1) : 1.0;
-    if (Ns >= 2 * kBlock) {
+#ifndef PPF_GUESS_DIAG
+#define PPF_GUESS_DIAG 0    // timing-only builds: 1 no brute grid, 2 no polish
+#endif
+    if (PPF_GUESS_DIAG & 1) {
+        for (int j = threadIdx.x; j < Ns; j += kBlock) sh[j] = (double)j;
+    } else if (Ns >= 2 * kBlock) {
         // large grids (ppalign: Ns = nbin): one point per lane, two points
         // in flight; harmonics broadcast from LDS, phasor e^{2 pi i k ph} by
         // recurrence, re-seeded exactly every 64 harmonics
@@ -346,7 +351,7 @@ __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int 
         double f1 = wave_fps_eval(xm, nharm, sim1, inv_err2); ++nf;
         if (f1 < f0) { double t = sim0; sim0 = sim1; sim1 = t; t = f0; f0 = f1; f1 = t; }
         int iters = 1;
-        while (nf < 200 && iters < 200) {
+        while (!(PPF_GUESS_DIAG & 2) && nf < 200 && iters < 200) {
             if (fabs(sim1 - sim0) <= 1e-4 && fabs(f0 - f1) <= 1e-4) break;
             double xbar = sim0;
             double xr = 2.0 * xbar - sim1;

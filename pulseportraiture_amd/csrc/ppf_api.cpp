@@ -23,7 +23,8 @@ struct ppf_ctx {
     std::string err;               // last error message, guarded by err_mu
     mutable std::mutex err_mu;
     std::map<int, double2 *> tw;   // nbin -> [T (N) | T2 (N)]
-    std::mutex tw_mu;              // guards tw (calls from several host threads)
+    std::map<std::pair<int, int>, double2 *> cz;   // (Ns, Kmax) -> chirp z-transform tables
+    std::mutex tw_mu;              // guards tw and cz (calls from several host threads)
     bool prof = false;
     static constexpr int kRing = 256;
     // [0..4]: stage boundaries; [5, 6]: the first moment pass (k_xmom_g,
@@ -116,6 +117,42 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
     }
     *T = it->second;
     *T2 = it->second + ppf::rfft_len(nbin);
+    return PPF_OK;
+}
+
+// The guess's brute grid of a whole turn with Ns >= 512 points (ppalign:
+// Ns = nbin) as a chirp z-transform (k_guess, round 6): the plan and its
+// cached kernel tables.  Returns false (direct sums) where it does not apply.
+#ifndef PPF_GUESS_CZ
+#define PPF_GUESS_CZ 1
+#endif
+bool cz_plan(int Ns, int K, ppf::CzPlan &c) {
+    if (!PPF_GUESS_CZ || Ns < 2 * ppf::kBlock || K < 2) return false;
+    int P = 64;
+    while (P < 2 * K - 1) P *= 2;
+    if (P != 1024) return false;                 // cz_fft's size (nbin 1024)
+    c.Ns = Ns; c.K = K; c.P = P; c.J = P - K + 1; c.Q = (Ns + c.J - 1) / c.J;
+    return true;
+}
+int cz_tables(ppf_ctx *ctx, const ppf::CzPlan &c, hipStream_t st, const double2 **B, const double2 **T) {
+    const double2 *T2;
+    int rc = twiddles(ctx, 2 * c.P, st, T, &T2);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lock(ctx->tw_mu);
+    const auto key = std::make_pair(c.Ns, c.K);
+    auto it = ctx->cz.find(key);
+    if (it == ctx->cz.end()) {
+        double2 *p = nullptr;
+        hipError_t e = hipMalloc(&p, sizeof(double2) * (size_t)c.Q * c.P);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(cz)");
+        e = ppf::launch_cz_table(c, p, *T, st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "k_cz_table");
+        // cached for calls on any stream (as the twiddles)
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize(cz)");
+        it = ctx->cz.emplace(key, p).first;
+    }
+    *B = it->second;
     return PPF_OK;
 }
 
@@ -252,6 +289,7 @@ void ppf_destroy(ppf_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (auto &kv : ctx->tw) (void)hipFree(kv.second);
+    for (auto &kv : ctx->cz) (void)hipFree(kv.second);
     for (auto &set : ctx->ring)
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
@@ -553,6 +591,11 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.gpart = xa.gpart;
         ga.gwx = xa.gw;
         ga.nblk = L.nblk;
+        ppf::CzPlan cz{};
+        if (cz_plan(ga.Ns, d->nbin / 2 + 1, cz)) {
+            if ((rc = cz_tables(ctx, cz, st, &ga.czB, &ga.czT))) return rc;
+            ga.czP = cz.P; ga.czJ = cz.J; ga.czQ = cz.Q; ga.czK = cz.K;
+        }
         if ((e = ppf::launch_guess(ga, st)) != hipSuccess) return hip_fail(ctx, e, "k_guess");
     }
     mark(3);

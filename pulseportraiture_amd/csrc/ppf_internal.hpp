@@ -107,7 +107,21 @@ struct GuessArgs {
     const double2 *gpart;        // [nsub][nblk][guess_slots(log2N)]
     const double *gwx;           // [nsub][nblk][3]
     int nblk;
+    // brute grid of a whole turn (Ns >= 512, ppalign's Ns = nbin) as a
+    // chirp z-transform (round 6): czB = FFT_P of the chirp kernel of each of
+    // the czQ output chunks of czJ points (scaled by 1/P), czT its P-point
+    // twiddles; null: the direct sums
+    const double2 *czB, *czT;
+    int czP, czJ, czQ, czK;
 };
+
+// chirp z-transform plan of a whole-turn brute grid (k_guess): Kmax
+// harmonics, Ns points over [lo, lo + 1], outputs in Q chunks of J points,
+// P-point transforms (P = pow2 >= 2 Kmax - 1, J = P - Kmax + 1)
+struct CzPlan {
+    int Ns, K, P, J, Q;
+};
+hipError_t launch_cz_table(const CzPlan &c, double2 *B, const double2 *T, hipStream_t st);
 
 struct TRState;
 

@@ -295,8 +295,101 @@ __device__ double wave_fps_eval(const double2 *xm, int nharm, double phase, doub
 
 // Brute grid over Ns points of [lo, hi] (all waves), then fmin polish (wave
 // 0).  Returns the phase in every thread; fval/nfev via pointers (thread 0).
+// exp(i pi m^2 / L), m^2 reduced mod 2L in integers (exact phase; 32-bit:
+// |m|, L < 2^13 here, so r^2 < 2^28)
+__device__ __forceinline__ double2 cz_chirp(int m, int L) {
+    int r = m % (2 * L);
+    if (r < 0) r += 2 * L;
+    const int e = (r * r) % (2 * L);
+    double s, c;
+    sincospi((double)e / (double)L, &s, &c);
+    return cmk(c, s);
+}
+
+// the chirp z-transform's P-point FFTs, P = 1024 (nbin 1024, ppalign's
+// configs[3]): the compile-time-size Stockham passes, one radix-4 butterfly
+// per thread.  The runtime-size lds_fft (four), a 2048-point case (two) and
+// even a second 512-point instantiation each took k_guess from four waves
+// per SIMD to two or three, so other sizes keep the direct sums.
+template <bool INV>
+__device__ __forceinline__ void cz_fft(double2 *buf, int log2P, const double2 *T) {
+    (void)log2P;
+    lds_fft_t<10, INV>(buf, T);
+}
+
+// The brute grid of a whole turn as a chirp z-transform (round 6).  With
+// L = Ns - 1 and phi_j = lo + j / L, e^{2 pi i k phi_j} = e^{2 pi i k lo}
+// nu^{k^2} nu^{j^2} nu^{-(j-k)^2}, nu = e^{i pi / L}, so
+//   S_j = Re sum_k xm_k e^{2 pi i k phi_j} = Re nu^{j^2} (a * b)_j,
+//   a_k = xm_k e^{2 pi i k lo} nu^{k^2}, b_m = nu^{-m^2}:
+// per chunk of J outputs one P-point circular convolution against the
+// chunk's precomputed FFT_P(b) (k_cz_table), 2 Q block FFTs in all
+// instead of Ns x nharm phasor products.  buf: P double2 of LDS.
+// (inline: out of line, as a function compiled without the kernel's occupancy
+// target, it took 248 VGPRs + spills)
+__device__ __forceinline__ void cz_grid(const double2 *xm, int nharm, double inv_err2, int Ns, double lo,
+                                     double *sh, double2 *buf, const double2 *czB, const double2 *czT, int P,
+                                     int J, int Q, int K) {
+    const int L = Ns - 1;
+    int log2P = 0;
+    while ((1 << log2P) < P) ++log2P;
+    // per chunk: FFT_P(a) (rebuilt: kept in registers it would pin
+    // kMaxFftN / kBlock complex values per thread), times the chunk's
+    // FFT_P(b), inverse, the chunk's outputs
+    for (int q = 0; q < Q; ++q) {
+        for (int k = threadIdx.x; k < P; k += kBlock) {
+            double2 a = cmk(0.0, 0.0);
+            if (k < nharm && k < K) a = cmul(cmul(xm[k], cexp2pi((double)k * lo)), cz_chirp(k, L));
+            buf[k] = a;
+        }
+        __syncthreads();
+        cz_fft<false>(buf, log2P, czT);
+        __syncthreads();
+        const double2 *Bq = czB + (int64_t)q * P;
+        for (int t = threadIdx.x; t < P; t += kBlock) buf[t] = cmul(buf[t], Bq[t]);
+        __syncthreads();
+        cz_fft<true>(buf, log2P, czT);
+        __syncthreads();
+        for (int t = threadIdx.x; t < J; t += kBlock) {
+            const int j = q * J + t;
+            if (j < Ns) {
+                const double2 c = buf[t + K - 1];
+                const double2 w = cz_chirp(j, L);
+                sh[j] = -(c.x * w.x - c.y * w.y) * inv_err2;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// FFT_P of each chunk's chirp kernel b'_t = nu^{-(t + qJ - (K-1))^2}
+// (t < K + J - 1; 0 past), scaled by 1/P: one block per chunk
+__global__ __launch_bounds__(kBlock) void k_cz_table(CzPlan c, double2 *B, const double2 *T) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int q = blockIdx.x;
+    const int L = c.Ns - 1;
+    for (int t = threadIdx.x; t < c.P; t += kBlock) {
+        double2 b = cmk(0.0, 0.0);
+        if (t < c.K + c.J - 1) b = cconj(cz_chirp(t + q * c.J - (c.K - 1), L));
+        lds[t] = b;
+    }
+    __syncthreads();
+    int log2P = 0;
+    while ((1 << log2P) < c.P) ++log2P;
+    cz_fft<false>(lds, log2P, T);
+    __syncthreads();
+    for (int t = threadIdx.x; t < c.P; t += kBlock) B[(int64_t)q * c.P + t] = cscale(lds[t], 1.0 / (double)c.P);
+}
+
+hipError_t launch_cz_table(const CzPlan &c, double2 *B, const double2 *T, hipStream_t st) {
+    hipLaunchKernelGGL(k_cz_table, dim3((unsigned)c.Q), dim3(kBlock), sizeof(double2) * (size_t)c.P, st, c, B, T);
+    return hipGetLastError();
+}
+
+// grid_done: sh[0..Ns) already holds the grid (cz_grid)
 __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int Ns, double lo,
-                             double hi, double *sh /*LDS >= 2*Ns+8*/, double *fval, int *nfev) {
+                             double hi, double *sh /*LDS >= 2*Ns+8*/, double *fval, int *nfev,
+                             bool grid_done = false) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double step = (Ns != 1) ? (hi - lo) / (double)(Ns - 1) : 1.0;
 #ifndef PPF_GUESS_DIAG
@@ -304,6 +397,7 @@ __device__ double brute_fmin(const double2 *xm, int nharm, double inv_err2, int 
 #endif
     if (PPF_GUESS_DIAG & 1) {
         for (int j = threadIdx.x; j < Ns; j += kBlock) sh[j] = (double)j;
+    } else if (grid_done) {
     } else if (Ns >= 2 * kBlock) {
         // large grids (ppalign: Ns = nbin): one point per lane, two points
         // in flight; harmonics broadcast from LDS, phasor e^{2 pi i k ph} by
@@ -794,12 +888,13 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 // ===========================================================================
 template <bool MX>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
-    // lds: z[rfft_len] (packed profile, FFT in place) | xm[N+1] | sh[Ns+8]
+    // lds: z[max(rfft_len, czP)] (packed profile, FFT in place; then the
+    // chirp z-transform's buffer) | xm[N+1] | sh[Ns+8]
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const int N = a.nbin >> 1, nharm = N + 1, s = blockIdx.x, tid = threadIdx.x;
     const bool odd = a.nbin & 1;
-    double2 *z = lds, *xm = lds + rfft_len(a.nbin);
+    double2 *z = lds, *xm = lds + (a.czB && a.czP > rfft_len(a.nbin) ? a.czP : rfft_len(a.nbin));
     double *sh = reinterpret_cast<double *>(xm + nharm + 1);
     // fused (k_xspec_w accumulated the guess spectrum of its rows in the
     // Fourier domain): the block partials of the covered harmonics
@@ -903,8 +998,11 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
     // fused: the profile's expected noise, sqrt(sum w^2 errs_FT^2) / W
     const double err = fused ? sqrt(sh[2]) / wsum : sig * sqrt((double)a.nbin / 2.0);
+    if (a.czB && !(PPF_GUESS_DIAG & 1))
+        cz_grid(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, sh, z, a.czB, a.czT, a.czP, a.czJ, a.czQ,
+                a.czK);
     const double phase = brute_fmin(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
-                                    nullptr);
+                                    nullptr, a.czB != nullptr);
     // nu_mean of the usable channels (block reduction: 16384-channel
     // portraits made a serial loop here cost ~0.2 ms per sub-int)
     double nv[2] = {0.0, 0.0};
@@ -1516,7 +1614,8 @@ hipError_t launch_dsum(const DsumArgs &a_in, hipStream_t st) {
 }
 
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
-    size_t lds = (size_t)(rfft_len(a.nbin) + a.nbin / 2 + 2) * sizeof(double2) +
+    const int zs = (a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin);
+    size_t lds = (size_t)(zs + a.nbin / 2 + 2) * sizeof(double2) +
                  (size_t)(a.Ns + 8) * sizeof(double);
     if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_guess<false>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_guess<true>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);

@@ -295,10 +295,11 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     if flags_t.numel() == 5:
         flags_t = flags_t.repeat(nsub)
     flags_t = flags_t.reshape(nsub, 5).contiguous()
-    nan3 = torch.full((nsub, 3), float("nan"), dtype=f64, device=dev)
-    nu_fits_t = nan3.clone() if nu_fits is None else \
+    def nan3():
+        return torch.full((nsub, 3), float("nan"), dtype=f64, device=dev)
+    nu_fits_t = nan3() if nu_fits is None else \
         to_dev(nu_fits, dev, f64).reshape(nsub, 3).contiguous()
-    nu_outs_t = nan3.clone() if nu_outs is None else \
+    nu_outs_t = nan3() if nu_outs is None else \
         to_dev(nu_outs, dev, f64).reshape(nsub, 3).contiguous()
     errs_t = None if errs is None else \
         to_dev(errs, dev, f64).reshape(nsub, nchan).contiguous()

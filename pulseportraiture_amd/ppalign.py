@@ -251,7 +251,13 @@ class _Rows(object):
 def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     """One batched ppf_fit_batch of `rows` (guess + phase[/DM] fit), the
     reference's exceptions raised for failed sub-ints."""
-    flags = [1, int(bool(fit_dm)), 0, 0, 0]
+    # the flags stay resident with the rows' other inputs (a host list would
+    # be staged and copied in every iteration)
+    key = "flags%d" % int(bool(fit_dm))
+    if key not in dc:
+        dc[key] = torch.tensor([1, int(bool(fit_dm)), 0, 0, 0],
+                               dtype=torch.int32, device=dev)
+    flags = dc[key]
     # no scattering and a zero initial tau (init holds only the DM): no
     # sub-int streams the cross spectrum -- known on the host, so fit_batch
     # need not read the device-resident init back to count them
@@ -266,9 +272,18 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     r = res["results"]
     dc["last_results"] = r               # (diagnostics: bench.py --fit align)
     # the status bits are checked by raise_pending() once the iteration's
-    # rotate-and-sum is queued (the read-back is the iteration's one host
-    # sync; here it would idle the device while the host queued the rest)
-    dc.setdefault("_pending", []).append(r[:, I["status"]].to(torch.int64))
+    # rotate-and-sum is queued.  They travel to pinned host memory as soon
+    # as the fit has written them, behind an event, so the check waits for
+    # the fit only -- not for the rotate-and-sum queued after it, during
+    # which the host queues the next iteration (round 6: a .cpu() here
+    # waited for the whole queue and left the device idle while the host
+    # set up the next iteration, ~0.3 ms of a 3-ms C4 iteration)
+    st = r[:, I["status"]]
+    hs = torch.empty(st.shape, dtype=st.dtype, pin_memory=True)
+    hs.copy_(st, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    dc.setdefault("_pending", []).append((hs, ev))
     phi = r[:, I["params"]][:, 0]
     DM = r[:, I["params"]][:, 1]
     nu_ref = r[:, I["nu_out"]][:, 0]
@@ -296,8 +311,9 @@ def raise_pending(R):
         if not dc or not dc.get("_pending"):
             continue
         sts, dc["_pending"] = dc["_pending"], []
-        for st in sts:
-            st = st.cpu().numpy()
+        for hs, ev in sts:
+            ev.synchronize()
+            st = hs.numpy().astype(np.int64)
             bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR |
                                  _lib.ST_NOSPACE))[0]
             if len(bad):

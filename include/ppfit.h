@@ -309,6 +309,20 @@ int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin,
                     const double *weights, double *out, double *wsum,
                     void *workspace, size_t workspace_bytes, void *stream);
 
+/* ppalign's per-row rotation phases and weights from a fit (ppalign.py:
+ * 222-247; round 6, ABI 6): for sub-int s, channel n with mask[s][n] != 0
+ *   phases[s][n]  = phi_s + Dconst DM_s / P_s (freqs[s][n]^-2 - nu_DM,s^-2)
+ *   weights[s][n] = scales[s][n] / errs[s][n]^2
+ * and 0 where masked; phi, DM, nu_DM from results[s] (ppf_result: params[0],
+ * params[1], nu_out[0]).  One launch instead of the dozen elementwise
+ * operations it replaces in each ppalign iteration.  results: [nsub]
+ * ppf_result; freqs, scales, errs, phases, weights: [nsub][nchan]; P:
+ * [nsub]; mask: [nsub][nchan] or NULL (all used). */
+int ppf_align_phases(ppf_ctx *ctx, int32_t nsub, int32_t nchan, const double *results,
+                     const double *freqs, const double *P, const uint8_t *mask,
+                     const double *scales, const double *errs, double *phases,
+                     double *weights, void *stream);
+
 /* Channel reduced chi^2 of a fit (pptoas.get_channels_to_zap,
  * pptoas.py:1266-1343, through show_fit 1375-1480 and get_red_chi2
  * pplib.py:754-779): for each row r,

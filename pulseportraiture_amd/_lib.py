@@ -101,6 +101,8 @@ SIGNATURES = {
     "ppf_resid_chi2_batch": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _i32,
                                             _vp, _vp, _vp, _vp, _vp, _vp,
                                             ctypes.c_double, _vp, _vp]),
+    "ppf_align_phases": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _vp, _vp]),
     "ppf_align_workspace_bytes": (ctypes.c_size_t, [_i32, _i32, _i32]),
     "ppf_align_accum": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i32, _vp, _vp,
                                        _vp, _vp, _vp, _vp, ctypes.c_size_t,

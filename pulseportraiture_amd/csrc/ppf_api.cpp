@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -120,16 +122,54 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
     return PPF_OK;
 }
 
+// A small device -> pinned-host read-back the iteration loop waits on (round
+// 6).  hipStreamSynchronize wakes the host 30-70 us after the copy lands
+// (C4's kernel trace: the gaps before the re-centring k_xmom_g and before
+// k_postfit); the words are instead preset to a sentinel no count takes and
+// polled until the copy has overwritten them, with the stream
+// synchronisation as the fallback after 2 s (and for any copy error).
+#ifndef PPF_SPIN_WAIT
+#define PPF_SPIN_WAIT 1
+#endif
+constexpr unsigned kUnset = 0xFFFFFFFFu;
+int read_back(ppf_ctx *ctx, unsigned *host, const unsigned *dev, int n, hipStream_t st) {
+    volatile unsigned *h = host;
+    for (int i = 0; i < n; ++i) h[i] = kUnset;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    hipError_t e = hipMemcpyAsync(host, dev, n * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync");
+    if (PPF_SPIN_WAIT) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            bool done = true;
+            for (int i = 0; i < n; ++i) done = done && h[i] != kUnset;
+            if (done) {
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                return PPF_OK;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+    return PPF_OK;
+}
+
 // The guess's brute grid of a whole turn with Ns >= 512 points (ppalign:
 // Ns = nbin) as a chirp z-transform (k_guess, round 6): the plan and its
 // cached kernel tables.  Returns false (direct sums) where it does not apply.
+// (Round 6, first build: P was taken >= 2K - 1 = 1025, i.e. 2048, which
+// cz_fft refuses, so the A/B of ab_czc4_status.txt ran the direct sums on
+// both sides.)
 #ifndef PPF_GUESS_CZ
 #define PPF_GUESS_CZ 1
 #endif
 bool cz_plan(int Ns, int K, ppf::CzPlan &c) {
     if (!PPF_GUESS_CZ || Ns < 2 * ppf::kBlock || K < 2) return false;
+    // P >= K + J - 1 with chunks of J >= 256 outputs (nbin 1024: K = 513,
+    // P = 1024, two chunks of 512)
     int P = 64;
-    while (P < 2 * K - 1) P *= 2;
+    while (P < K + 255) P *= 2;
     if (P != 1024) return false;                 // cz_fft's size (nbin 1024)
     c.Ns = Ns; c.K = K; c.P = P; c.J = P - K + 1; c.Q = (Ns + c.J - 1) / c.J;
     return true;
@@ -647,10 +687,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // nothing left to fit exit at once
     bool any_mom = true, any_pass = false;
     if (!((d->options & PPF_OPT_NO_X) && sa.moments)) {
-        if ((e = hipMemcpyAsync(ctx->host_active + 1, sa.kinds, 2 * sizeof(unsigned), hipMemcpyDeviceToHost,
-                                st)) != hipSuccess)
-            return hip_fail(ctx, e, "hipMemcpyAsync");
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+        if ((rc = read_back(ctx, ctx->host_active + 1, sa.kinds, 2, st))) return rc;
         any_mom = ctx->host_active[1] != 0;
         any_pass = ctx->host_active[2] != 0;
     }
@@ -739,10 +776,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             }
         }
         iter += group;
-        if ((e = hipMemcpyAsync(ctx->host_active, sa.active, sizeof(unsigned), hipMemcpyDeviceToHost,
-                                st)) != hipSuccess)
-            return hip_fail(ctx, e, "hipMemcpyAsync");
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+        if ((rc = read_back(ctx, ctx->host_active, sa.active, 1, st))) return rc;
         if (*ctx->host_active == 0 || iter > maxiter + 2) break;
     }
     {
@@ -800,6 +834,22 @@ size_t ppf_align_workspace_bytes(int32_t nsub, int32_t nchan, int32_t nbin) {
     const size_t g = (size_t)ppf::align_groups(nsub, nchan);
     return align256(g * nchan * (size_t)(nbin / 2 + 1) * sizeof(double2)) +
            align256(g * nchan * sizeof(double));
+}
+
+int ppf_align_phases(ppf_ctx *ctx, int32_t nsub, int32_t nchan, const double *results, const double *freqs,
+                     const double *P, const uint8_t *mask, const double *scales, const double *errs,
+                     double *phases, double *weights, void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nsub < 0 || nchan <= 0) return fail(ctx, PPF_EINVAL, "bad align shape");
+    if (nsub == 0) return PPF_OK;
+    if (!results || !freqs || !P || !scales || !errs || !phases || !weights)
+        return fail(ctx, PPF_EINVAL, "null align_phases argument");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    if ((e = ppf::launch_align_phases(nsub, nchan, results, freqs, P, mask, scales, errs, phases, weights,
+                                      (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(ctx, e, "k_align_phases");
+    return PPF_OK;
 }
 
 int ppf_align_accum(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nbin, int32_t in_dtype,

@@ -117,7 +117,7 @@ struct GuessArgs {
 
 // chirp z-transform plan of a whole-turn brute grid (k_guess): Kmax
 // harmonics, Ns points over [lo, lo + 1], outputs in Q chunks of J points,
-// P-point transforms (P = pow2 >= 2 Kmax - 1, J = P - Kmax + 1)
+// P-point transforms (P = pow2 >= Kmax + 255, J = P - Kmax + 1)
 struct CzPlan {
     int Ns, K, P, J, Q;
 };
@@ -193,7 +193,10 @@ struct AlignArgs {
 int align_groups(int nsub, int nchan);
 hipError_t launch_align(const AlignArgs &a, hipStream_t st);
 bool align_wave_supported(int log2N);                                   // nbin 256..2048
-hipError_t launch_align_part_w(const AlignArgs &a, hipStream_t st);     // wave-per-row partials
+hipError_t launch_align_part_w(const AlignArgs &a, hipStream_t st);
+hipError_t launch_align_phases(int nsub, int nchan, const double *results, const double *freqs, const double *P,
+                               const uint8_t *mask, const double *scales, const double *errs, double *phases,
+                               double *weights, hipStream_t st);     // wave-per-row partials
 
 // per-row reduced chi^2 of (rotated data - scale * model) (the channel test
 // of pptoas.get_channels_to_zap, pptoas.py:1266-1343 via show_fit 1375-1480)

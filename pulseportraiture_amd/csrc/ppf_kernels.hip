@@ -1613,6 +1613,33 @@ hipError_t launch_dsum(const DsumArgs &a_in, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ppalign's rotation phases and weights (ppf_align_phases, ppalign.py:
+// 222-247): a thread per (sub-int, channel)
+__global__ __launch_bounds__(kBlock) void k_align_phases(int nsub, int nchan, const double *results,
+                                                         const double *freqs, const double *P,
+                                                         const uint8_t *mask, const double *scales,
+                                                         const double *errs, double *phases, double *weights) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (int64_t)nsub * nchan) return;
+    const int64_t s = i / nchan;
+    const double *r = results + s * (int64_t)(sizeof(ppf_result) / sizeof(double));
+    const double phi = r[offsetof(ppf_result, params) / sizeof(double)];
+    const double DM = r[offsetof(ppf_result, params) / sizeof(double) + 1];
+    const double nu_ref = r[offsetof(ppf_result, nu_out) / sizeof(double)];
+    const bool ok = !mask || mask[i];
+    phases[i] = ok ? phi + kDconst * DM / P[s] * (pow(freqs[i], -2.0) - pow(nu_ref, -2.0)) : 0.0;
+    weights[i] = ok ? scales[i] / (errs[i] * errs[i]) : 0.0;
+}
+
+hipError_t launch_align_phases(int nsub, int nchan, const double *results, const double *freqs, const double *P,
+                               const uint8_t *mask, const double *scales, const double *errs, double *phases,
+                               double *weights, hipStream_t st) {
+    const int64_t n = (int64_t)nsub * nchan;
+    hipLaunchKernelGGL(k_align_phases, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, nsub,
+                       nchan, results, freqs, P, mask, scales, errs, phases, weights);
+    return hipGetLastError();
+}
+
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
     const int zs = (a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin);
     size_t lds = (size_t)(zs + a.nbin / 2 + 2) * sizeof(double2) +

@@ -522,6 +522,27 @@ def align_accum(data, phases, weights, out, wsum, dev=None):
     return out, wsum
 
 
+def align_phases(results, freqs, P, mask, scales, errs, dev=None):
+    """ppalign's per-row rotation phases and weights from fit results
+    (ppf_align_phases, ppalign.py:222-247): device tensors results [nsub,
+    32], freqs / scales / errs [nsub, nchan] float64, P [nsub], mask [nsub,
+    nchan] uint8 (or None) -> (phases, weights) [nsub, nchan] float64."""
+    dev = device(dev)
+    nsub, nchan = freqs.shape
+    for t in (results, freqs, P, scales, errs):
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError("align_phases takes contiguous float64 tensors")
+    ph = torch.empty((nsub, nchan), dtype=torch.float64, device=dev)
+    wt = torch.empty((nsub, nchan), dtype=torch.float64, device=dev)
+    ctx = _lib.context(dev.index)
+    rc = _lib.load().ppf_align_phases(
+        ctx, nsub, nchan, _p(results), _p(freqs), _p(P),
+        None if mask is None else _p(mask), _p(scales), _p(errs), _p(ph),
+        _p(wt), _stream(dev))
+    _lib.check(rc, ctx)
+    return ph, wt
+
+
 def resid_chi2_rows(rows, phases, model_rows, model_index, scales, errs, dof,
                     dev=None):
     """Per row: sum_t (rotate(row, phase) - scale * model_rows[index])^2 /

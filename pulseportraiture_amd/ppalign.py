@@ -284,21 +284,11 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     dc.setdefault("_pending", []).append((hs, ev))
-    phi = r[:, I["params"]][:, 0]
-    DM = r[:, I["params"]][:, 1]
-    nu_ref = r[:, I["nu_out"]][:, 0]
-    # the iteration-invariant factors once per batch of rows (each torch op
-    # is a launch and a Python round trip in every ppalign iteration)
-    if "ok" not in dc:
-        dc["ok"] = dc["mask"] != 0
-        dc["f2"] = dc["freqs"] ** -2.0
-        dc["e2"] = dc["errs"] ** 2
-        dc["zero"] = torch.zeros((), dtype=torch.float64, device=dev)
-    ok, zero = dc["ok"], dc["zero"]
-    ph = phi[:, None] + (Dconst * DM / dc["P"])[:, None] * (
-        dc["f2"] - (nu_ref ** -2.0)[:, None])
-    ph = torch.where(ok, ph, zero)
-    wt = torch.where(ok, res["scales"] / dc["e2"], zero)
+    # phases and weights in one launch (ppf_align_phases; the elementwise
+    # torch form was a dozen launches and Python round trips per iteration
+    # while the device waited for them)
+    ph, wt = engine.align_phases(r, dc["freqs"], dc["P"], dc["mask"],
+                                 res["scales"], dc["errs"], dev)
     return ph, wt
 
 

@@ -170,7 +170,7 @@ bool cz_plan(int Ns, int K, ppf::CzPlan &c) {
     // P = 1024, two chunks of 512)
     int P = 64;
     while (P < K + 255) P *= 2;
-    if (P != 1024) return false;                 // cz_fft's size (nbin 1024)
+    if (P < 512 || P > 2048) return false;       // k_guess's instantiations (nbin 512-2048)
     c.Ns = Ns; c.K = K; c.P = P; c.J = P - K + 1; c.Q = (Ns + c.J - 1) / c.J;
     return true;
 }

@@ -306,15 +306,14 @@ __device__ __forceinline__ double2 cz_chirp(int m, int L) {
     return cmk(c, s);
 }
 
-// the chirp z-transform's P-point FFTs, P = 1024 (nbin 1024, ppalign's
-// configs[3]): the compile-time-size Stockham passes, one radix-4 butterfly
-// per thread.  The runtime-size lds_fft (four), a 2048-point case (two) and
-// even a second 512-point instantiation each took k_guess from four waves
-// per SIMD to two or three, so other sizes keep the direct sums.
-template <bool INV>
-__device__ __forceinline__ void cz_fft(double2 *buf, int log2P, const double2 *T) {
-    (void)log2P;
-    lds_fft_t<10, INV>(buf, T);
+// the chirp z-transform's P-point FFTs: the compile-time-size Stockham
+// passes, a k_guess instantiation per size (CZL = log2 P: 9, 10, 11 for
+// nbin 512, 1024, 2048).  In one kernel beside each other (or as the
+// runtime-size lds_fft) they took k_guess from four waves per SIMD to three
+// or two; alone, the 1024-point one keeps it at four.
+template <int CZL, bool INV>
+__device__ __forceinline__ void cz_fft(double2 *buf, const double2 *T) {
+    lds_fft_t<CZL, INV>(buf, T);
 }
 
 // The brute grid of a whole turn as a chirp z-transform (round 6).  With
@@ -327,12 +326,12 @@ __device__ __forceinline__ void cz_fft(double2 *buf, int log2P, const double2 *T
 // instead of Ns x nharm phasor products.  buf: P double2 of LDS.
 // (inline: out of line, as a function compiled without the kernel's occupancy
 // target, it took 248 VGPRs + spills)
+template <int CZL>
 __device__ __forceinline__ void cz_grid(const double2 *xm, int nharm, double inv_err2, int Ns, double lo,
-                                     double *sh, double2 *buf, const double2 *czB, const double2 *czT, int P,
-                                     int J, int Q, int K) {
+                                     double *sh, double2 *buf, const double2 *czB, const double2 *czT, int J,
+                                     int Q, int K) {
+    constexpr int P = 1 << CZL;
     const int L = Ns - 1;
-    int log2P = 0;
-    while ((1 << log2P) < P) ++log2P;
     // per chunk: FFT_P(a) (rebuilt: kept in registers it would pin
     // kMaxFftN / kBlock complex values per thread), times the chunk's
     // FFT_P(b), inverse, the chunk's outputs
@@ -343,12 +342,12 @@ __device__ __forceinline__ void cz_grid(const double2 *xm, int nharm, double inv
             buf[k] = a;
         }
         __syncthreads();
-        cz_fft<false>(buf, log2P, czT);
+        cz_fft<CZL, false>(buf, czT);
         __syncthreads();
         const double2 *Bq = czB + (int64_t)q * P;
         for (int t = threadIdx.x; t < P; t += kBlock) buf[t] = cmul(buf[t], Bq[t]);
         __syncthreads();
-        cz_fft<true>(buf, log2P, czT);
+        cz_fft<CZL, true>(buf, czT);
         __syncthreads();
         for (int t = threadIdx.x; t < J; t += kBlock) {
             const int j = q * J + t;
@@ -376,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_cz_table(CzPlan c, double2 *B, const
     __syncthreads();
     int log2P = 0;
     while ((1 << log2P) < c.P) ++log2P;
-    cz_fft<false>(lds, log2P, T);
+    lds_fft(lds, log2P, T, false);
     __syncthreads();
     for (int t = threadIdx.x; t < c.P; t += kBlock) B[(int64_t)q * c.P + t] = cscale(lds[t], 1.0 / (double)c.P);
 }
@@ -886,7 +885,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
 // ===========================================================================
-template <bool MX>
+template <bool MX, int CZL = 0>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // lds: z[max(rfft_len, czP)] (packed profile, FFT in place; then the
     // chirp z-transform's buffer) | xm[N+1] | sh[Ns+8]
@@ -998,11 +997,13 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const double sig = sqrt(pw[0] / (double)(nharm - a.kc) / (double)a.nbin);
     // fused: the profile's expected noise, sqrt(sum w^2 errs_FT^2) / W
     const double err = fused ? sqrt(sh[2]) / wsum : sig * sqrt((double)a.nbin / 2.0);
-    if (a.czB && !(PPF_GUESS_DIAG & 1))
-        cz_grid(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, sh, z, a.czB, a.czT, a.czP, a.czJ, a.czQ,
-                a.czK);
+    if constexpr (CZL > 0) {
+        if (!(PPF_GUESS_DIAG & 1))
+            cz_grid<CZL>(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, sh, z, a.czB, a.czT, a.czJ, a.czQ,
+                         a.czK);
+    }
     const double phase = brute_fmin(xm, (int)kmx[0], 1.0 / (err * err), a.Ns, -0.5, 0.5, sh, nullptr,
-                                    nullptr, a.czB != nullptr);
+                                    nullptr, CZL > 0);
     // nu_mean of the usable channels (block reduction: 16384-channel
     // portraits made a serial loop here cost ~0.2 ms per sub-int)
     double nv[2] = {0.0, 0.0};
@@ -1644,8 +1645,19 @@ hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
     const int zs = (a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin);
     size_t lds = (size_t)(zs + a.nbin / 2 + 2) * sizeof(double2) +
                  (size_t)(a.Ns + 8) * sizeof(double);
-    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_guess<false>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
-    else hipLaunchKernelGGL(k_guess<true>, dim3((unsigned)a.nsub), dim3(kBlock), lds, st, a);
+    const dim3 g((unsigned)a.nsub), b(kBlock);
+    if (a.czB && is_pow2(rfft_len(a.nbin))) {
+        switch (a.czP) {
+            case 512: hipLaunchKernelGGL((k_guess<false, 9>), g, b, lds, st, a); break;
+            case 1024: hipLaunchKernelGGL((k_guess<false, 10>), g, b, lds, st, a); break;
+            case 2048: hipLaunchKernelGGL((k_guess<false, 11>), g, b, lds, st, a); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else if (is_pow2(rfft_len(a.nbin))) {
+        hipLaunchKernelGGL((k_guess<false, 0>), g, b, lds, st, a);
+    } else {
+        hipLaunchKernelGGL((k_guess<true, 0>), g, b, lds, st, a);
+    }
     return hipGetLastError();
 }
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {

@@ -25,6 +25,8 @@ args_of() {
     c3) echo "--fit full --nsub 10000 --steps 3 --warmup 1 --cpu-sample 0";;
     c5) echo "--fit scat --nchan 16384 --nbin 1024 --nsub 500 --steps 3 --warmup 1 --cpu-sample 0";;
     c4) echo "--fit align --nsub 1000 --nchan 256 --nbin 1024 --steps 50 --warmup 5 --cpu-sample 0";;
+    c4n512) echo "--fit align --nsub 1000 --nchan 256 --nbin 512 --steps 50 --warmup 5 --cpu-sample 0";;
+    c4n2048) echo "--fit align --nsub 1000 --nchan 256 --nbin 2048 --steps 50 --warmup 5 --cpu-sample 0";;
     gtps) echo "--fit gettoas --psrfits --steps 4 --warmup 1";;
     gt) echo "--fit gettoas --steps 3 --warmup 1";;
     nb1000) echo "--nbin 1000 --nsub 4000 --steps 3 --warmup 1 --cpu-sample 0";;

@@ -13,6 +13,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -147,8 +148,12 @@ int read_back(ppf_ctx *ctx, unsigned *host, const unsigned *dev, int n, hipStrea
                 std::atomic_thread_fence(std::memory_order_seq_cst);
                 return PPF_OK;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
-            __builtin_ia32_pause();
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::seconds(2)) break;
+            // past the first 50 us the core is offered to other host threads
+            // between polls (GetTOAs' readers and stagers share the CPUs)
+            if (dt > std::chrono::microseconds(50)) std::this_thread::yield();
+            else __builtin_ia32_pause();
         }
     }
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");

@@ -116,8 +116,16 @@ enum ppf_option {
                                 PPF_OPT_FUSED_MOM) where the GetTOAs guess
                                 rides along in the spectrum pass: guess != 0
                                 and nbin = 2048 */
-    PPF_OPT_FUSED_MOM = 16   /* force the fused k_xmom_g pass (no X for the
+    PPF_OPT_FUSED_MOM = 16,  /* force the fused k_xmom_g pass (no X for the
                                 phase/DM/GM fits) */
+    PPF_OPT_SPIN_WAIT = 32   /* (ABI 6) the call's read-backs of the count
+                                of fits still iterating are polled on the
+                                host instead of waited for with
+                                hipStreamSynchronize: 30-70 us less per
+                                read-back, for a caller with no host threads
+                                of its own competing for the cores (ppalign:
+                                C4 +2-3 %; GetTOAs' readers and stagers lost
+                                up to 20 % to it) */
 };
 
 enum ppf_mode {

@@ -25,6 +25,7 @@ OPT_NO_X = 2
 OPT_SCIPY_TR = 4          # scattering fits follow scipy's trust-ncg path
 OPT_MOM_X = 8             # phase/DM/GM fits: moments from the stored cross spectrum
 OPT_FUSED_MOM = 16        # ... from the fused k_xmom_g pass (no X)
+OPT_SPIN_WAIT = 32        # poll the iteration loop's read-backs (ppalign)
 ABI_VERSION = 6
 
 # ppf_result: 32 doubles (include/ppfit.h)

@@ -126,20 +126,22 @@ int twiddles(ppf_ctx *ctx, int nbin, hipStream_t st, const double2 **T, const do
 // A small device -> pinned-host read-back the iteration loop waits on (round
 // 6).  hipStreamSynchronize wakes the host 30-70 us after the copy lands
 // (C4's kernel trace: the gaps before the re-centring k_xmom_g and before
-// k_postfit); the words are instead preset to a sentinel no count takes and
-// polled until the copy has overwritten them, with the stream
-// synchronisation as the fallback after 2 s (and for any copy error).
+// k_postfit); with PPF_OPT_SPIN_WAIT the words are instead preset to a
+// sentinel no count takes and polled until the copy has overwritten them,
+// with the stream synchronisation as the fallback after 2 s.  Opt-in: on
+// GetTOAs' threaded host pipeline the polling cost 20 % of the PSRFITS rate
+// even yielding the core (profiles/r06/ab_gtspin_status.txt).
 #ifndef PPF_SPIN_WAIT
 #define PPF_SPIN_WAIT 1
 #endif
 constexpr unsigned kUnset = 0xFFFFFFFFu;
-int read_back(ppf_ctx *ctx, unsigned *host, const unsigned *dev, int n, hipStream_t st) {
+int read_back(ppf_ctx *ctx, unsigned *host, const unsigned *dev, int n, hipStream_t st, bool spin) {
     volatile unsigned *h = host;
     for (int i = 0; i < n; ++i) h[i] = kUnset;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     hipError_t e = hipMemcpyAsync(host, dev, n * sizeof(unsigned), hipMemcpyDeviceToHost, st);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync");
-    if (PPF_SPIN_WAIT) {
+    if (PPF_SPIN_WAIT && spin) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
             bool done = true;
@@ -692,7 +694,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     // nothing left to fit exit at once
     bool any_mom = true, any_pass = false;
     if (!((d->options & PPF_OPT_NO_X) && sa.moments)) {
-        if ((rc = read_back(ctx, ctx->host_active + 1, sa.kinds, 2, st))) return rc;
+        if ((rc = read_back(ctx, ctx->host_active + 1, sa.kinds, 2, st, d->options & PPF_OPT_SPIN_WAIT))) return rc;
         any_mom = ctx->host_active[1] != 0;
         any_pass = ctx->host_active[2] != 0;
     }
@@ -781,7 +783,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             }
         }
         iter += group;
-        if ((rc = read_back(ctx, ctx->host_active, sa.active, 1, st))) return rc;
+        if ((rc = read_back(ctx, ctx->host_active, sa.active, 1, st, d->options & PPF_OPT_SPIN_WAIT))) return rc;
         if (*ctx->host_active == 0 || iter > maxiter + 2) break;
     }
     {

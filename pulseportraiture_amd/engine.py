@@ -209,7 +209,7 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
               max_iter=0, guess=False, guess_weights=None, guess_DM=None,
               guess_Ns=100, guess_tau=None, dev=None, workspace=None,
               n_x=None, no_hcut=False, max_workspace=None, guess_ref=0,
-              bounds=None, solver=None, mom_x=None):
+              bounds=None, solver=None, mom_x=None, spin_wait=False):
     """Fit nsub sub-integrations: data [nsub, nchan, nbin] (f32 or f64),
     model [nmodel, nchan, nbin] (or [nchan, nbin]), freqs [nsub, nchan],
     P [nsub], init [nsub, 5], fit_flags [nsub, 5] (or [5]).
@@ -229,6 +229,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
     spectrum (True, PPF_OPT_MOM_X) or from the fused pass (False,
     PPF_OPT_FUSED_MOM); None = MOM_X (env PPF_MOM_X; unset: the library
     chooses).
+    spin_wait: poll the read-backs of the iteration loop on the host
+    (PPF_OPT_SPIN_WAIT) -- for callers with no host threads of their own.
     max_workspace: workspace budget in bytes (default
     half the free device memory); a batch needing more is fitted in
     consecutive chunks of sub-ints (a sub-int's result does not depend on
@@ -336,7 +338,8 @@ def fit_batch(data, model, freqs, P, init, fit_flags, nu_fits=None,
                is_toa=is_toa, mode=mode, max_iter=max_iter, guess=guess,
                guess_Ns=guess_Ns, no_hcut=no_hcut, guess_ref=guess_ref,
                solver=_solver(solver),
-               mom_x=MOM_X if mom_x is None else bool(mom_x))
+               mom_x=MOM_X if mom_x is None else bool(mom_x),
+               spin_wait=bool(spin_wait))
     lib = _lib.load()
     d0 = _desc(per_sub, 0, nsub, n_x, cfg)
     need = _desc_workspace_bytes(lib, d0)
@@ -407,7 +410,8 @@ def _desc(per_sub, c0, c1, n_x, cfg):
         (_lib.OPT_NO_X if n_x == 0 else 0) | \
         (_lib.OPT_SCIPY_TR if cfg.get("solver") == "scipy" else 0) | \
         (_lib.OPT_MOM_X if cfg.get("mom_x") is True else 0) | \
-        (_lib.OPT_FUSED_MOM if cfg.get("mom_x") is False else 0)
+        (_lib.OPT_FUSED_MOM if cfg.get("mom_x") is False else 0) | \
+        (_lib.OPT_SPIN_WAIT if cfg.get("spin_wait") else 0)
     d.guess_ref = int(cfg["guess_ref"])
     d.bounds = pp(per_sub["bounds"])
     return d

@@ -267,7 +267,7 @@ def _fit_rows(rows, model, mi, dc, fit_dm, nbin, dev):
         chan_mask=dc["mask"], model_index=mi, log10_tau=False, is_toa=True,
         guess=True, guess_weights=dc["gw"], guess_DM=dc["DM"],
         guess_Ns=nbin, dev=dev, guess_ref=1,   # ppalign.py:214-219: at nu_fit
-        n_x=0)
+        n_x=0, spin_wait=True)
     I = _lib.RESULT_INDEX
     r = res["results"]
     dc["last_results"] = r               # (diagnostics: bench.py --fit align)
@@ -302,7 +302,8 @@ def raise_pending(R):
             continue
         sts, dc["_pending"] = dc["_pending"], []
         for hs, ev in sts:
-            ev.synchronize()
+            if ev is not None:           # (None: host-resident already)
+                ev.synchronize()
             st = hs.numpy().astype(np.int64)
             bad = np.where(st & (_lib.ST_NO_ROOT | _lib.ST_SINGULAR |
                                  _lib.ST_NOSPACE))[0]

@@ -1,5 +1,6 @@
 """Host-side logic of the drop-in layer that runs without a GPU: ppalign's
-deferred status check (the reference's exceptions for failed rows, raised
+deferred status check (round 6: the status column reaches pinned host memory
+behind an event, so the check waits for the fit only) (the reference's exceptions for failed rows, raised
 after the iteration's rotate-and-sum is queued; ppalign.py:222-247 through
 pptoaslib.py:1068-1079)."""
 from types import SimpleNamespace
@@ -12,7 +13,9 @@ from pulseportraiture_amd import _lib, ppalign
 
 
 def _rows(*status):
-    return torch.tensor(status, dtype=torch.int64)
+    # a pending record as _fit_rows queues it: (pinned host copy of the
+    # status column, the event behind which it lands; None: already there)
+    return (torch.tensor(status, dtype=torch.float64), None)
 
 
 def test_raise_pending_clean_rows_pass_and_clear():

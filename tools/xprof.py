@@ -21,7 +21,10 @@ def main():
     get = dll.ppf_debug_xprof
     get.argtypes = [ctypes.c_void_p, ctypes.c_int]
     out = np.zeros(8, dtype=np.uint64)
-    sys.argv = ["bench.py", "--nsub", "2500", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"]
+    # BENCH_ARGS: another workload (e.g. C4: "--fit align --nsub 1000
+    # --nchan 256 --nbin 1024")
+    extra = os.environ.get("BENCH_ARGS", "--nsub 2500").split()
+    sys.argv = ["bench.py"] + extra + ["--steps", "1", "--warmup", "0", "--cpu-sample", "0"]
     import bench
     get(out.ctypes.data, 1)
     bench.main()

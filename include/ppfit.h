@@ -366,6 +366,20 @@ int ppf_noise_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype,
                    const void *in, int32_t frac, double *out, void *workspace,
                    size_t workspace_bytes, void *stream);
 
+/* rotate_data's rotation of rows of ANY length (round 6, ABI 6): rows the
+ * LDS transforms of ppf_rotate_batch do not take (even nbin > 8192, odd
+ * nbin > 4095), as Bluestein transforms both ways (up to 2^23 complex
+ * points).  out[r] = irfft(rfft(in[r]) * exp(2 pi i k phases[r])), nbin
+ * samples, or nbin - 1 at odd nbin with ref_len != 0 (the reference's
+ * length-less irfft, as ppf_rotate_batch_ref).  in: [nrows][nbin]
+ * (in_dtype); phases: [nrows]; out: [nrows][nout] f64; workspace: device
+ * scratch of ppf_rotate_long_workspace_bytes(nrows, nbin, ref_len) bytes
+ * (0: unsupported). */
+size_t ppf_rotate_long_workspace_bytes(int64_t nrows, int64_t nbin, int32_t ref_len);
+int ppf_rotate_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype,
+                    const void *in, const double *phases, double *out, int32_t ref_len,
+                    void *workspace, size_t workspace_bytes, void *stream);
+
 /* Batched 1-D FFTFIT: pplib.fit_phase_shift (pplib.py:2136-2182): brute
  * force over Ns points of [lo, hi] then Nelder-Mead (scipy fmin) polish.
  * data: [nprof][nbin] (in_dtype); model: [nmodel_prof][nbin] double with

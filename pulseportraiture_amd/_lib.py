@@ -94,6 +94,12 @@ SIGNATURES = {
                                             _vp, _vp, _vp, _vp]),
     "ppf_noise_batch": (ctypes.c_int, [_vp, ctypes.c_int64, _i32, _i32, _vp,
                                        _i32, _vp, _vp]),
+    "ppf_rotate_long_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64,
+                                                          ctypes.c_int64,
+                                                          _i32]),
+    "ppf_rotate_long": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64,
+                                       _i32, _vp, _vp, _vp, _i32, _vp,
+                                       ctypes.c_size_t, _vp]),
     "ppf_noise_long_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64,
                                                          ctypes.c_int64]),
     "ppf_noise_long": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64,

@@ -1023,6 +1023,95 @@ int ppf_noise_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype, 
     return PPF_OK;
 }
 
+// ppf_rotate_long's plans and workspace: Bluestein transforms both ways
+namespace {
+bool bluestein_plan(int64_t nbin, int64_t n, bool packed, ppf::LongNoiseArgs &a) {
+    a = ppf::LongNoiseArgs{};
+    a.nbin = nbin; a.n = n; a.packed = packed ? 1 : 0; a.bluestein = 1;
+    int64_t M = 64;
+    while (M < 2 * n - 1) M *= 2;
+    int m = 0;
+    while (((int64_t)1 << m) < M) ++m;
+    if (m > 24) return false;
+    a.M = M; a.log2M = m; a.log2M1 = (m + 1) / 2;
+    a.M1 = (int64_t)1 << a.log2M1; a.M2 = M / a.M1;
+    return true;
+}
+struct RotPlan {
+    ppf::LongRotArgs r;
+    int64_t rows_c;
+    size_t off_Bf, off_Bb, off_A, off_Y, bytes;
+};
+bool rot_plan(int64_t nrows, int64_t nbin, bool ref_len, RotPlan &p) {
+    if (nrows < 0 || nbin < 2) return false;
+    const bool odd = nbin & 1;
+    if (!bluestein_plan(nbin, odd ? nbin : nbin / 2, !odd, p.r.f)) return false;
+    const bool out_even = !odd || ref_len;
+    const int64_t nout = odd && ref_len ? nbin - 1 : nbin;
+    if (!bluestein_plan(nbin, out_even ? nout / 2 : nout, false, p.r.b)) return false;
+    p.r.out_even = out_even ? 1 : 0;
+    p.r.nout = nout;
+    const size_t row_b = (size_t)p.r.f.M * sizeof(double2);     // b.M <= f.M
+    int64_t rc = (int64_t)((size_t)(256u << 20) / (2 * row_b));
+    if (rc < 1) rc = 1;
+    p.rows_c = nrows < rc ? (nrows > 0 ? nrows : 1) : rc;
+    size_t off = 0;
+    p.off_Bf = off; off += align256(2 * row_b);
+    p.off_Bb = off; off += align256(2 * (size_t)p.r.b.M * sizeof(double2));
+    p.off_A = off; off += align256((size_t)p.rows_c * row_b);
+    p.off_Y = off; off += align256((size_t)p.rows_c * row_b);
+    p.bytes = off;
+    return true;
+}
+}  // namespace
+
+size_t ppf_rotate_long_workspace_bytes(int64_t nrows, int64_t nbin, int32_t ref_len) {
+    RotPlan p;
+    return rot_plan(nrows, nbin, ref_len != 0, p) ? p.bytes : 0;
+}
+
+int ppf_rotate_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype, const void *in,
+                    const double *phases, double *out, int32_t ref_len, void *workspace, size_t workspace_bytes,
+                    void *stream) {
+    if (!ctx) return PPF_EINVAL;
+    if (nrows < 0 || nbin < 2 || (nrows > 0 && (!in || !phases || !out)))
+        return fail(ctx, PPF_EINVAL, "bad rotate arguments");
+    if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    RotPlan p;
+    if (!rot_plan(nrows, nbin, ref_len != 0, p))
+        return fail(ctx, PPF_EUNSUP, "nbin=%lld: transform longer than 2^24 points", (long long)nbin);
+    if (nrows == 0) return PPF_OK;
+    if (!workspace || workspace_bytes < p.bytes)
+        return fail(ctx, PPF_EINVAL, "workspace %zu < %zu bytes", workspace_bytes, p.bytes);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t st = (hipStream_t)stream;
+    const double2 *T1f, *T2f, *T1b, *T2b, *unused;
+    int rc;
+    if ((rc = twiddles(ctx, (int)(2 * p.r.f.M1), st, &T1f, &unused))) return rc;
+    if ((rc = twiddles(ctx, (int)(2 * p.r.f.M2), st, &T2f, &unused))) return rc;
+    if ((rc = twiddles(ctx, (int)(2 * p.r.b.M1), st, &T1b, &unused))) return rc;
+    if ((rc = twiddles(ctx, (int)(2 * p.r.b.M2), st, &T2b, &unused))) return rc;
+    char *ws = (char *)workspace;
+    double2 *Bff = (double2 *)(ws + p.off_Bf), *Bfb = (double2 *)(ws + p.off_Bb);
+    if ((e = ppf::launch_chirp_ft(p.r.f, Bff, Bff + p.r.f.M, T1f, T2f, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_lf_chirp");
+    if ((e = ppf::launch_chirp_ft(p.r.b, Bfb, Bfb + p.r.b.M, T1b, T2b, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_lf_chirp");
+    p.r.f.in_dtype = in_dtype;
+    p.r.f.in = in;
+    p.r.phases = phases;
+    p.r.out = out;
+    for (int64_t r0 = 0; r0 < nrows; r0 += p.rows_c) {
+        p.r.f.row0 = p.r.b.row0 = r0;
+        const int64_t nr = nrows - r0 < p.rows_c ? nrows - r0 : p.rows_c;
+        e = ppf::launch_rotate_long(p.r, nr, (double2 *)(ws + p.off_A), (double2 *)(ws + p.off_Y), Bff, Bfb,
+                                    T1f, T2f, T1b, T2b, st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "k_lr");
+    }
+    return PPF_OK;
+}
+
 int ppf_scales_batch(ppf_ctx *ctx, int32_t nsub, int32_t nchan, int32_t nharm, const double *D,
                      const double *M, const int32_t *model_index, const double *errs_FT,
                      const double *params, const double *P, const double *freqs, const double *nus,

@@ -233,6 +233,15 @@ struct LongNoiseArgs {
     const void *in;
     int64_t row0;               // first row of this launch
 };
+// ppf_rotate_long: the forward (f: nbin) and inverse (b: output) Bluestein
+// plans of one call
+struct LongRotArgs {
+    LongNoiseArgs f, b;
+    int out_even;               // output of even length 2 b.n (packed inverse)
+    int64_t nout;               // output samples per row
+    const double *phases;       // [nrows]
+    double *out;                // [nrows][nout]
+};
 struct LongPassArgs {
     int64_t nbatch;
     int len, log2len;
@@ -383,6 +392,9 @@ hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 int lf_pow_blocks(const LongNoiseArgs &a);
 hipError_t launch_chirp_ft(const LongNoiseArgs &a, double2 *Bf, double2 *Bs, const double2 *T1,
                            const double2 *T2, hipStream_t st);
+hipError_t launch_rotate_long(const LongRotArgs &r, int64_t nrows, double2 *A, double2 *Y, const double2 *Bff,
+                              const double2 *Bfb, const double2 *T1f, const double2 *T2f, const double2 *T1b,
+                              const double2 *T2b, hipStream_t st);
 hipError_t launch_noise_long(const LongNoiseArgs &a, int64_t nrows, double2 *A, double2 *Y,
                              const double2 *Bf, double *part, double *out, const double2 *T1,
                              const double2 *T2, hipStream_t st);

@@ -211,4 +211,102 @@ hipError_t launch_noise_long(const LongNoiseArgs &a, int64_t nrows, double2 *A, 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Rotation of rows of any length (ppf_rotate_long, round 6): rotate_data's
+// irfft(rfft(x) e^{2 pi i k phi}) (pplib.py:2427-2515) where the block
+// kernels' LDS transforms do not reach.  Both transforms are Bluestein's
+// (natural order in and out, any length): the forward one on the packed /
+// odd row as in ppf_noise_long, the inverse as conj(DFT(conj Y)) of the
+// spectrum repacked for a real output -- even output length L = 2 No:
+// Y_j = E_j + i O_j, E_j = (R_j + conj R_{No-j}) / 2, O_j = e^{2 pi i j / L}
+// (R_j - conj R_{No-j}) / 2, so IDFT_No(Y)_j = x_2j + i x_2j+1; odd L = nbin:
+// the Hermitian fill R_j, conj R_{L-j}.  R = X e^{2 pi i k phi} with the
+// imaginary parts irfft ignores (R_0, and R_No at even L) dropped.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_lr_mid(LongRotArgs r, const double2 *Yf, double2 *A2) {
+    const int64_t row = blockIdx.y;
+    const LongNoiseArgs &f = r.f, &b = r.b;
+    const double2 *Z = Yf + row * f.M;
+    const double phi = r.phases[f.row0 + row];
+    auto zk = [&](int64_t k) -> double2 {
+        if (k >= f.n) k -= f.n;
+        return cmul(Z[k], chirp(k, f.n));
+    };
+    // the rotated spectrum R_k, 0 <= k <= nbin / 2
+    auto Rk = [&](int64_t k) -> double2 {
+        double2 X;
+        if (f.packed) {
+            const double2 z1 = zk(k), z2 = cconj(zk(f.n - k));
+            const double2 e = cscale(cadd(z1, z2), 0.5), o = cscale(csub(z1, z2), 0.5);
+            const double2 wo = cmul(phasor_pi(2 * k, f.nbin, -1.0), o);
+            X = cmk(e.x + wo.y, e.y - wo.x);
+        } else {
+            X = zk(k);
+        }
+        double2 R = cmul(X, cexp2pi((double)k * phi));
+        if (k == 0 || (r.out_even && k == b.n)) R.y = 0.0;
+        return R;
+    };
+    double2 *out = A2 + row * b.M;
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < b.M; j += (int64_t)gridDim.x * kBlock) {
+        double2 y = cmk(0.0, 0.0);
+        if (j < b.n) {
+            double2 Y;
+            if (r.out_even) {
+                const double2 r1 = Rk(j), r2 = cconj(Rk(b.n - j));
+                const double2 E = cscale(cadd(r1, r2), 0.5);
+                const double2 O = cmul(phasor_pi(2 * j, 2 * b.n, 1.0), cscale(csub(r1, r2), 0.5));
+                Y = cmk(E.x - O.y, E.y + O.x);            // E + i O
+            } else {
+                const int64_t N = b.n / 2;                  // odd L = b.n: k <= N stored
+                Y = j <= N ? Rk(j) : cconj(Rk(b.n - j));
+            }
+            // inverse DFT as conj(DFT(conj Y)): Bluestein input conj(Y) w_j
+            y = cmul(cconj(Y), chirp(j, b.n));
+        }
+        out[j] = y;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_lr_out(LongRotArgs r, const double2 *Yb) {
+    const int64_t row = blockIdx.y;
+    const LongNoiseArgs &b = r.b;
+    const double2 *Y = Yb + row * b.M;
+    double *out = r.out + (r.b.row0 + row) * r.nout;
+    const double s = 1.0 / (double)b.n;
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < b.n; j += (int64_t)gridDim.x * kBlock) {
+        // IDFT(Y)_j = conj(w_j y_j) / n
+        const double2 v = cscale(cconj(cmul(Y[j], chirp(j, b.n))), s);
+        if (r.out_even) {
+            out[2 * j] = v.x;
+            out[2 * j + 1] = v.y;
+        } else {
+            out[j] = v.x;
+        }
+    }
+}
+
+hipError_t launch_rotate_long(const LongRotArgs &r, int64_t nrows, double2 *A, double2 *Y, const double2 *Bff,
+                              const double2 *Bfb, const double2 *T1f, const double2 *T2f, const double2 *T1b,
+                              const double2 *T2b, hipStream_t st) {
+    hipError_t e;
+    const LongNoiseArgs &f = r.f, &b = r.b;
+    // forward: chirped row -> DFT_n in natural order (in A)
+    hipLaunchKernelGGL(k_lf_load, dim3(stride_blocks(f.M), (unsigned)nrows), dim3(kBlock), 0, st, f, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(f, nrows, A, Y, false, T1f, T2f, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lf_mul, dim3(stride_blocks(f.M), (unsigned)nrows), dim3(kBlock), 0, st, f, A, Bff);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(f, nrows, A, Y, true, T1f, T2f, st)) != hipSuccess) return e;
+    // rotate, repack, chirp for the inverse (into Y, row stride b.M)
+    hipLaunchKernelGGL(k_lr_mid, dim3(stride_blocks(b.M), (unsigned)nrows), dim3(kBlock), 0, st, r, A, Y);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(b, nrows, Y, A, false, T1b, T2b, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lf_mul, dim3(stride_blocks(b.M), (unsigned)nrows), dim3(kBlock), 0, st, b, Y, Bfb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(b, nrows, Y, A, true, T1b, T2b, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lr_out, dim3(stride_blocks(b.n), (unsigned)nrows), dim3(kBlock), 0, st, r, Y);
+    return hipGetLastError();
+}
+
 }  // namespace ppf

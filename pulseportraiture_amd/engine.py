@@ -490,6 +490,23 @@ def rotate_rows(rows, phases, dev=None, ref_len=False):
     out = torch.empty((r2.shape[0], nout), dtype=torch.float64, device=dev)
     ctx = _lib.context(dev.index)
     lib = _lib.load()
+    if not _noise_batch_len_ok(nbin):
+        # past the LDS transforms (even > 8192, odd > 4095; the same rule as
+        # ppf_noise_batch): Bluestein transforms both ways (ppf_rotate_long)
+        nb = lib.ppf_rotate_long_workspace_bytes(r2.shape[0], nbin,
+                                                 int(bool(ref_len)))
+        if nb == 0:
+            raise NotImplementedError(
+                "rotation of %d-sample rows: past the 2^23-point transform"
+                % nbin)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        rc = lib.ppf_rotate_long(
+            ctx, r2.shape[0], nbin,
+            _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,
+            _p(r2), _p(ph), _p(out), int(bool(ref_len)), _p(ws), nb,
+            _stream(dev))
+        _lib.check(rc, ctx)
+        return out.reshape(tuple(shape[:-1]) + (nout,))
     fn = lib.ppf_rotate_batch_ref if ref_len else lib.ppf_rotate_batch
     rc = fn(ctx, r2.shape[0], nbin,
             _lib.PPF_F32 if r2.dtype == torch.float32 else _lib.PPF_F64,

@@ -95,6 +95,12 @@ def test_workspace_query_and_validation_without_gpu():
         2 * (1 << 19) * 16 + 256 * 8
     assert lib.ppf_noise_long(None, 1, 1 << 20, _lib.PPF_F64, None, 4, None,
                               None, 0, None) == _lib.PPF_EINVAL
+    # rotation of long rows: Bluestein both ways, any length to 2^23 points
+    for nb in (4097, 8194, 16384, 1 << 23):
+        assert lib.ppf_rotate_long_workspace_bytes(2, nb, 1) > 0, nb
+    assert lib.ppf_rotate_long_workspace_bytes(2, (1 << 24) + 2, 0) == 0
+    assert lib.ppf_rotate_long(None, 1, 16384, _lib.PPF_F64, None, None,
+                               None, 0, None, 0, None) == _lib.PPF_EINVAL
 
 
 @pytest.mark.parametrize("seed", range(40))

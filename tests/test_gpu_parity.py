@@ -155,13 +155,18 @@ def test_rotate_matches_reference(ppl, ppt):
 
 
 @pytest.mark.parametrize("nbin", [1000, 1022, 2006, 4094, 33, 127, 511,
-                                  1001, 1023, 4095])
+                                  1001, 1023, 4095,
+                                  # round 6: past the LDS transforms
+                                  # (ppf_rotate_long, Bluestein both ways)
+                                  4097, 8194, 12001, 16384])
 def test_rotate_any_nbin_matches_numpy(ppl, nbin):
     """rotate_data (pplib.py:2427-2480) at nbin/2 not a power of two, on
     the mixed-radix (1000) and generic-radix (1022 = 2 x 7 x 73, 2006 =
     2 x 17 x 59, 4094 = 2 x 23 x 89) LDS FFTs, and at odd nbin (33, 127
     prime, 511 = 7 x 73, 1001, 1023, 4095 = 3^2 5 7 13: the row as nbin
-    complex points, Hermitian inverse), against its own NumPy arithmetic:
+    complex points, Hermitian inverse), and past the LDS transforms (4097,
+    8194 = 2 x 17 x 241, 12001, 16384: ppf_rotate_long), against its own
+    NumPy arithmetic:
     rfft, phasor, irfft -- the irfft WITHOUT a length, as the reference calls
     it (pplib.py:2466, 2508-2512, 2550, 2652; pptoaslib.py:89): at odd nbin
     the public routines return nbin - 1 samples.  The internal full-length

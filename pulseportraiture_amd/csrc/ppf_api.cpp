@@ -212,6 +212,11 @@ int cz_tables(ppf_ctx *ctx, const ppf::CzPlan &c, hipStream_t st, const double2 
 struct FitLayout {
     size_t M, X, chan, stats, x0, gP, gw, nuref, Msum, gpart, gwx, gflag, state, partials, active, mom, dphi,
         mres, hcen, Mpow, MP, KC, needx, xslot, rclist, Bt, total;
+    // rows past the LDS transforms (round 6): their rFFTs (data spectra,
+    // long-transform chirp tables and work rows, rows per chunk)
+    int lng;
+    size_t spec, lchirp, lA, lY;
+    int64_t lrows;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
     int momx;     // wave shapes, PPF_OPT_MOM_X: every fit's moments from X (k_xspec_w + k_moments)
@@ -230,6 +235,16 @@ static bool mom16_layout(const FitLayout &L, int nbin) {
 
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+bool bluestein_plan(int64_t nbin, int64_t n, bool packed, ppf::LongNoiseArgs &a);
+
+// fits at nbin past the LDS transforms (even > 8192, odd > 4095): the rows'
+// rFFTs on the long transforms, then the X-based fit; no GetTOAs guess there
+bool long_fit_ok(const ppf_fit_desc *d) {
+    ppf::LongNoiseArgs f;
+    return !nbin_supported(d->nbin) && d->nbin > 4095 && !d->guess &&
+           bluestein_plan(d->nbin, (d->nbin & 1) ? d->nbin : d->nbin / 2, !(d->nbin & 1), f);
+}
 
 FitLayout fit_layout(const ppf_fit_desc *d) {
     FitLayout L{};
@@ -281,16 +296,59 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
             L.gflag = o; o += align256(nsub);
         }
     }
+    L.lng = long_fit_ok(d) ? 1 : 0;
+    if (L.lng) {
+        ppf::LongNoiseArgs f;
+        bluestein_plan(d->nbin, (d->nbin & 1) ? d->nbin : d->nbin / 2, !(d->nbin & 1), f);
+        const size_t row_b = (size_t)f.M * sizeof(double2);
+        const int64_t rows = (int64_t)(nsub > (size_t)(d->nmodel > 0 ? d->nmodel : 1) ? nsub
+                                       : (size_t)(d->nmodel > 0 ? d->nmodel : 1)) * (int64_t)nchan;
+        int64_t rc = (int64_t)((size_t)(256u << 20) / (2 * row_b));
+        if (rc < 1) rc = 1;
+        L.lrows = rows < rc ? rows : rc;
+        L.spec = o;   o += align256(sizeof(double2) * nsub * nchan * nharm);
+        L.lchirp = o; o += align256(2 * row_b);
+        L.lA = o;     o += align256((size_t)L.lrows * row_b);
+        L.lY = o;     o += align256((size_t)L.lrows * row_b);
+    }
     L.total = o;
     return L;
+}
+
+// the rFFTs of nrows real rows of nbin samples on the long transforms into
+// out[row][k], k <= nbin / 2 (Bluestein; the chirp table once per call)
+int long_rfft_rows(ppf_ctx *ctx, const FitLayout &L, char *ws, int64_t nbin, int64_t nrows, int dtype,
+                   const void *in, double2 *out, bool chirp_ready, hipStream_t st) {
+    ppf::LongNoiseArgs f;
+    if (!bluestein_plan(nbin, (nbin & 1) ? nbin : nbin / 2, !(nbin & 1), f))
+        return fail(ctx, PPF_EUNSUP, "nbin=%lld", (long long)nbin);
+    const double2 *T1, *T2, *unused;
+    int rc;
+    if ((rc = twiddles(ctx, (int)(2 * f.M1), st, &T1, &unused))) return rc;
+    if ((rc = twiddles(ctx, (int)(2 * f.M2), st, &T2, &unused))) return rc;
+    double2 *Bf = (double2 *)(ws + L.lchirp);
+    hipError_t e;
+    if (!chirp_ready && (e = ppf::launch_chirp_ft(f, Bf, Bf + f.M, T1, T2, st)) != hipSuccess)
+        return hip_fail(ctx, e, "k_lf_chirp");
+    f.in_dtype = dtype;
+    f.in = in;
+    for (int64_t r0 = 0; r0 < nrows; r0 += L.lrows) {
+        f.row0 = r0;
+        const int64_t nr = nrows - r0 < L.lrows ? nrows - r0 : L.lrows;
+        if ((e = ppf::launch_rfft_long(f, nr, (double2 *)(ws + L.lA), (double2 *)(ws + L.lY), Bf, out, T1, T2,
+                                       st)) != hipSuccess)
+            return hip_fail(ctx, e, "k_lr_spec");
+    }
+    return PPF_OK;
 }
 
 int check_fit_desc(ppf_ctx *ctx, const ppf_fit_desc *d) {
     if (!d) return fail(ctx, PPF_EINVAL, "null descriptor");
     if (d->nsub < 1 || d->nchan < 1) return fail(ctx, PPF_EINVAL, "nsub=%d nchan=%d", d->nsub, d->nchan);
-    if (!nbin_supported(d->nbin))
+    if (!nbin_supported(d->nbin) && !long_fit_ok(d))
         return fail(ctx, PPF_EUNSUP,
-                    "nbin=%d: must be even in [32, 8192] or odd in [33, 4095]", d->nbin);
+                    "nbin=%d: must be even in [32, 8192] or odd in [33, 4095], or longer without the "
+                    "GetTOAs guess (up to 2^23 transform points)", d->nbin);
     if (d->data_dtype != PPF_F32 && d->data_dtype != PPF_F64)
         return fail(ctx, PPF_EINVAL, "data_dtype=%d", d->data_dtype);
     if (d->nmodel < 1) return fail(ctx, PPF_EINVAL, "nmodel=%d", d->nmodel);
@@ -473,7 +531,8 @@ const char *ppf_last_error(const ppf_ctx *ctx) {
 }
 
 size_t ppf_fit_workspace_bytes(const ppf_fit_desc *desc) {
-    if (!desc || desc->nsub < 1 || desc->nchan < 1 || !nbin_supported(desc->nbin)) return 0;
+    if (!desc || desc->nsub < 1 || desc->nchan < 1 || (!nbin_supported(desc->nbin) && !long_fit_ok(desc)))
+        return 0;
     return fit_layout(desc).total;
 }
 
@@ -484,9 +543,10 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     hipStream_t st = (hipStream_t)stream;
-    const double2 *T, *T2;
-    if ((rc = twiddles(ctx, d->nbin, st, &T, &T2))) return rc;
     const FitLayout L = fit_layout(d);
+    // (long rows: no LDS transform runs, so no twiddle table of nbin)
+    const double2 *T = nullptr, *T2 = nullptr;
+    if (!L.lng && (rc = twiddles(ctx, d->nbin, st, &T, &T2))) return rc;
     char *ws = (char *)d->workspace;
     double2 *Mft = (double2 *)(ws + L.M);
     const int nharm = d->nbin / 2 + 1;
@@ -525,9 +585,15 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
     ctx->ran[slot][2] = d->guess != 0;
     ctx->ran[slot][4] = ctx->ran[slot][5] = false;
     mark(0);
-    ppf::RfftArgs ra{d->nbin, rfft_log2(d->nbin), PPF_F64, d->model, T, T2, Mft};
-    if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
-        return hip_fail(ctx, e, "k_rfft_rows");
+    if (L.lng) {
+        if ((rc = long_rfft_rows(ctx, L, ws, d->nbin, (int64_t)d->nmodel * d->nchan, PPF_F64, d->model, Mft,
+                                 false, st)))
+            return rc;
+    } else {
+        ppf::RfftArgs ra{d->nbin, rfft_log2(d->nbin), PPF_F64, d->model, T, T2, Mft};
+        if ((e = ppf::launch_rfft_rows(ra, (int64_t)d->nmodel * d->nchan, st)) != hipSuccess)
+            return hip_fail(ctx, e, "k_rfft_rows");
+    }
     double *Mpow = (double *)(ws + L.Mpow);
     if ((e = ppf::launch_model_pow_t(Mft, d->nchan, nharm, d->nmodel, (double *)(ws + L.MP), st)) !=
         hipSuccess)
@@ -601,6 +667,13 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         if (!(fused && L.xcap == 0) &&
             (e = ppf::launch_xspec_wave(xa, st)) != hipSuccess)
             return hip_fail(ctx, e, "k_xspec_w");
+    } else if (L.lng) {
+        double2 *spec = (double2 *)(ws + L.spec);
+        if ((rc = long_rfft_rows(ctx, L, ws, d->nbin, (int64_t)d->nsub * d->nchan, d->data_dtype, d->data, spec,
+                                 true, st)))
+            return rc;
+        xa.spec = spec;
+        if ((e = ppf::launch_xspec_spec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec_spec");
     } else {
         if ((e = ppf::launch_xspec(xa, st)) != hipSuccess) return hip_fail(ctx, e, "k_xspec");
     }

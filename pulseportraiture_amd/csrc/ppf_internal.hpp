@@ -25,6 +25,7 @@ struct XspecArgs {
     const double2 *T, *T2;
     double2 *X;                  // [nsub][N+1][nchan] (harmonic-major)
     double *chan;                // [nsub][nchan][4]
+    const double2 *spec;         // k_xspec_spec: the rows' rFFTs [nsub][nchan][N+1] (long rows)
     // wave path: model row power sum_{k>=1} |M_nk|^2 ([nmodel][nchan]) and
     // the per-sub-int "write X" flag (null: every sub-int).  Sub-ints whose
     // fit runs on moments (k_xmom) are skipped.
@@ -392,6 +393,9 @@ hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st);
 int lf_pow_blocks(const LongNoiseArgs &a);
 hipError_t launch_chirp_ft(const LongNoiseArgs &a, double2 *Bf, double2 *Bs, const double2 *T1,
                            const double2 *T2, hipStream_t st);
+hipError_t launch_rfft_long(const LongNoiseArgs &f, int64_t nrows, double2 *A, double2 *Y, const double2 *Bf,
+                            double2 *out, const double2 *T1, const double2 *T2, hipStream_t st);
+hipError_t launch_xspec_spec(const XspecArgs &a, hipStream_t st);
 hipError_t launch_rotate_long(const LongRotArgs &r, int64_t nrows, double2 *A, double2 *Y, const double2 *Bff,
                               const double2 *Bfb, const double2 *T1f, const double2 *T2f, const double2 *T1b,
                               const double2 *T2b, hipStream_t st);

@@ -275,6 +275,68 @@ __global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
 }
 
 // ===========================================================================
+// k_xspec_spec: k_xspec_any's per-row arithmetic on rows whose rFFT was
+// taken beforehand (a.spec, the long-row transforms of ppf_longfft.hip:
+// even nbin > 8192, odd > 4095; round 6) -- noise, Sd_n, S_n and X from the
+// stored bins, no LDS transform
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_xspec_spec(XspecArgs a) {
+    __shared__ double red[kWaves * 4];
+    const int N = a.nbin >> 1, NH = N + 1;
+    const int tid = threadIdx.x;
+    const int s = blockIdx.x / a.nblk, cb = blockIdx.x % a.nblk;
+    if (a.needx && !a.needx[s]) return;
+    const int c0 = cb * a.cb, c1 = min(a.nchan, c0 + a.cb);
+    const int mi = a.model_index ? a.model_index[s] : 0;
+    const uint8_t *mask = a.mask ? a.mask + (int64_t)s * a.nchan : nullptr;
+    const double sqrt_half_nbin = sqrt((double)a.nbin / 2.0);
+    for (int n = c0; n < c1; ++n) {
+        const int64_t crow = (int64_t)s * a.nchan + n;
+        if (mask && !mask[n]) {
+            if (tid < 4) a.chan[crow * 4 + tid] = 0.0;
+            continue;
+        }
+        const double2 *D = a.spec + crow * NH;
+        double acc[2] = {0.0, 0.0};
+        for (int k = tid; k <= N; k += kBlock) {
+            const double p2 = cabs2(D[k]);
+            if (k >= a.kc) acc[0] += p2;
+            if (k >= 1) acc[1] += p2;
+        }
+        block_sum<2>(acc, red);
+        double errs_FT;
+        if (a.errs) errs_FT = a.errs[crow] * sqrt_half_nbin;
+        else errs_FT = sqrt(acc[0] / (double)(NH - a.kc) / (double)a.nbin) * sqrt_half_nbin;
+        const double inv_e2 = 1.0 / (errs_FT * errs_FT);
+        double2 *Xrow = a.X + (int64_t)(a.xslot ? a.xslot[s] : s) * NH * a.nchan + n;
+        const double2 *Mrow = a.Mft + ((int64_t)mi * a.nchan + n) * NH;
+        double mpow[1] = {0.0};
+        for (int k = tid; k <= N; k += kBlock) {
+            if (k == 0) {
+                Xrow[0] = cmk(0.0, 0.0);
+            } else {
+                const double2 M = Mrow[k];
+                mpow[0] += cabs2(M);
+                Xrow[(int64_t)k * a.nchan] = cscale(cmulc(D[k], M), inv_e2);
+            }
+        }
+        block_sum<1>(mpow, red);
+        if (tid == 0) {
+            double *chan = a.chan + crow * 4;
+            chan[0] = errs_FT;
+            chan[1] = inv_e2;
+            chan[2] = acc[1] * inv_e2;
+            chan[3] = mpow[0] * inv_e2;
+        }
+    }
+}
+
+hipError_t launch_xspec_spec(const XspecArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(k_xspec_spec, dim3((unsigned)((int64_t)a.nsub * a.nblk)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
+// ===========================================================================
 // 1-D FFTFIT objective and scipy brute + fmin replica (pplib.py:1294-1306,
 // 2136-2182; scipy.optimize.brute / _minimize_neldermead), one workgroup.
 // xm[k] = D_k conj(M_k) (k = 0 zeroed), in LDS.

@@ -286,6 +286,44 @@ __global__ __launch_bounds__(kBlock) void k_lr_out(LongRotArgs r, const double2 
     }
 }
 
+// rFFT bins X_k, k < nbin / 2 + 1, of rows transformed by the forward
+// Bluestein plan f (natural-order y in Yf) -> out[row0 + row][k] (the fit's
+// long-row spectra: model rows for Mft, data rows for k_xspec_spec)
+__global__ __launch_bounds__(kBlock) void k_lr_spec(LongNoiseArgs f, const double2 *Yf, double2 *out) {
+    const int64_t row = blockIdx.y;
+    const double2 *Z = Yf + row * f.M;
+    const int64_t nharm = f.nbin / 2 + 1;
+    auto zk = [&](int64_t k) -> double2 {
+        if (k >= f.n) k -= f.n;
+        return cmul(Z[k], chirp(k, f.n));
+    };
+    double2 *o = out + (f.row0 + row) * nharm;
+    for (int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x; k < nharm; k += (int64_t)gridDim.x * kBlock) {
+        if (f.packed) {
+            const double2 z1 = zk(k), z2 = cconj(zk(f.n - k));
+            const double2 e = cscale(cadd(z1, z2), 0.5), q = cscale(csub(z1, z2), 0.5);
+            const double2 wo = cmul(phasor_pi(2 * k, f.nbin, -1.0), q);
+            o[k] = cmk(e.x + wo.y, e.y - wo.x);
+        } else {
+            o[k] = zk(k);
+        }
+    }
+}
+
+hipError_t launch_rfft_long(const LongNoiseArgs &f, int64_t nrows, double2 *A, double2 *Y, const double2 *Bf,
+                            double2 *out, const double2 *T1, const double2 *T2, hipStream_t st) {
+    hipError_t e;
+    hipLaunchKernelGGL(k_lf_load, dim3(stride_blocks(f.M), (unsigned)nrows), dim3(kBlock), 0, st, f, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(f, nrows, A, Y, false, T1, T2, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lf_mul, dim3(stride_blocks(f.M), (unsigned)nrows), dim3(kBlock), 0, st, f, A, Bf);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = four_step(f, nrows, A, Y, true, T1, T2, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lr_spec, dim3(stride_blocks(f.nbin / 2 + 1), (unsigned)nrows), dim3(kBlock), 0, st, f,
+                       A, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_rotate_long(const LongRotArgs &r, int64_t nrows, double2 *A, double2 *Y, const double2 *Bff,
                               const double2 *Bfb, const double2 *T1f, const double2 *T2f, const double2 *T1b,
                               const double2 *T2b, hipStream_t st) {

@@ -424,9 +424,11 @@ def _workspace_bytes(lib, per_sub, c0, c1, n_x, cfg):
 def _desc_workspace_bytes(lib, d):
     nbytes = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
     if nbytes == 0:
-        raise NotImplementedError("unsupported shape nsub=%d nchan=%d nbin=%d"
-                                  " (nbin must be even in [32, 8192] or odd in [33, 4095])" %
-                                  (d.nsub, d.nchan, d.nbin))
+        raise NotImplementedError(
+            "unsupported shape nsub=%d nchan=%d nbin=%d (nbin must be even in"
+            " [32, 8192] or odd in [33, 4095]; longer rows fit without the"
+            " GetTOAs guess, up to 2^23 transform points)" %
+            (d.nsub, d.nchan, d.nbin))
     return nbytes
 
 

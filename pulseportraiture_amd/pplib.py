@@ -349,7 +349,7 @@ def get_noise_PS(data, frac=4, chans=False):
     if not engine.noise_len_supported(row.size):
         # the flattened portrait (nchan nbin samples; pplib.py:2334-2338) is
         # longer than the LDS transforms of ppf_noise_batch (even <= 8192,
-        # odd <= 4095 points): one library rFFT on the device (rocFFT) instead
+        # odd <= 4095 points): the long transforms of ppf_noise_long
         return engine.noise_long(row, frac)
     return float(engine.noise_rows(row[None, :], frac).cpu().numpy()[0])
 

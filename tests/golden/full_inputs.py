@@ -103,6 +103,14 @@ FITS = [
          seed=114),
     dict(name="pdta_64x1001", nchan=64, nbin=1001, flags=[1, 1, 0, 1, 1],
          seed=115, tau=2e-3),
+    # round 6: rows past the LDS transforms (even nbin > 8192, odd > 4095):
+    # the rFFTs on the long (four-step / chirp z) transforms, fits on X
+    dict(name="pd_16x16384", nchan=16, nbin=16384, flags=[1, 1, 0, 0, 0],
+         seed=116),
+    dict(name="pdta_16x10002", nchan=16, nbin=10002, flags=[1, 1, 0, 1, 1],
+         seed=117, tau=2e-3),
+    dict(name="pd_16x8193", nchan=16, nbin=8193, flags=[1, 1, 0, 0, 0],
+         seed=118),
 ]
 
 

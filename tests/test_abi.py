@@ -66,13 +66,24 @@ def test_workspace_query_and_validation_without_gpu():
     # nbin 1000 (nbin/2 = 2^2 5^3) runs on the mixed-radix LDS FFT, nbin/2
     # with a prime factor above 7 (1002 = 2 x 3 x 167, 8186 = 2 x 4093) on
     # its generic-radix stage; odd nbin up to 4095 as a full-length complex
-    # transform; longer odd rows and nbin past 8192 are refused
+    # transform
     for nb in (1000, 1002, 1022, 8186, 33, 1001, 1023, 4095):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
-    for nb in (4097, 8191, 8194, 16, 31):
+    # round 6: rows past the LDS transforms fit on the long transforms --
+    # without the GetTOAs guess, whose profile FFT is an LDS transform: with
+    # it they are refused; short rows stay refused
+    for nb in (16, 31):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
+    for nb in (4097, 8191, 8194, 16384):
+        d.nbin = nb
+        assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
+        d.guess, d.guess_Ns = 1, 100
+        assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
+        d.guess = 0
+    d.nbin = (1 << 24) + 2                        # past 2^23 transform points
+    assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0
     # with the GetTOAs guess at nbin 2048 the phase/DM fits take their
     # moments from X by default (every sub-int holds a slot); the fused
     # pass can be forced

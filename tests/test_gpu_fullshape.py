@@ -36,7 +36,10 @@ def _kept_harmonic_fraction(model):
                                   "lowsnr_all_512x2048", "pd_128x1000",
                                   "pdta_128x1536", "pd_128x1022",
                                   "pdta_64x2006", "pd_128x1023",
-                                  "pdta_64x1001"])
+                                  "pdta_64x1001",
+                                  # round 6: rows past the LDS transforms
+                                  "pd_16x16384", "pdta_16x10002",
+                                  "pd_16x8193"])
 def test_fullshape_fit_matches_reference(name):
     """configs[2]'s fit (phi, DM, GM, tau, alpha) and phi+DM+tau+alpha at
     512 x 2048, a narrow-component template at 512 x 2048 (no harmonic
@@ -47,7 +50,10 @@ def test_fullshape_fit_matches_reference(name):
     small; S/N 133 with all five parameters), nbin = 1000 and 1536 (not
     powers of two: the mixed-radix LDS FFT), 1022 and 2006 (the
     generic-radix stage), the odd 1023 and 1001 (full-length complex
-    transforms of the rows), through the drop-in fit_portrait_full."""
+    transforms of the rows), and rows past the LDS transforms (16384,
+    10002 = 2 x 3 x 1667 with scattering, the odd 8193: the rows' rFFTs on
+    the long four-step / chirp z-transforms, round 6), through the drop-in
+    fit_portrait_full."""
     from pulseportraiture_amd import pptoaslib
     c, data, model, freqs = F.fit_case(name)
     if int(c["narrow"]):

@@ -215,7 +215,7 @@ struct FitLayout {
     // rows past the LDS transforms (round 6): their rFFTs (data spectra,
     // long-transform chirp tables and work rows, rows per chunk)
     int lng;
-    size_t spec, lchirp, lA, lY;
+    size_t spec, lchirp, lA, lY, gprof, gspec;
     int64_t lrows;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
@@ -240,9 +240,15 @@ bool bluestein_plan(int64_t nbin, int64_t n, bool packed, ppf::LongNoiseArgs &a)
 
 // fits at nbin past the LDS transforms (even > 8192, odd > 4095): the rows'
 // rFFTs on the long transforms, then the X-based fit; no GetTOAs guess there
+// With the GetTOAs guess the profile's spectrum (N + 1 harmonics) and the
+// brute grid sit in one workgroup's LDS: nbin up to ~18,000.
 bool long_fit_ok(const ppf_fit_desc *d) {
     ppf::LongNoiseArgs f;
-    return !nbin_supported(d->nbin) && d->nbin > 4095 && !d->guess &&
+    if (d->guess) {
+        const size_t lds = ((size_t)d->nbin / 2 + 2) * sizeof(double2) + (size_t)(d->guess_Ns + 8) * sizeof(double);
+        if (lds > 150u * 1024u) return false;
+    }
+    return !nbin_supported(d->nbin) && d->nbin > 4095 &&
            bluestein_plan(d->nbin, (d->nbin & 1) ? d->nbin : d->nbin / 2, !(d->nbin & 1), f);
 }
 
@@ -307,6 +313,10 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
         if (rc < 1) rc = 1;
         L.lrows = rows < rc ? rows : rc;
         L.spec = o;   o += align256(sizeof(double2) * nsub * nchan * nharm);
+        if (d->guess) {
+            L.gprof = o; o += align256(sizeof(double) * nsub * (size_t)d->nbin);
+            L.gspec = o; o += align256(sizeof(double2) * nsub * nharm);
+        }
         L.lchirp = o; o += align256(2 * row_b);
         L.lA = o;     o += align256((size_t)L.lrows * row_b);
         L.lY = o;     o += align256((size_t)L.lrows * row_b);
@@ -711,6 +721,15 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
         ga.gpart = xa.gpart;
         ga.gwx = xa.gw;
         ga.nblk = L.nblk;
+        if (L.lng) {
+            // the profiles' rFFTs on the long transforms (same plan as the rows)
+            double *prof = (double *)(ws + L.gprof);
+            double2 *gspec = (double2 *)(ws + L.gspec);
+            if ((e = ppf::launch_gsum(d->nsub, L.nblkd, d->nbin, da.gP, prof, st)) != hipSuccess)
+                return hip_fail(ctx, e, "k_gsum");
+            if ((rc = long_rfft_rows(ctx, L, ws, d->nbin, d->nsub, PPF_F64, prof, gspec, true, st))) return rc;
+            ga.gspec = gspec;
+        }
         ppf::CzPlan cz{};
         if (cz_plan(ga.Ns, d->nbin / 2 + 1, cz)) {
             if ((rc = cz_tables(ctx, cz, st, &ga.czB, &ga.czT))) return rc;
@@ -1289,7 +1308,12 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
                              const double *scattering_index, const double *freqs,
                              const double *nu_ref, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    // rows past the LDS transforms (round 6): the Gaussians are evaluated
+    // per bin in LDS (nbin doubles); only the scattering convolution needs a
+    // transform, so long rows take unscattered models only
+    const bool lng = !nbin_supported(nbin);
+    if (lng && (nbin <= 4095 || (size_t)nbin * sizeof(double) > 150u * 1024u))
+        return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nport < 0 || nchan < 1 || ngauss < 0 ||
         (nport > 0 && (!params || !scattering_index || !freqs || !nu_ref || !out)))
         return fail(ctx, PPF_EINVAL, "bad gauss_portrait arguments");
@@ -1306,15 +1330,29 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     hipStream_t st = (hipStream_t)stream;
-    const double2 *T, *T2;
-    int rc = twiddles(ctx, nbin, st, &T, &T2);
-    if (rc) return rc;
+    const double2 *T = nullptr, *T2 = nullptr;
+    int rc;
+    if (lng) {
+        // the models' tau (params[p][1]) on the host: a scattered one at
+        // this length is refused, not half-built (a one-off small copy)
+        std::vector<double> prm((size_t)nport * (2 + 6 * ngauss));
+        if ((e = hipMemcpyAsync(prm.data(), params, prm.size() * sizeof(double), hipMemcpyDeviceToHost, st)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMemcpyAsync(params)");
+        for (int p = 0; p < nport; ++p)
+            if (prm[(size_t)p * (2 + 6 * ngauss) + 1] != 0.0)
+                return fail(ctx, PPF_EUNSUP, "scattered model (TAU != 0) at nbin=%d: the convolution needs an "
+                            "LDS transform (even nbin <= 8192, odd <= 4095)", nbin);
+    } else if ((rc = twiddles(ctx, nbin, st, &T, &T2))) {
+        return rc;
+    }
     a.nport = nport; a.nchan = nchan; a.nbin = nbin; a.log2N = rfft_log2(nbin);
     a.ngauss = ngauss; a.npar = 2 + 6 * ngauss;
     a.params = params; a.scat_index = scattering_index; a.freqs = freqs; a.nu_ref = nu_ref;
     a.T = T; a.T2 = T2; a.out = out;
     a.Te = T; a.T2e = T2;
-    if ((nbin & 1) && (rc = twiddles(ctx, nbin - 1, st, &a.Te, &a.T2e))) return rc;
+    if (!lng && (nbin & 1) && (rc = twiddles(ctx, nbin - 1, st, &a.Te, &a.T2e))) return rc;
     if ((e = ppf::launch_gauss_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_gauss_port");
     return PPF_OK;
 }

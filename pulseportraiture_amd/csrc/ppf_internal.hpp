@@ -114,6 +114,9 @@ struct GuessArgs {
     // twiddles; null: the direct sums
     const double2 *czB, *czT;
     int czP, czJ, czQ, czK;
+    // long rows (round 6): the guess profiles' rFFTs [nsub][N+1], taken on
+    // the long transforms, replace the LDS transform of the profile
+    const double2 *gspec;
 };
 
 // chirp z-transform plan of a whole-turn brute grid (k_guess): Kmax
@@ -396,6 +399,7 @@ hipError_t launch_chirp_ft(const LongNoiseArgs &a, double2 *Bf, double2 *Bs, con
 hipError_t launch_rfft_long(const LongNoiseArgs &f, int64_t nrows, double2 *A, double2 *Y, const double2 *Bf,
                             double2 *out, const double2 *T1, const double2 *T2, hipStream_t st);
 hipError_t launch_xspec_spec(const XspecArgs &a, hipStream_t st);
+hipError_t launch_gsum(int nsub, int nblkd, int nbin, const double *gP, double *prof, hipStream_t st);
 hipError_t launch_rotate_long(const LongRotArgs &r, int64_t nrows, double2 *A, double2 *Y, const double2 *Bff,
                               const double2 *Bfb, const double2 *T1f, const double2 *T2f, const double2 *T1b,
                               const double2 *T2b, hipStream_t st);

@@ -274,6 +274,23 @@ __global__ __launch_bounds__(kBlock) void k_xspec_any(XspecArgs a) {
     }
 }
 
+// the guess profiles of long rows: prof[s][t] = sum_b gP[s][b][t] (the
+// block partials of k_dsum in k_guess's order), for their long rFFT
+__global__ __launch_bounds__(kBlock) void k_gsum(int nblkd, int nbin, const double *gP, double *prof) {
+    const int64_t s = blockIdx.y;
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < nbin; t += gridDim.x * kBlock) {
+        double p = 0.0;
+        for (int b = 0; b < nblkd; ++b) p += gP[((int64_t)s * nblkd + b) * nbin + t];
+        prof[s * nbin + t] = p;
+    }
+}
+
+hipError_t launch_gsum(int nsub, int nblkd, int nbin, const double *gP, double *prof, hipStream_t st) {
+    hipLaunchKernelGGL(k_gsum, dim3((unsigned)((nbin + kBlock - 1) / kBlock), (unsigned)nsub), dim3(kBlock), 0,
+                       st, nblkd, nbin, gP, prof);
+    return hipGetLastError();
+}
+
 // ===========================================================================
 // k_xspec_spec: k_xspec_any's per-row arithmetic on rows whose rFFT was
 // taken beforehand (a.spec, the long-row transforms of ppf_longfft.hip:
@@ -950,12 +967,14 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 template <bool MX, int CZL = 0>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // lds: z[max(rfft_len, czP)] (packed profile, FFT in place; then the
-    // chirp z-transform's buffer) | xm[N+1] | sh[Ns+8]
+    // chirp z-transform's buffer; none with gspec) | xm[N+1] | sh[Ns+8]
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const int N = a.nbin >> 1, nharm = N + 1, s = blockIdx.x, tid = threadIdx.x;
     const bool odd = a.nbin & 1;
-    double2 *z = lds, *xm = lds + (a.czB && a.czP > rfft_len(a.nbin) ? a.czP : rfft_len(a.nbin));
+    const bool pre = a.gspec != nullptr;      // (uniform) the profile's rFFT given
+    double2 *z = lds,
+            *xm = lds + (pre ? 0 : (a.czB && a.czP > rfft_len(a.nbin) ? a.czP : rfft_len(a.nbin)));
     double *sh = reinterpret_cast<double *>(xm + nharm + 1);
     // fused (k_xspec_w accumulated the guess spectrum of its rows in the
     // Fourier domain): the block partials of the covered harmonics
@@ -977,7 +996,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
         }
         sh[0] = w0; sh[1] = w1; sh[2] = w2;
     }
-    if (!fused) {
+    if (!fused && !pre) {
         // weighted dedispersed profile: sum of the k_dsum block partials
         // (fixed order), packed z_j = p_2j + i p_2j+1 for the real FFT
         // (odd nbin: z_j = p_j)
@@ -998,7 +1017,7 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     }
     __syncthreads();
     const double wsum = sh[0], cnt = sh[1];
-    if (!fused) lds_fft_n<MX>(z, rfft_len(a.nbin), a.T, false);
+    if (!fused && !pre) lds_fft_n<MX>(z, rfft_len(a.nbin), a.T, false);
     // R_k of the fused partials (k < NL; 0 above: past every channel's cutoff)
     auto fused_bin = [&](int k) {
         double2 r = cmk(0.0, 0.0);
@@ -1044,7 +1063,8 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
             }
         }
         if (!kv || k >= kloop) continue;
-        double2 R = cscale(fused ? fused_bin(k) : rbin(z, a.nbin, a.T2, k), 1.0 / wsum);
+        double2 R = cscale(fused ? fused_bin(k) : (pre ? a.gspec[(int64_t)s * nharm + k] : rbin(z, a.nbin, a.T2, k)),
+                           1.0 / wsum);
         M = cscale(M, 1.0 / cnt);
         if (a.guess_tau && a.guess_tau[s] != 0.0) {   // scattered model profile
             double u = kTwoPi * (double)k * a.guess_tau[s];
@@ -1704,7 +1724,7 @@ hipError_t launch_align_phases(int nsub, int nchan, const double *results, const
 }
 
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
-    const int zs = (a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin);
+    const int zs = a.gspec ? 0 : ((a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin));
     size_t lds = (size_t)(zs + a.nbin / 2 + 2) * sizeof(double2) +
                  (size_t)(a.Ns + 8) * sizeof(double);
     const dim3 g((unsigned)a.nsub), b(kBlock);
@@ -1725,6 +1745,12 @@ hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st) {
     size_t lds = (size_t)rfft_len(a.nbin) * sizeof(double2);
     dim3 g((unsigned)((int64_t)a.nport * a.nchan)), b(kBlock);
+    if (!fft_len_supported(rfft_len(a.nbin))) {
+        // long rows, unscattered models (checked by the caller): the row in
+        // LDS only; the smallest instantiation (its transform never runs)
+        hipLaunchKernelGGL((k_gauss_port<1, false>), g, b, (size_t)a.nbin * sizeof(double), st, a);
+        return hipGetLastError();
+    }
     const bool mx = !is_pow2(rfft_len(a.nbin));
     switch (kmax_pow2(a.nbin / 2 + (a.nbin & 1))) {
         case 1: MXL(mx, k_gauss_port, 1, g, b, lds, st, a); break;

@@ -175,6 +175,9 @@ TOAS = [
     # get_TOAs with a spline template (pptoas.py:416-419), 512 -> 1024 bins
     dict(name="spline", nfile=2, nsub=4, nchan=64, nbin=1024, seed=204,
          spline=True),
+    # round 6: rows past the LDS transforms (the guess profile's rFFT and
+    # every row's on the long transforms)
+    dict(name="long16384", nfile=1, nsub=3, nchan=16, nbin=16384, seed=208),
     # ---- the non-default branches of get_TOAs (round 3) ----------------
     # (a) configs[2]'s drop-in entry: fit_GM + fit_scat at 512 x 2048 with a
     # .gmodel whose TAU != 0 (tau guess from gparams, phase guess against

@@ -70,17 +70,18 @@ def test_workspace_query_and_validation_without_gpu():
     for nb in (1000, 1002, 1022, 8186, 33, 1001, 1023, 4095):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
-    # round 6: rows past the LDS transforms fit on the long transforms --
-    # without the GetTOAs guess, whose profile FFT is an LDS transform: with
-    # it they are refused; short rows stay refused
+    # round 6: rows past the LDS transforms fit on the long transforms; with
+    # the GetTOAs guess while its profile spectrum fits one workgroup's LDS
+    # (nbin up to ~18,000 at Ns = 100); short rows stay refused
     for nb in (16, 31):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
-    for nb in (4097, 8191, 8194, 16384):
+    for nb in (4097, 8191, 8194, 16384, 40000):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
         d.guess, d.guess_Ns = 1, 100
-        assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
+        assert (lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0) == \
+            (nb < 18000), nb
         d.guess = 0
     d.nbin = (1 << 24) + 2                        # past 2^23 transform points
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0

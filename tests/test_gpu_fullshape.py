@@ -143,14 +143,16 @@ def _same_printed_number(a, b):
     return abs(fa - fb) <= 1.01 * 10 ** (-dec)
 
 
-@pytest.mark.parametrize("name", ["c1", "c2", "narrow", "spline"])
+@pytest.mark.parametrize("name", ["c1", "c2", "narrow", "spline",
+                                  "long16384"])
 def test_fullshape_gettoas_matches_reference(name, monkeypatch, tmp_path,
                                              capsys):
     """GetTOAs.get_TOAs against the reference's run: configs[0] (the
     examples/example.py archive set: 5 x 10 x 64 x 512 with scintillation,
     get_TOAs(DM0=DM0)), one configs[1]-shape archive (8 x 512 x 2048), the
-    narrow-template archive and a spline (make_spline_model) template
-    resampled 512 -> 1024 bins; per sub-int phases/DMs within 0.01 sigma,
+    narrow-template archive, a spline (make_spline_model) template
+    resampled 512 -> 1024 bins and 3 x 16 x 16384 rows (round 6: every rFFT,
+    the guess profile's included, on the long transforms); per sub-int phases/DMs within 0.01 sigma,
     chi2_red 1e-8, DeltaDM, and every .tim token to its printed precision."""
     from pulseportraiture_amd import pptoas, pplib
     c, files, gm = _archives(name)

@@ -48,8 +48,8 @@ extern "C" {
 /* ABI 5 (round 6): ppf_rotate_batch_ref. */
 /* ABI 6 (round 6): ppf_noise_long, ppf_rotate_long (+ their workspace
  * queries), ppf_align_phases, PPF_OPT_SPIN_WAIT; ppf_fit_batch /
- * ppf_gauss_portrait_batch accept nbin past the LDS transforms (even > 8192,
- * odd > 4095) on the long transforms. */
+ * ppf_gauss_portrait_batch / ppf_phase_shift_batch accept nbin past the LDS
+ * transforms (even > 8192, odd > 4095) on the long transforms. */
 #define PPF_ABI_VERSION 6
 
 enum ppf_error {

@@ -46,6 +46,11 @@ struct ppf_ctx {
     int nsolv[kRing] = {};
     long ncalls = 0;
     unsigned *host_active = nullptr;   // pinned, for the iteration loop
+    // device scratch of the long-row FFTFIT (ppf_phase_shift_batch past the
+    // LDS transforms; grown on demand, held for the whole synchronous call)
+    void *lscr = nullptr;
+    size_t lscr_bytes = 0;
+    std::mutex lscr_mu;
 };
 
 namespace {
@@ -419,6 +424,7 @@ void ppf_destroy(ppf_ctx *ctx) {
             (void)hipEventDestroy(pr.second);
         }
     if (ctx->host_active) (void)hipHostFree(ctx->host_active);
+    if (ctx->lscr) (void)hipFree(ctx->lscr);
     delete ctx;
 }
 
@@ -1284,22 +1290,76 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
                           const double *noise, int32_t Ns, double lo, double hi, double *out,
                           void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!nbin_supported(nbin)) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
+    // rows past the LDS transforms (round 6): their rFFTs on the long
+    // transforms first, the FFTFIT on the stored bins (a synchronous call)
+    const bool lng = !nbin_supported(nbin) && nbin > 4095;
+    if (!nbin_supported(nbin) && !lng) return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
     if (nprof < 0 || Ns < 1 || Ns > 65536 || (nprof > 0 && (!data || !model || !out)))
         return fail(ctx, PPF_EINVAL, "bad phase-shift arguments");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
+    if (lng && ((size_t)(nbin / 2 + 2) * sizeof(double2) + (size_t)(Ns + 8) * sizeof(double) > 150u * 1024u))
+        return fail(ctx, PPF_EUNSUP, "nbin=%d Ns=%d: the spectrum and grid exceed one workgroup's LDS", nbin, Ns);
     if (nprof == 0) return PPF_OK;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     hipStream_t st = (hipStream_t)stream;
-    const double2 *T, *T2;
-    int rc = twiddles(ctx, nbin, st, &T, &T2);
-    if (rc) return rc;
+    const double2 *T = nullptr, *T2 = nullptr;
+    int rc;
+    if (!lng && (rc = twiddles(ctx, nbin, st, &T, &T2))) return rc;
     ppf::PhaseShiftArgs a{};
     a.nbin = nbin; a.log2N = rfft_log2(nbin); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
     a.Ns = Ns; a.lo = lo; a.hi = hi; a.data = data; a.model = model; a.model_index = model_index;
     a.noise = noise; a.T = T; a.T2 = T2; a.out = out;
+    if (!lng) {
+        if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
+        return PPF_OK;
+    }
+    // model rows in use: 1 + the largest model_index
+    int nmodel = 1;
+    if (model_index) {
+        std::vector<int32_t> mi(nprof);
+        if ((e = hipMemcpyAsync(mi.data(), model_index, nprof * sizeof(int32_t), hipMemcpyDeviceToHost, st)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMemcpyAsync(model_index)");
+        for (int i = 0; i < nprof; ++i) {
+            if (mi[i] < 0) return fail(ctx, PPF_EINVAL, "model_index[%d] = %d", i, mi[i]);
+            nmodel = std::max(nmodel, mi[i] + 1);
+        }
+    }
+    ppf::LongNoiseArgs f;
+    if (!bluestein_plan(nbin, (nbin & 1) ? nbin : nbin / 2, !(nbin & 1), f))
+        return fail(ctx, PPF_EUNSUP, "nbin=%d", nbin);
+    const size_t nharm = (size_t)nbin / 2 + 1, row_b = (size_t)f.M * sizeof(double2);
+    FitLayout L{};
+    const int64_t rows = std::max<int64_t>(nprof, nmodel);
+    int64_t rcn = (int64_t)((size_t)(256u << 20) / (2 * row_b));
+    L.lrows = rows < rcn ? rows : (rcn < 1 ? 1 : rcn);
+    size_t o = 0;
+    const size_t oD = o; o += align256(sizeof(double2) * (size_t)nprof * nharm);
+    const size_t oM = o; o += align256(sizeof(double2) * (size_t)nmodel * nharm);
+    L.lchirp = o; o += align256(2 * row_b);
+    L.lA = o; o += align256((size_t)L.lrows * row_b);
+    L.lY = o; o += align256((size_t)L.lrows * row_b);
+    std::lock_guard<std::mutex> lk(ctx->lscr_mu);
+    if (ctx->lscr_bytes < o) {
+        if (ctx->lscr) {
+            if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(ctx, e, "hipDeviceSynchronize");
+            (void)hipFree(ctx->lscr);
+            ctx->lscr = nullptr;
+            ctx->lscr_bytes = 0;
+        }
+        if ((e = hipMalloc(&ctx->lscr, o)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(long scratch)");
+        ctx->lscr_bytes = o;
+    }
+    char *ws = (char *)ctx->lscr;
+    if ((rc = long_rfft_rows(ctx, L, ws, nbin, nmodel, PPF_F64, model, (double2 *)(ws + oM), false, st))) return rc;
+    if ((rc = long_rfft_rows(ctx, L, ws, nbin, nprof, in_dtype, data, (double2 *)(ws + oD), true, st))) return rc;
+    a.Mspec = (const double2 *)(ws + oM);
+    a.Dspec = (const double2 *)(ws + oD);
     if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
+    // the scratch is reused by the next call (any stream): finish here
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
     return PPF_OK;
 }
 

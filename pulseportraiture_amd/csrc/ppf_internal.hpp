@@ -265,6 +265,9 @@ struct PhaseShiftArgs {
     const double *noise;
     const double2 *T, *T2;
     double *out;
+    // long rows (round 6): the profiles' and model rows' rFFTs ([nprof] /
+    // [nmodel][N+1]) taken beforehand on the long transforms; null: LDS FFTs
+    const double2 *Dspec, *Mspec;
 };
 
 struct SynthArgs {

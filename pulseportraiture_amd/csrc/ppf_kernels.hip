@@ -1221,28 +1221,33 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     // [rfft_len] fft | [N+1] xm | sh
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
-    const int N = a.nbin >> 1, nharm = N + 1, NF = rfft_len(a.nbin);
+    const bool pre = a.Dspec != nullptr;   // (uniform) rFFTs given: long rows
+    const int N = a.nbin >> 1, nharm = N + 1, NF = pre ? 0 : rfft_len(a.nbin);
     double *sh = reinterpret_cast<double *>(lds + NF + N + 2);
     const int64_t prof = blockIdx.x;
     double2 *fbuf = lds, *xm = lds + NF;
     // model spectrum first (into xm as M_k)
     const int mi = a.model_index ? a.model_index[prof] : 0;
-    load_row(fbuf, a.model, 1, mi, a.nbin);
-    __syncthreads();
-    lds_fft_n<MX>(fbuf, NF, a.T, false);
+    if (!pre) {
+        load_row(fbuf, a.model, 1, mi, a.nbin);
+        __syncthreads();
+        lds_fft_n<MX>(fbuf, NF, a.T, false);
+    }
     double pp[1] = {0.0};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
-        double2 M = rbin(fbuf, a.nbin, a.T2, k);
+        double2 M = pre ? a.Mspec[(int64_t)mi * nharm + k] : rbin(fbuf, a.nbin, a.T2, k);
         xm[k] = M;
         if (k >= 1) pp[0] += cabs2(M);
     }
     __syncthreads();
-    load_row(fbuf, a.data, a.dtype, prof, a.nbin);
-    __syncthreads();
-    lds_fft_n<MX>(fbuf, NF, a.T, false);
+    if (!pre) {
+        load_row(fbuf, a.data, a.dtype, prof, a.nbin);
+        __syncthreads();
+        lds_fft_n<MX>(fbuf, NF, a.T, false);
+    }
     double acc[3] = {0.0, 0.0, pp[0]};
     for (int k = threadIdx.x; k <= N; k += kBlock) {
-        double2 D = rbin(fbuf, a.nbin, a.T2, k);
+        double2 D = pre ? a.Dspec[prof * nharm + k] : rbin(fbuf, a.nbin, a.T2, k);
         double p2 = cabs2(D);
         if (k >= a.kc) acc[0] += p2;
         if (k >= 1) acc[1] += p2;
@@ -1999,7 +2004,7 @@ hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st) {
-    size_t lds = (size_t)(rfft_len(a.nbin) + a.nbin / 2 + 2) * sizeof(double2) +
+    size_t lds = (size_t)((a.Dspec ? 0 : rfft_len(a.nbin)) + a.nbin / 2 + 2) * sizeof(double2) +
                  (size_t)(a.Ns + 8) * sizeof(double);
     if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_phase_shift<true>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);

@@ -210,6 +210,30 @@ def test_rotate_round_trip_and_bad_shapes(ppl, capsys):
     assert "Wrong shape for array of periods." in capsys.readouterr().out
 
 
+@pytest.mark.parametrize("nbin", [16384, 8193])
+def test_fit_phase_shift_long_rows_match_oracle(ppl, nbin):
+    """fit_phase_shift (pplib.py:2136-2182) at nbin past the LDS transforms
+    (round 6: the rFFTs on the long transforms, ppf_phase_shift_batch's
+    synchronous path) against the oracle's restatement of the reference
+    (scipy brute + fmin)."""
+    from oracle import ppfit_oracle as O
+    rng = np.random.default_rng(nbin)
+    t = np.arange(nbin) / nbin
+    model = np.exp(-0.5 * ((t - 0.4) / 0.01) ** 2) + \
+        0.3 * np.exp(-0.5 * ((t - 0.47) / 0.02) ** 2)
+    for shift in (0.123, -0.31):
+        X = np.fft.rfft(model) * np.exp(2j * np.pi * np.arange(nbin // 2 + 1)
+                                        * shift)
+        d = 2.5 * np.fft.irfft(X, n=nbin) + rng.normal(0, 0.05, nbin)
+        got = ppl.fit_phase_shift(d, model, Ns=100)
+        want = O.fit_phase_shift(d, model, Ns=100)
+        assert abs(G.phase_diff(got.phase, want["phase"])) < \
+            0.01 * want["phase_err"]
+        assert abs(got.phase_err / want["phase_err"] - 1) < 1e-4
+        assert abs(got.scale / want["scale"] - 1) < 1e-6
+        assert abs(got.snr / want["snr"] - 1) < 1e-6
+
+
 def test_fit_phase_shift_matches_reference(ppl):
     m = G.misc()
     for row in m["fps_rows"]:

@@ -467,7 +467,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
         // the current group is summed (software pipeline, one memory wait per
         // group)
 #ifndef PPF_PASS_KB
-#define PPF_PASS_KB 4
+// harmonics per load group.  Round 6: 3 instead of 4 -- at three waves per
+// SIMD the 4-harmonic body spilled 40 B (168 VGPRs), the 3-harmonic one
+// fits in 154: C3 +0.8 %, C5 +2 % (profiles/r06/ab_kb_status.txt)
+#define PPF_PASS_KB 3
 #endif
         constexpr int KB = PPF_PASS_KB;
         // two buffers, loads one group ahead of the sums.  The loop is
@@ -493,7 +496,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PPF_PASS
         };
         double2 E = cmk(1.0, 0.0);
         auto sum_group = [&](int kb, const double2 (&xv)[KB], const double (&pv)[KB]) {
-            if ((kb & 63) == 0) E = cexp2pi((double)kb * phin);   // exact seed every 64
+            // exact seed at the first group of every 64 harmonics (KB need
+            // not divide 64; with KB = 4 this is kb % 64 == 0 as before)
+            if ((kb & 63) < KB) E = cexp2pi((double)kb * phin);
 #pragma unroll
             for (int u = 0; u < KB; ++u) {
                 const double kk = (double)(kb + u);

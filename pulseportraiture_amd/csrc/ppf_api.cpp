@@ -220,7 +220,7 @@ struct FitLayout {
     // rows past the LDS transforms (round 6): their rFFTs (data spectra,
     // long-transform chirp tables and work rows, rows per chunk)
     int lng;
-    size_t spec, lchirp, lA, lY, gprof, gspec;
+    size_t spec, lchirp, lA, lY, gprof, gspec, gsh;
     int64_t lrows;
     int nblk, cb, cbd, nblkd;
     int fused;    // phase+DM fits on the fused moment pass (k_xmom_g), X only for scattering fits
@@ -244,15 +244,23 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 bool bluestein_plan(int64_t nbin, int64_t n, bool packed, ppf::LongNoiseArgs &a);
 
 // fits at nbin past the LDS transforms (even > 8192, odd > 4095): the rows'
-// rFFTs on the long transforms, then the X-based fit; no GetTOAs guess there
-// With the GetTOAs guess the profile's spectrum (N + 1 harmonics) and the
-// brute grid sit in one workgroup's LDS: nbin up to ~18,000.
+// rFFTs on the long transforms, then the X-based fit.  With the GetTOAs
+// guess the profile's spectrum (N + 1 harmonics) sits in one workgroup's
+// LDS (nbin up to ~19,000); its brute grid too where it fits, else in
+// global memory (grid_gsh: ppalign's Ns = nbin)
+//
+// grid_gsh: whether the FFTFIT brute grid of Ns points leaves the LDS for
+// global memory ([rows][Ns + 8] doubles): the spectrum (N + 2 bins), the
+// rFFT buffer of the LDS transforms (none for long rows, whose spectra come
+// from the long transforms) and the grid past 150 KB.  ppalign at nbin 8192
+// (Ns = nbin: 197 KB) and past.
+bool grid_gsh(int nbin, int Ns, bool lng) {
+    const size_t fb = lng ? 0 : (size_t)ppf::rfft_len(nbin) * sizeof(double2);
+    return fb + ((size_t)nbin / 2 + 2) * sizeof(double2) + (size_t)(Ns + 8) * sizeof(double) > 150u * 1024u;
+}
 bool long_fit_ok(const ppf_fit_desc *d) {
     ppf::LongNoiseArgs f;
-    if (d->guess) {
-        const size_t lds = ((size_t)d->nbin / 2 + 2) * sizeof(double2) + (size_t)(d->guess_Ns + 8) * sizeof(double);
-        if (lds > 150u * 1024u) return false;
-    }
+    if (d->guess && ((size_t)d->nbin / 2 + 2) * sizeof(double2) > 150u * 1024u) return false;
     return !nbin_supported(d->nbin) && d->nbin > 4095 &&
            bluestein_plan(d->nbin, (d->nbin & 1) ? d->nbin : d->nbin / 2, !(d->nbin & 1), f);
 }
@@ -325,6 +333,9 @@ FitLayout fit_layout(const ppf_fit_desc *d) {
         L.lchirp = o; o += align256(2 * row_b);
         L.lA = o;     o += align256((size_t)L.lrows * row_b);
         L.lY = o;     o += align256((size_t)L.lrows * row_b);
+    }
+    if (d->guess && grid_gsh(d->nbin, d->guess_Ns, L.lng)) {
+        L.gsh = o; o += align256(sizeof(double) * nsub * ((size_t)d->guess_Ns + 8));
     }
     L.total = o;
     return L;
@@ -736,6 +747,7 @@ int ppf_fit_batch(ppf_ctx *ctx, const ppf_fit_desc *d, void *stream) {
             if ((rc = long_rfft_rows(ctx, L, ws, d->nbin, d->nsub, PPF_F64, prof, gspec, true, st))) return rc;
             ga.gspec = gspec;
         }
+        if (grid_gsh(d->nbin, ga.Ns, L.lng)) ga.gsh = (double *)(ws + L.gsh);
         ppf::CzPlan cz{};
         if (cz_plan(ga.Ns, d->nbin / 2 + 1, cz)) {
             if ((rc = cz_tables(ctx, cz, st, &ga.czB, &ga.czT))) return rc;
@@ -1285,6 +1297,21 @@ int ppf_copy_from_pinned(ppf_ctx *ctx, void *dst, const void *src, int64_t nbyte
     return PPF_OK;
 }
 
+// grows the context's scratch to at least `bytes` (lscr_mu held)
+static int lscr_reserve(ppf_ctx *ctx, size_t bytes) {
+    if (ctx->lscr_bytes >= bytes) return PPF_OK;
+    hipError_t e;
+    if (ctx->lscr) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(ctx, e, "hipDeviceSynchronize");
+        (void)hipFree(ctx->lscr);
+        ctx->lscr = nullptr;
+        ctx->lscr_bytes = 0;
+    }
+    if ((e = hipMalloc(&ctx->lscr, bytes)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(scratch)");
+    ctx->lscr_bytes = bytes;
+    return PPF_OK;
+}
+
 int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_dtype,
                           const void *data, const double *model, const int32_t *model_index,
                           const double *noise, int32_t Ns, double lo, double hi, double *out,
@@ -1297,8 +1324,8 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     if (nprof < 0 || Ns < 1 || Ns > 65536 || (nprof > 0 && (!data || !model || !out)))
         return fail(ctx, PPF_EINVAL, "bad phase-shift arguments");
     if (in_dtype != PPF_F32 && in_dtype != PPF_F64) return fail(ctx, PPF_EINVAL, "in_dtype");
-    if (lng && ((size_t)(nbin / 2 + 2) * sizeof(double2) + (size_t)(Ns + 8) * sizeof(double) > 150u * 1024u))
-        return fail(ctx, PPF_EUNSUP, "nbin=%d Ns=%d: the spectrum and grid exceed one workgroup's LDS", nbin, Ns);
+    if (lng && (size_t)(nbin / 2 + 2) * sizeof(double2) > 150u * 1024u)
+        return fail(ctx, PPF_EUNSUP, "nbin=%d: the spectrum exceeds one workgroup's LDS", nbin);
     if (nprof == 0) return PPF_OK;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
@@ -1310,8 +1337,18 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     a.nbin = nbin; a.log2N = rfft_log2(nbin); a.dtype = in_dtype; a.kc = noise_kc(nbin / 2 + 1, 4);
     a.Ns = Ns; a.lo = lo; a.hi = hi; a.data = data; a.model = model; a.model_index = model_index;
     a.noise = noise; a.T = T; a.T2 = T2; a.out = out;
-    if (!lng) {
+    if (!lng && !grid_gsh(nbin, Ns, false)) {
         if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
+        return PPF_OK;
+    }
+    if (!lng) {
+        // the brute grid past the LDS (Ns = nbin at 8192): in the context's
+        // scratch, held for the whole (synchronous) call
+        std::lock_guard<std::mutex> lk(ctx->lscr_mu);
+        if ((rc = lscr_reserve(ctx, align256(sizeof(double) * (size_t)nprof * ((size_t)Ns + 8))))) return rc;
+        a.gsh = (double *)ctx->lscr;
+        if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
         return PPF_OK;
     }
     // model rows in use: 1 + the largest model_index
@@ -1341,22 +1378,16 @@ int ppf_phase_shift_batch(ppf_ctx *ctx, int32_t nprof, int32_t nbin, int32_t in_
     L.lchirp = o; o += align256(2 * row_b);
     L.lA = o; o += align256((size_t)L.lrows * row_b);
     L.lY = o; o += align256((size_t)L.lrows * row_b);
+    const bool gs = grid_gsh(nbin, Ns, true);
+    const size_t oG = o; o += gs ? align256(sizeof(double) * (size_t)nprof * ((size_t)Ns + 8)) : 0;
     std::lock_guard<std::mutex> lk(ctx->lscr_mu);
-    if (ctx->lscr_bytes < o) {
-        if (ctx->lscr) {
-            if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(ctx, e, "hipDeviceSynchronize");
-            (void)hipFree(ctx->lscr);
-            ctx->lscr = nullptr;
-            ctx->lscr_bytes = 0;
-        }
-        if ((e = hipMalloc(&ctx->lscr, o)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc(long scratch)");
-        ctx->lscr_bytes = o;
-    }
+    if ((rc = lscr_reserve(ctx, o))) return rc;
     char *ws = (char *)ctx->lscr;
     if ((rc = long_rfft_rows(ctx, L, ws, nbin, nmodel, PPF_F64, model, (double2 *)(ws + oM), false, st))) return rc;
     if ((rc = long_rfft_rows(ctx, L, ws, nbin, nprof, in_dtype, data, (double2 *)(ws + oD), true, st))) return rc;
     a.Mspec = (const double2 *)(ws + oM);
     a.Dspec = (const double2 *)(ws + oD);
+    if (gs) a.gsh = (double *)(ws + oG);
     if ((e = ppf::launch_phase_shift(a, nprof, st)) != hipSuccess) return hip_fail(ctx, e, "k_phase_shift");
     // the scratch is reused by the next call (any stream): finish here
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");

@@ -117,6 +117,9 @@ struct GuessArgs {
     // long rows (round 6): the guess profiles' rFFTs [nsub][N+1], taken on
     // the long transforms, replace the LDS transform of the profile
     const double2 *gspec;
+    // long rows whose brute grid does not fit next to the spectrum in LDS
+    // (ppalign: Ns = nbin): the grid in global memory, [nsub][Ns + 8]
+    double *gsh;
 };
 
 // chirp z-transform plan of a whole-turn brute grid (k_guess): Kmax
@@ -268,6 +271,9 @@ struct PhaseShiftArgs {
     // long rows (round 6): the profiles' and model rows' rFFTs ([nprof] /
     // [nmodel][N+1]) taken beforehand on the long transforms; null: LDS FFTs
     const double2 *Dspec, *Mspec;
+    // their brute grid in global memory ([nprof][Ns + 8]) when it does not
+    // fit next to the spectrum in LDS; null: in LDS
+    double *gsh;
 };
 
 struct SynthArgs {

@@ -964,7 +964,7 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
 // ===========================================================================
-template <bool MX, int CZL = 0>
+template <bool MX, int CZL = 0, bool GS = false>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // lds: z[max(rfft_len, czP)] (packed profile, FFT in place; then the
     // chirp z-transform's buffer; none with gspec) | xm[N+1] | sh[Ns+8]
@@ -975,7 +975,8 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     const bool pre = a.gspec != nullptr;      // (uniform) the profile's rFFT given
     double2 *z = lds,
             *xm = lds + (pre ? 0 : (a.czB && a.czP > rfft_len(a.nbin) ? a.czP : rfft_len(a.nbin)));
-    double *sh = reinterpret_cast<double *>(xm + nharm + 1);
+    // GS (long rows, a grid past the LDS): sh in global memory
+    double *sh = GS ? a.gsh + (int64_t)s * (a.Ns + 8) : reinterpret_cast<double *>(xm + nharm + 1);
     // fused (k_xspec_w accumulated the guess spectrum of its rows in the
     // Fourier domain): the block partials of the covered harmonics
     const bool fused = a.gflag && a.gflag[s];
@@ -1216,15 +1217,15 @@ __global__ __launch_bounds__(kBlock) void k_noise(NoiseArgs a) {
 // ===========================================================================
 // k_phase_shift: pplib.fit_phase_shift per profile
 // ===========================================================================
-template <bool MX>
+template <bool MX, bool GS = false>
 __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
     // [rfft_len] fft | [N+1] xm | sh
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     __shared__ double red[kWaves * 4];
     const bool pre = a.Dspec != nullptr;   // (uniform) rFFTs given: long rows
     const int N = a.nbin >> 1, nharm = N + 1, NF = pre ? 0 : rfft_len(a.nbin);
-    double *sh = reinterpret_cast<double *>(lds + NF + N + 2);
     const int64_t prof = blockIdx.x;
+    double *sh = GS ? a.gsh + prof * (a.Ns + 8) : reinterpret_cast<double *>(lds + NF + N + 2);
     double2 *fbuf = lds, *xm = lds + NF;
     // model spectrum first (into xm as M_k)
     const int mi = a.model_index ? a.model_index[prof] : 0;
@@ -1731,9 +1732,14 @@ hipError_t launch_align_phases(int nsub, int nchan, const double *results, const
 hipError_t launch_guess(const GuessArgs &a, hipStream_t st) {
     const int zs = a.gspec ? 0 : ((a.czB && a.czP > rfft_len(a.nbin)) ? a.czP : rfft_len(a.nbin));
     size_t lds = (size_t)(zs + a.nbin / 2 + 2) * sizeof(double2) +
-                 (size_t)(a.Ns + 8) * sizeof(double);
+                 (a.gsh ? 0 : (size_t)(a.Ns + 8) * sizeof(double));
     const dim3 g((unsigned)a.nsub), b(kBlock);
-    if (a.czB && is_pow2(rfft_len(a.nbin))) {
+    if (a.gsh) {
+        // the brute grid in global memory (long rows: gspec given, no
+        // transform runs in the kernel)
+        if (a.gspec || is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL((k_guess<false, 0, true>), g, b, lds, st, a);
+        else hipLaunchKernelGGL((k_guess<true, 0, true>), g, b, lds, st, a);
+    } else if (a.czB && is_pow2(rfft_len(a.nbin))) {
         switch (a.czP) {
             case 512: hipLaunchKernelGGL((k_guess<false, 9>), g, b, lds, st, a); break;
             case 1024: hipLaunchKernelGGL((k_guess<false, 10>), g, b, lds, st, a); break;
@@ -2005,8 +2011,12 @@ hipError_t launch_noise(const NoiseArgs &a, int64_t nrows, hipStream_t st) {
 }
 hipError_t launch_phase_shift(const PhaseShiftArgs &a, int nprof, hipStream_t st) {
     size_t lds = (size_t)((a.Dspec ? 0 : rfft_len(a.nbin)) + a.nbin / 2 + 2) * sizeof(double2) +
-                 (size_t)(a.Ns + 8) * sizeof(double);
-    if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+                 (a.gsh ? 0 : (size_t)(a.Ns + 8) * sizeof(double));
+    if (a.gsh) {   // the brute grid in global memory
+        if (a.Dspec || is_pow2(rfft_len(a.nbin)))
+            hipLaunchKernelGGL((k_phase_shift<false, true>), dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+        else hipLaunchKernelGGL((k_phase_shift<true, true>), dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
+    } else if (is_pow2(rfft_len(a.nbin))) hipLaunchKernelGGL(k_phase_shift<false>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     else hipLaunchKernelGGL(k_phase_shift<true>, dim3((unsigned)nprof), dim3(kBlock), lds, st, a);
     return hipGetLastError();
 }

@@ -533,6 +533,15 @@ def align_accum(data, phases, weights, out, wsum, dev=None):
             wsum.shape != (nchan,) or wsum.dtype != torch.float64:
         raise ValueError("out must be float64 [nchan, nbin], wsum [nchan]")
     lib = _lib.load()
+    if not _noise_batch_len_ok(nbin):
+        # rows past the LDS transforms: the rotations on the long transforms
+        # (ppf_rotate_long), the weighted sum over sub-ints on the stream;
+        # rows of weight 0 contribute nothing whatever they hold
+        rot = rotate_rows(d, ph, dev).reshape(nsub, nchan, nbin)
+        wr = w.unsqueeze(-1)
+        out += torch.where(wr != 0.0, wr * rot, 0.0).sum(dim=0)
+        wsum += w.sum(dim=0)
+        return out, wsum
     nbytes = lib.ppf_align_workspace_bytes(nsub, nchan, nbin)
     ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
     ctx = _lib.context(dev.index)

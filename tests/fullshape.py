@@ -110,3 +110,36 @@ def align_case(name):
         subints=guess[None, None], weights=np.ones([1, tn]), arch=None,
         state="Intensity")
     return c, archives, model_data
+
+
+def align_synthetic(nchan, nbin, nsub, nfile, seed, noise=0.5):
+    """(archives, model_data) of a synthetic align run (no golden: the
+    oracle's align_archives is the checker), built like align_case's with
+    full_inputs.align_inputs; noise stds at the synthesis level and unit
+    S/N weights."""
+    conf = dict(nchan=nchan, nbin=nbin, nsub=nsub, nfile=nfile, seed=seed,
+                noise=noise)
+    arch, guess, freqs, tfreqs = FI.align_inputs(conf)
+    archives = []
+    for a in arch:
+        w = a["weights"]
+        wn = np.where(w == 0.0, 0.0, 1.0)
+        archives.append(G.Bunch(
+            DM=float(S.DM0), dmc=0, freqs=np.tile(freqs, (nsub, 1)),
+            masks=np.einsum("ij,k", wn, np.ones(nbin))[:, None], nbin=nbin,
+            nchan=nchan, noise_stds=np.full((nsub, 1, nchan), noise), npol=1,
+            nsub=nsub, ok_ichans=[np.compress(wn[j], list(range(nchan)))
+                                  for j in range(nsub)],
+            ok_isubs=np.arange(nsub), prof_SNR=100.0,
+            Ps=np.ones(nsub) * float(S.P0), SNRs=np.ones((nsub, 1, nchan)),
+            subints=a["subints"].astype(np.float32).astype(np.float64)[:, None],
+            weights=w, state="Intensity"))
+    tn = len(tfreqs)
+    model_data = G.Bunch(
+        DM=0.0, dmc=1, freqs=tfreqs[None, :], masks=np.ones([1, 1, tn, nbin]),
+        nbin=nbin, nchan=tn, noise_stds=np.ones([1, 1, tn]), npol=1, nsub=1,
+        ok_ichans=[np.arange(tn)], ok_isubs=np.arange(1), prof_SNR=100.0,
+        Ps=np.ones(1) * float(S.P0), SNRs=np.ones([1, 1, tn]),
+        subints=guess[None, None], weights=np.ones([1, tn]), arch=None,
+        state="Intensity")
+    return archives, model_data

@@ -347,7 +347,8 @@ def align_inputs(c):
             phi = rng.uniform(-0.5, 0.5)
             dDM = rng.normal(3e-4, 2e-4)
             subs[s] = S.subint(c["seed"] * 1000 + f * 10 + s, model, freqs,
-                               phi, S.DM0 + dDM, S.P0, noise=0.5)
+                               phi, S.DM0 + dDM, S.P0,
+                               noise=c.get("noise", 0.5))
         weights = np.ones((nsub, nchan))
         if f == 2:
             weights[:, rng.choice(nchan, 4, replace=False)] = 0.0

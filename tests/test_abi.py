@@ -72,7 +72,8 @@ def test_workspace_query_and_validation_without_gpu():
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
     # round 6: rows past the LDS transforms fit on the long transforms; with
     # the GetTOAs guess while its profile spectrum fits one workgroup's LDS
-    # (nbin up to ~18,000 at Ns = 100); short rows stay refused
+    # (nbin up to ~19,000; the brute grid goes to global memory when it does
+    # not fit beside it, e.g. ppalign's Ns = nbin); short rows stay refused
     for nb in (16, 31):
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0, nb
@@ -80,9 +81,14 @@ def test_workspace_query_and_validation_without_gpu():
         d.nbin = nb
         assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0, nb
         d.guess, d.guess_Ns = 1, 100
-        assert (lib.ppf_fit_workspace_bytes(ctypes.byref(d)) > 0) == \
-            (nb < 18000), nb
-        d.guess = 0
+        w100 = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+        assert (w100 > 0) == (nb < 19000), nb
+        d.guess_Ns = nb
+        wn = lib.ppf_fit_workspace_bytes(ctypes.byref(d))
+        assert (wn > 0) == (nb < 19000), nb
+        if nb == 16384:                           # grid [nsub][Ns + 8] global
+            assert wn - w100 >= d.nsub * (nb + 8) * 8, nb
+        d.guess, d.guess_Ns = 0, 100
     d.nbin = (1 << 24) + 2                        # past 2^23 transform points
     assert lib.ppf_fit_workspace_bytes(ctypes.byref(d)) == 0
     # with the GetTOAs guess at nbin 2048 the phase/DM fits take their

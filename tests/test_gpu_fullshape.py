@@ -428,6 +428,32 @@ def test_fullshape_align_matches_reference(name, monkeypatch):
     np.testing.assert_array_equal(w, c["out_weights"])
 
 
+@pytest.mark.parametrize("nbin", [8192, 16384])
+def test_align_long_rows_match_oracle(nbin, monkeypatch):
+    """ppalign.align_archives at nbin 8192 and 16384 (round 6: the
+    fit_phase_shift(Ns=nbin) grids of the fit's guess and of the final FFTFIT
+    in global memory, past the LDS beside the spectra; at 16384 the rows on
+    the long transforms) against the
+    oracle's restatement of ppalign.py:65-257 on the same synthetic
+    archives (2 archives x 1 sub-int x 8 channels; ~30 s of oracle).  The
+    noise is 0.1 per bin: at 0.5 the 8-channel likelihood has several
+    minima near the guess at nbin >= 8192, and scipy's trust-ncg (the
+    oracle) and the device's Newton trust region settle in different ones
+    (tools/diag_long_align*.py; at 2048 bins they agree to 1e-10)."""
+    from oracle import ppfit_oracle as O
+    from pulseportraiture_amd import ppalign, pptoas
+    archives, model_data = F.align_synthetic(8, nbin, 1, 2, 71, 0.1)
+    files = {"arch%d.fits" % i: a for i, a in enumerate(archives)}
+    files["guess.fits"] = model_data
+    monkeypatch.setattr(pptoas, "load_data", lambda n, **kw: files[n])
+    r = ppalign.align_archives(["arch0.fits", "arch1.fits"], "guess.fits",
+                               fit_dm=True, niter=1, outfile=None, quiet=True)
+    ref, tw = O.align_archives(archives, model_data, fit_dm=True, niter=1)
+    np.testing.assert_allclose(r.port[0], ref[0], rtol=0,
+                               atol=1e-6 * np.abs(ref).max())
+    np.testing.assert_allclose(r.total_weights, tw, rtol=1e-6)
+
+
 # ------------------------------------------- the bench.py pipelines (C2/C3) --
 def _bench_fit(b, nsub, nchan, nbin, flags, scat):
     """engine.fit_batch exactly as bench.py's step() calls it."""

@@ -210,12 +210,13 @@ def test_rotate_round_trip_and_bad_shapes(ppl, capsys):
     assert "Wrong shape for array of periods." in capsys.readouterr().out
 
 
-@pytest.mark.parametrize("nbin", [16384, 8193])
+@pytest.mark.parametrize("nbin", [16384, 8193, 8192])
 def test_fit_phase_shift_long_rows_match_oracle(ppl, nbin):
     """fit_phase_shift (pplib.py:2136-2182) at nbin past the LDS transforms
     (round 6: the rFFTs on the long transforms, ppf_phase_shift_batch's
-    synchronous path) against the oracle's restatement of the reference
-    (scipy brute + fmin)."""
+    synchronous path) and at 8192 with Ns = nbin (the brute grid in global
+    memory beside the LDS transform) against the oracle's restatement of the
+    reference (scipy brute + fmin)."""
     from oracle import ppfit_oracle as O
     rng = np.random.default_rng(nbin)
     t = np.arange(nbin) / nbin
@@ -225,13 +226,15 @@ def test_fit_phase_shift_long_rows_match_oracle(ppl, nbin):
         X = np.fft.rfft(model) * np.exp(2j * np.pi * np.arange(nbin // 2 + 1)
                                         * shift)
         d = 2.5 * np.fft.irfft(X, n=nbin) + rng.normal(0, 0.05, nbin)
-        got = ppl.fit_phase_shift(d, model, Ns=100)
-        want = O.fit_phase_shift(d, model, Ns=100)
-        assert abs(G.phase_diff(got.phase, want["phase"])) < \
-            0.01 * want["phase_err"]
-        assert abs(got.phase_err / want["phase_err"] - 1) < 1e-4
-        assert abs(got.scale / want["scale"] - 1) < 1e-6
-        assert abs(got.snr / want["snr"] - 1) < 1e-6
+        # Ns = nbin (ppalign's): at 16384 the grid leaves the LDS
+        for Ns in (100, nbin):
+            got = ppl.fit_phase_shift(d, model, Ns=Ns)
+            want = O.fit_phase_shift(d, model, Ns=Ns)
+            assert abs(G.phase_diff(got.phase, want["phase"])) < \
+                0.01 * want["phase_err"]
+            assert abs(got.phase_err / want["phase_err"] - 1) < 1e-4
+            assert abs(got.scale / want["scale"] - 1) < 1e-6
+            assert abs(got.snr / want["snr"] - 1) < 1e-6
 
 
 def test_fit_phase_shift_matches_reference(ppl):

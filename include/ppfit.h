@@ -477,7 +477,11 @@ int ppf_host_copy(void *dst, const void *src, int64_t nbytes, int32_t nthreads);
  * (anything else: PPF_EINVAL, the reference's KeyError).  params:
  * [nport][2 + 6*ngauss] = DC, tau [bin], then per component loc, m_loc,
  * wid, m_wid, amp, m_amp; scattering_index, nu_ref: [nport];
- * freqs: [nport][nchan]; out: [nport][nchan][nbin] f64 (device). */
+ * freqs: [nport][nchan]; out: [nport][nchan][nbin] f64 (device).
+ * Rows past the LDS transforms (even nbin > 8192, odd > 4095; nbin ≤
+ * 19,200, the row in LDS): built per bin, a scattered model's convolution
+ * then on the long transforms (synchronous; PPF_EUNSUP for a scattered
+ * model at odd nbin there). */
 int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin,
                              int32_t ngauss, const char *model_code, const double *params,
                              const double *scattering_index, const double *freqs,

@@ -1180,6 +1180,9 @@ size_t ppf_rotate_long_workspace_bytes(int64_t nrows, int64_t nbin, int32_t ref_
     return rot_plan(nrows, nbin, ref_len != 0, p) ? p.bytes : 0;
 }
 
+static int rotate_long_run(ppf_ctx *ctx, RotPlan &p, int64_t nrows, int32_t in_dtype, const void *in,
+                           const double *phases, const double *taus, double *out, char *ws, hipStream_t st);
+
 int ppf_rotate_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype, const void *in,
                     const double *phases, double *out, int32_t ref_len, void *workspace, size_t workspace_bytes,
                     void *stream) {
@@ -1195,14 +1198,22 @@ int ppf_rotate_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype,
         return fail(ctx, PPF_EINVAL, "workspace %zu < %zu bytes", workspace_bytes, p.bytes);
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    hipStream_t st = (hipStream_t)stream;
+    return rotate_long_run(ctx, p, nrows, in_dtype, in, phases, nullptr, out, (char *)workspace,
+                           (hipStream_t)stream);
+}
+
+// the long rotation / scattering convolution of nrows rows on a plan whose
+// workspace is `ws` (in may be out: each chunk's rows are read before
+// they are written)
+static int rotate_long_run(ppf_ctx *ctx, RotPlan &p, int64_t nrows, int32_t in_dtype, const void *in,
+                           const double *phases, const double *taus, double *out, char *ws, hipStream_t st) {
+    hipError_t e;
     const double2 *T1f, *T2f, *T1b, *T2b, *unused;
     int rc;
     if ((rc = twiddles(ctx, (int)(2 * p.r.f.M1), st, &T1f, &unused))) return rc;
     if ((rc = twiddles(ctx, (int)(2 * p.r.f.M2), st, &T2f, &unused))) return rc;
     if ((rc = twiddles(ctx, (int)(2 * p.r.b.M1), st, &T1b, &unused))) return rc;
     if ((rc = twiddles(ctx, (int)(2 * p.r.b.M2), st, &T2b, &unused))) return rc;
-    char *ws = (char *)workspace;
     double2 *Bff = (double2 *)(ws + p.off_Bf), *Bfb = (double2 *)(ws + p.off_Bb);
     if ((e = ppf::launch_chirp_ft(p.r.f, Bff, Bff + p.r.f.M, T1f, T2f, st)) != hipSuccess)
         return hip_fail(ctx, e, "k_lf_chirp");
@@ -1211,6 +1222,7 @@ int ppf_rotate_long(ppf_ctx *ctx, int64_t nrows, int64_t nbin, int32_t in_dtype,
     p.r.f.in_dtype = in_dtype;
     p.r.f.in = in;
     p.r.phases = phases;
+    p.r.taus = taus;
     p.r.out = out;
     for (int64_t r0 = 0; r0 < nrows; r0 += p.rows_c) {
         p.r.f.row0 = p.r.b.row0 = r0;
@@ -1400,8 +1412,10 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
                              const double *nu_ref, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
     // rows past the LDS transforms (round 6): the Gaussians are evaluated
-    // per bin in LDS (nbin doubles); only the scattering convolution needs a
-    // transform, so long rows take unscattered models only
+    // per bin in LDS (nbin doubles); the scattering convolution of even rows
+    // then runs on the long transforms (ppf_rotate_long's pipeline with the
+    // 1 / (1 + 2 pi i k tau_n) factor in place of the phasor; a synchronous
+    // call with the context's scratch); scattered odd rows are refused
     const bool lng = !nbin_supported(nbin);
     if (lng && (nbin <= 4095 || (size_t)nbin * sizeof(double) > 150u * 1024u))
         return fail(ctx, PPF_EUNSUP, "nbin=%d unsupported", nbin);
@@ -1423,6 +1437,7 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     hipStream_t st = (hipStream_t)stream;
     const double2 *T = nullptr, *T2 = nullptr;
     int rc;
+    bool lscat = false;
     if (lng) {
         // the models' tau (params[p][1]) on the host: a scattered one at
         // this length is refused, not half-built (a one-off small copy)
@@ -1432,9 +1447,10 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
             (e = hipStreamSynchronize(st)) != hipSuccess)
             return hip_fail(ctx, e, "hipMemcpyAsync(params)");
         for (int p = 0; p < nport; ++p)
-            if (prm[(size_t)p * (2 + 6 * ngauss) + 1] != 0.0)
-                return fail(ctx, PPF_EUNSUP, "scattered model (TAU != 0) at nbin=%d: the convolution needs an "
-                            "LDS transform (even nbin <= 8192, odd <= 4095)", nbin);
+            if (prm[(size_t)p * (2 + 6 * ngauss) + 1] != 0.0) lscat = true;
+        if (lscat && (nbin & 1))
+            return fail(ctx, PPF_EUNSUP, "scattered model (TAU != 0) at odd nbin=%d past 4095 (the reference's "
+                        "nbin - 1-bin irfft rows)", nbin);
     } else if ((rc = twiddles(ctx, nbin, st, &T, &T2))) {
         return rc;
     }
@@ -1444,7 +1460,22 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
     a.T = T; a.T2 = T2; a.out = out;
     a.Te = T; a.T2e = T2;
     if (!lng && (nbin & 1) && (rc = twiddles(ctx, nbin - 1, st, &a.Te, &a.T2e))) return rc;
+    if (!lscat) {
+        if ((e = ppf::launch_gauss_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_gauss_port");
+        return PPF_OK;
+    }
+    const int64_t nrows = (int64_t)nport * nchan;
+    RotPlan rp;
+    if (!rot_plan(nrows, nbin, false, rp)) return fail(ctx, PPF_EUNSUP, "nbin=%d", nbin);
+    const size_t oT = align256(rp.bytes);
+    std::lock_guard<std::mutex> lk(ctx->lscr_mu);
+    if ((rc = lscr_reserve(ctx, oT + align256(sizeof(double) * (size_t)nrows)))) return rc;
+    char *ws = (char *)ctx->lscr;
+    a.taus_out = (double *)(ws + oT);
     if ((e = ppf::launch_gauss_port(a, st)) != hipSuccess) return hip_fail(ctx, e, "k_gauss_port");
+    if ((rc = rotate_long_run(ctx, rp, nrows, PPF_F64, out, nullptr, a.taus_out, out, ws, st))) return rc;
+    // the scratch is reused by the next call (any stream): finish here
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
     return PPF_OK;
 }
 

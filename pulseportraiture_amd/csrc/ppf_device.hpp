@@ -122,6 +122,19 @@ __device__ __forceinline__ double wave_reduce(double v, Op op) {
     }
     return readlane63_d(v);
 }
+
+// the scattering kernel 1 / (1 + i b) of pplib.scattering_portrait_FT:
+// NumPy's complex reciprocal (loops CDOUBLE_reciprocal) of 1 + i b
+__device__ __forceinline__ double2 scat_recip(double b) {
+#pragma clang fp contract(off)
+    if (fabs(b) <= 1.0) {
+        const double r = b / 1.0, d = 1.0 + b * r;
+        return cmk(1.0 / d, -r / d);
+    }
+    const double r = 1.0 / b, d = 1.0 * r + b;
+    return cmk(r / d, -1.0 / d);
+}
+
 #ifdef PPF_SHFL_REDUCE
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -246,7 +246,11 @@ struct LongRotArgs {
     LongNoiseArgs f, b;
     int out_even;               // output of even length 2 b.n (packed inverse)
     int64_t nout;               // output samples per row
-    const double *phases;       // [nrows]
+    const double *phases;       // [nrows], or null: no rotation
+    // [nrows] scattering tau_n (rotations per harmonic): the spectrum times
+    // 1 / (1 + 2 pi i k tau_n) (the long rows' scattered Gaussian
+    // portraits); null: none
+    const double *taus;
     double *out;                // [nrows][nout]
 };
 struct LongPassArgs {
@@ -334,6 +338,9 @@ struct GaussArgs {
     const double2 *T, *T2;
     const double2 *Te, *T2e;     // odd nbin: the twiddles of nbin - 1 (the scattered rows' irfft)
     double *out;                 // [nport][nchan][nbin] (odd nbin, tau != 0: nbin - 1 bins, then 0)
+    // long rows: the unscattered rows, and each row's tau_n here for the
+    // convolution on the long transforms (0: unscattered); null: in LDS
+    double *taus_out;
 };
 hipError_t launch_gauss_port(const GaussArgs &a, hipStream_t st);
 

@@ -1399,16 +1399,6 @@ __device__ __forceinline__ double gp_raw(int j, int nbin, double mean, double si
     return exp(-0.5 * (z * z)) / (sigma * 2.5066282746310002);   // sqrt(2 pi)
 }
 
-// NumPy's complex reciprocal (loops CDOUBLE_reciprocal) of 1 + i b
-__device__ __forceinline__ double2 scat_recip(double b) {
-#pragma clang fp contract(off)
-    if (fabs(b) <= 1.0) {
-        const double r = b / 1.0, d = 1.0 + b * r;
-        return cmk(1.0 / d, -r / d);
-    }
-    const double r = 1.0 / b, d = 1.0 * r + b;
-    return cmk(r / d, -1.0 / d);
-}
 
 template <int KMAX, bool MX>
 __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
@@ -1461,7 +1451,11 @@ __global__ __launch_bounds__(kBlock) void k_gauss_port(GaussArgs a) {
         }
     }
     const double tau = prm[1];
-    if (tau != 0.0) {
+    if (a.taus_out) {
+        // long rows: tau_n for the convolution on the long transforms
+        if (threadIdx.x == 0)
+            a.taus_out[blockIdx.x] = tau != 0.0 ? tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]) : 0.0;
+    } else if (tau != 0.0) {
         // taus = (tau / nbin) * (freqs / nu_ref)**alpha; B_k = 1 / (1 + 2 pi i k tau_n)
         const double tn = tau / (double)nbin * pow(f / nu_ref, a.scat_index[p]);
         const bool odd = nbin & 1;

@@ -227,7 +227,8 @@ __global__ __launch_bounds__(kBlock) void k_lr_mid(LongRotArgs r, const double2 
     const int64_t row = blockIdx.y;
     const LongNoiseArgs &f = r.f, &b = r.b;
     const double2 *Z = Yf + row * f.M;
-    const double phi = r.phases[f.row0 + row];
+    const double phi = r.phases ? r.phases[f.row0 + row] : 0.0;
+    const double tn = r.taus ? r.taus[f.row0 + row] : 0.0;
     auto zk = [&](int64_t k) -> double2 {
         if (k >= f.n) k -= f.n;
         return cmul(Z[k], chirp(k, f.n));
@@ -243,7 +244,8 @@ __global__ __launch_bounds__(kBlock) void k_lr_mid(LongRotArgs r, const double2 
         } else {
             X = zk(k);
         }
-        double2 R = cmul(X, cexp2pi((double)k * phi));
+        double2 R = r.phases ? cmul(X, cexp2pi((double)k * phi)) : X;
+        if (tn != 0.0) R = cmul(R, scat_recip((2.0 * kPi * (double)k) * tn));
         if (k == 0 || (r.out_even && k == b.n)) R.y = 0.0;
         return R;
     };

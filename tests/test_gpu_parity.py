@@ -1097,6 +1097,35 @@ def test_gauss_portraits_match_reference(ppl, tmp_path):
                                   c["freqs"], c["nu_ref"])
 
 
+@pytest.mark.parametrize("nbin", [16384, 10002])
+def test_gauss_portraits_long_scattered_match_oracle(nbin):
+    """Scattered Gaussian portraits at even nbin past the LDS transforms
+    (round 6: the rows built per bin in LDS, then the convolution with
+    1 / (1 + 2 pi i k tau_n) on the long transforms) against the oracle's
+    gen_gaussian_portrait (pplib.py:900-960: rfft, scattering_portrait_FT,
+    irfft), in one batch with an unscattered portrait; scattered odd rows
+    past 4095 are refused (the reference's nbin - 1-bin irfft)."""
+    from pulseportraiture_amd import engine
+    import oracle as O
+    g = G.gauss()
+    c = G.gauss_case(g, "example_64x512")
+    prm = np.stack([c["params"]] * 2)
+    prm[0, 1] = 40.0                      # tau [bin] at nu_ref
+    prm[1, 1] = 0.0
+    freqs = np.stack([c["freqs"][::8], c["freqs"][::8] * 0.8])
+    nus = [c["nu_ref"], 1300.0]
+    batch = engine.gauss_portraits(c["code"], prm, [c["alpha"]] * 2, freqs,
+                                   nus, nbin).cpu().numpy()
+    for i in range(2):
+        ref = O.gen_gaussian_portrait(c["code"], prm[i], c["alpha"],
+                                      np.zeros(nbin), freqs[i], nus[i])
+        np.testing.assert_allclose(batch[i], ref, rtol=0,
+                                   atol=GAUSS_ATOL * np.abs(ref).max())
+    with pytest.raises(NotImplementedError):
+        engine.gauss_portraits(c["code"], prm[:1], [c["alpha"]], freqs[:1],
+                               nus[:1], 8193)
+
+
 # ------------------------------------------------------ harmonic cutoff ---
 def _cut_fraction(model):
     """Fraction of harmonics k_model_cut keeps (numpy restatement of its

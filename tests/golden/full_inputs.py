@@ -178,6 +178,10 @@ TOAS = [
     # round 6: rows past the LDS transforms (the guess profile's rFFT and
     # every row's on the long transforms)
     dict(name="long16384", nfile=1, nsub=3, nchan=16, nbin=16384, seed=208),
+    # and with the scattered .gmodel (its convolution on the long
+    # transforms), fitting scattering
+    dict(name="scatlong", nfile=1, nsub=2, nchan=16, nbin=16384, seed=210,
+         gmodel="scat", tau=2e-3, kw=dict(fit_scat=True)),
     # ---- the non-default branches of get_TOAs (round 3) ----------------
     # (a) configs[2]'s drop-in entry: fit_GM + fit_scat at 512 x 2048 with a
     # .gmodel whose TAU != 0 (tau guess from gparams, phase guess against

@@ -221,7 +221,7 @@ def _tim_tokens_match(lines, ref, skip_lines=(), nu0_tokens=True,
 
 
 BRANCHES = ["scatgm", "scatfix", "opts", "chan12", "tscr", "tnc", "tncscat",
-            "ncg", "nb1000", "nb1022", "nb1023"]
+            "ncg", "nb1000", "nb1022", "nb1023", "scatlong"]
 
 
 @pytest.mark.timeout(300)

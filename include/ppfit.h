@@ -495,8 +495,10 @@ int ppf_gauss_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t
  * <= 5) evaluated at freqs[p][n] as FITPACK splev (ext = 0), expanded on
  * eigvec [nbin_model][ncomp] plus mean_prof [nbin_model]; ncomp = 0 tiles
  * mean_prof.  nbin != nbin_model: scipy.signal.resample to nbin, then the
- * reference's half-bin rotate_portrait.  nbin_model and nbin are powers of
- * two in [32, 8192]; ncomp <= 64.  out: [nport][nchan][nbin] f64 (device). */
+ * reference's half-bin rotate_portrait.  nbin == nbin_model: any length;
+ * resampled: both even in [32, 8192] on the LDS transforms (round 6: any
+ * such length, was powers of two; else PPF_EUNSUP); ncomp <= 64.
+ * out: [nport][nchan][nbin] f64 (device). */
 int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_t nbin_model,
                               int32_t nbin, int32_t ncomp, int32_t nknots, int32_t degree,
                               const double *mean_prof, const double *eigvec,

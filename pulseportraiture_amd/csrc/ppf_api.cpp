@@ -1484,8 +1484,14 @@ int ppf_spline_portrait_batch(ppf_ctx *ctx, int32_t nport, int32_t nchan, int32_
                               const double *mean_prof, const double *eigvec, const double *knots,
                               const double *coefs, const double *freqs, double *out, void *stream) {
     if (!ctx) return PPF_EINVAL;
-    if (!pow2_in_range(nbin) || !pow2_in_range(nbin_model))
-        return fail(ctx, PPF_EUNSUP, "nbin=%d nbin_model=%d: powers of two in [32, 8192]", nbin,
+    // the model's own length: no transform (any nbin); resampled: two even
+    // lengths the LDS transforms take (scipy.signal.resample's Nyquist
+    // split as restated in k_spline_port assumes even lengths)
+    const bool same = nbin == nbin_model;
+    if (same ? nbin < 2
+             : !(nbin % 2 == 0 && nbin_model % 2 == 0 && nbin_supported(nbin) && nbin_supported(nbin_model)))
+        return fail(ctx, PPF_EUNSUP,
+                    "nbin=%d nbin_model=%d: the model's own length, or both even in [32, 8192]", nbin,
                     nbin_model);
     if (nport < 0 || nchan < 1 || ncomp < 0 || ncomp > ppf::kSplineMaxComp || degree < 0 ||
         degree > ppf::kSplineMaxDeg || (ncomp > 0 && nknots < 2 * degree + 2))

@@ -254,7 +254,12 @@ SPLINES = [("same", 64, 1100.0, 800.0, None), ("n512", 48, 1150.0, 700.0, 512),
            ("up1024", 64, 1100.0, 800.0, 1024), ("up4096", 32, 1200.0, 600.0,
                                                    4096),
            ("down256", 64, 1100.0, 800.0, 256), ("down64", 100, 1120.0, 760.0,
-                                                 64)]
+                                                 64),
+           # round 6: resampled to lengths that are not powers of two (the
+           # mixed-radix LDS transforms)
+           ("n1000", 64, 1100.0, 800.0, 1000), ("n1536", 48, 1150.0, 700.0,
+                                                1536),
+           ("down300", 64, 1100.0, 800.0, 300)]
 
 
 def toa_inputs(c):

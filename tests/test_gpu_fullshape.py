@@ -589,7 +589,8 @@ def test_spline_portrait_matches_reference(name):
     (pplib.py:966-990, 3060-3096) on the device (k_spline_port) against the
     reference's portraits: splev per channel, eigenvector expansion and
     scipy.signal.resample + half-bin rotation for nbin != 512 (up to 4096,
-    down to 64); "mean" is the ncomp = 0 branch resampled to 1024 bins.
+    down to 64; round 6: 1000, 1536 and 300 bins on the mixed-radix
+    transforms); "mean" is the ncomp = 0 branch resampled to 1024 bins.
     Tolerance 1e-11 of the portrait's peak (fp64 FFT rounding)."""
     from pulseportraiture_amd import pplib
     g = F.case("spline", "gen")

@@ -593,6 +593,13 @@ def resid_chi2_rows(rows, phases, model_rows, model_index, scales, errs, dof,
         raise ValueError("need one phase / model index / scale / err per row")
     if n and (int(mi.min()) < 0 or int(mi.max()) >= m.shape[0]):
         raise ValueError("model index out of range")
+    if not _noise_batch_len_ok(nbin):
+        # rows past the LDS transforms (round 6): the rotation on the long
+        # transforms (ppf_rotate_long, full nbin as k_resid_chi2's), the
+        # residual sum of squares on the stream
+        rot = rotate_rows(r2, ph, dev)
+        res = (rot - sc.unsqueeze(-1) * m[mi.long()]) / er.unsqueeze(-1)
+        return (res * res).sum(dim=-1) / float(dof)
     out = torch.empty(n, dtype=torch.float64, device=dev)
     ctx = _lib.context(dev.index)
     rc = _lib.load().ppf_resid_chi2_batch(

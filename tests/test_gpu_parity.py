@@ -1097,6 +1097,27 @@ def test_gauss_portraits_match_reference(ppl, tmp_path):
                                   c["freqs"], c["nu_ref"])
 
 
+@pytest.mark.parametrize("nbin", [16384, 8193])
+def test_resid_chi2_long_rows_match_oracle(nbin):
+    """The zap / show_fit per-channel reduced chi^2 (pplib.py:754-779 after
+    rotate_portrait_full) at nbin past the LDS transforms (round 6: the
+    rotation on the long transforms) against the oracle, rtol 1e-12."""
+    from pulseportraiture_amd import engine
+    import oracle as O
+    rng = np.random.default_rng(nbin)
+    rows = rng.normal(size=(5, nbin))
+    mrows = rng.normal(size=(2, nbin))
+    phs = rng.uniform(-0.5, 0.5, 5)
+    mi = np.array([0, 1, 0, 1, 1], dtype=np.int32)
+    sc = rng.uniform(0.5, 2.0, 5)
+    er = rng.uniform(0.5, 1.5, 5)
+    got = engine.resid_chi2_rows(rows.astype(np.float32), phs, mrows, mi, sc,
+                                 er, nbin - 2).cpu().numpy()
+    want = O.channel_red_chi2s(rows.astype(np.float32).astype(np.float64),
+                               phs, mrows[mi], sc, er, nbin - 2)
+    np.testing.assert_allclose(got, want, rtol=1e-12)
+
+
 @pytest.mark.parametrize("nbin", [16384, 10002])
 def test_gauss_portraits_long_scattered_match_oracle(nbin):
     """Scattered Gaussian portraits at even nbin past the LDS transforms

@@ -220,6 +220,9 @@ hipError_t launch_gflag(int nsub, int nchan, const uint8_t *needx, const int32_t
     return hipGetLastError();
 }
 
+#ifndef PPF_TRINIT_ZERO
+#define PPF_TRINIT_ZERO 0   // 1: k_tr_init zeroes the moment fits' stats slots
+#endif
 // ===========================================================================
 // k_tr_init: one wave per sub-integration (4 per workgroup)
 // ===========================================================================
@@ -348,11 +351,14 @@ __global__ __launch_bounds__(kBlock) void k_tr_init(SolveArgs a) {
             const double nu = fr[n];
             dp[2 * n + 0] = kDconst * (pow(nu, -2.0) - nuDM2) / P;
             dp[2 * n + 1] = kDconst * kDconst * (pow(nu, -4.0) - nuGM4) / P;
-            // S_n (slot 6) is stored with C, C', C'' by k_tr_mom
-            for (int q = 0; q < 2; ++q) {
-                double *d = st + ((int64_t)q * a.nchan + n) * 10;
-                for (int j = 0; j < 10; ++j) d[j] = 0.0;
-            }
+            // S_n (slot 6) is stored with C, C', C'' by k_tr_mom, and (round
+            // 6) the scattering slots' zeros with them: zeroing both slots
+            // here wrote nsub x nchan x 160 B (840 MB, 0.3 ms at C2)
+            if (PPF_TRINIT_ZERO)
+                for (int q = 0; q < 2; ++q) {
+                    double *d = st + ((int64_t)q * a.nchan + n) * 10;
+                    for (int j = 0; j < 10; ++j) d[j] = 0.0;
+                }
         }
     }
 }
@@ -1512,6 +1518,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(PPF_TRMOM_WP
             const double C = F.x, Cp = -kTwoPi * K1.y, Cpp = -kTwoPi * kTwoPi * K2.x;
             double *sn = st + (int64_t)n * 10;
             sn[0] = C; sn[1] = Cp; sn[2] = Cpp; sn[6] = Sn;
+            if (!PPF_TRINIT_ZERO) sn[3] = sn[4] = sn[5] = sn[7] = sn[8] = sn[9] = 0.0;
             const double iS = 1.0 / Sn;
             const double dph[3] = {1.0, d1, d2};
             const double hn = -2.0 * (C * Cpp + Cp * Cp) * iS;

@@ -964,6 +964,17 @@ __global__ __launch_bounds__(kBlock) void k_dsum_wn(DsumArgs a) {
 // dedispersed mean profile against the mean model profile, then
 // phase_transform to nu_fit_DM (pplib.py:2688-2712).
 // ===========================================================================
+// the block-partial sums of k_guess (fixed order, so bit-identical either
+// way) unrolled 8 deep: their loads independent, in flight together instead
+// of one latency each (PPF_GUESS_UNROLL 0: as through round 6's first builds)
+#ifndef PPF_GUESS_UNROLL
+#define PPF_GUESS_UNROLL 1
+#endif
+#if PPF_GUESS_UNROLL
+#define PPF_GU _Pragma("unroll 8")
+#else
+#define PPF_GU _Pragma("unroll 1")
+#endif
 template <bool MX, int CZL = 0, bool GS = false>
 __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // lds: z[max(rfft_len, czP)] (packed profile, FFT in place; then the
@@ -984,12 +995,14 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     if (tid == 0) {
         double w0 = 0.0, w1 = 0.0, w2 = 0.0;
         if (fused) {
+            PPF_GU
             for (int b = 0; b < a.nblk; ++b) {
                 w0 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 0];
                 w1 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 1];
                 w2 += a.gwx[((int64_t)s * a.nblk + b) * 3 + 2];
             }
         } else {
+            PPF_GU
             for (int b = 0; b < a.nblkd; ++b) {
                 w0 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 0];
                 w1 += a.gw[((int64_t)s * a.nblkd + b) * 2 + 1];
@@ -1003,11 +1016,13 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
         // (odd nbin: z_j = p_j)
         for (int j = tid; odd && j < a.nbin; j += kBlock) {
             double pj = 0.0;
+            PPF_GU
             for (int b = 0; b < a.nblkd; ++b) pj += a.gP[((int64_t)s * a.nblkd + b) * a.nbin + j];
             z[j] = cmk(pj, 0.0);
         }
         for (int j = tid; !odd && j < N; j += kBlock) {
             double pe = 0.0, po = 0.0;
+            PPF_GU
             for (int b = 0; b < a.nblkd; ++b) {
                 const double *pp = a.gP + ((int64_t)s * a.nblkd + b) * a.nbin;
                 pe += pp[2 * j];
@@ -1022,8 +1037,10 @@ __global__ __launch_bounds__(kBlock) void k_guess(GuessArgs a) {
     // R_k of the fused partials (k < NL; 0 above: past every channel's cutoff)
     auto fused_bin = [&](int k) {
         double2 r = cmk(0.0, 0.0);
-        if (k >= 1 && k < NL)
+        if (k >= 1 && k < NL) {
+            PPF_GU
             for (int b = 0; b < a.nblk; ++b) r = cadd(r, a.gpart[((int64_t)s * a.nblk + b) * NL + k]);
+        }
         return r;
     };
     double pw[1] = {0.0};

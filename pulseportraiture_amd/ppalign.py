@@ -340,8 +340,10 @@ def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
             device=dev)
         dc["nu_outs"] = torch.full((len(multi), 3), float("nan"), dtype=f64,
                                    device=dev)
-    phases = torch.zeros((S, nchan), dtype=f64, device=dev)
-    weights = torch.zeros((S, nchan), dtype=f64, device=dev)
+    # every row fitted in the one batch (the usual case): its phases and
+    # weights are the iteration's, with no zero-filled tensors to place them
+    # in (two fill launches fewer per iteration)
+    phases = weights = None
     if len(multi):
         rows = R.data[:, 0] if len(multi) == S else \
             R.data[torch.as_tensor(multi, device=dev), 0]
@@ -349,9 +351,14 @@ def _fit_and_weights(R, model_port, fit_dm, nbin, dev):
         if len(multi) == S:
             phases, weights = ph, wt
         else:
+            phases = torch.zeros((S, nchan), dtype=f64, device=dev)
+            weights = torch.zeros((S, nchan), dtype=f64, device=dev)
             mi = torch.as_tensor(multi, device=dev)
             phases[mi] = ph
             weights[mi] = wt
+    if phases is None:
+        phases = torch.zeros((S, nchan), dtype=f64, device=dev)
+        weights = torch.zeros((S, nchan), dtype=f64, device=dev)
     if getattr(R, "_dup_dev", None) is not None:
         # rows with duplicate model channels: fit in slot order against the
         # gathered template rows, then place each model channel's LAST slot
@@ -443,10 +450,11 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
                 phases, weights = _fit_and_weights(R, model_port, fit_dm,
                                                    nbin, dev)
                 for ipol in range(npol):
-                    w = torch.zeros_like(wsum)
+                    # the weight sum once (ipol 0); the other pols' into a
+                    # scratch that is dropped
+                    w = wsum if ipol == 0 else torch.zeros_like(wsum)
                     engine.align_accum(R.data[:, ipol], phases, weights,
-                                       out[ipol], wsum if ipol == 0 else w,
-                                       dev=dev)
+                                       out[ipol], w, dev=dev)
                 raise_pending(R)
         except Exception as exc:        # raised on every rank, below
             if not comm:
@@ -460,7 +468,7 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False,
         # channels with weight: divided by it; the rest (all zero) by 1 --
         # the same values as out[:, good] /= wsum[good], without the boolean
         # indexing's device-to-host round trip in every iteration
-        out /= torch.where(wsum > 0, wsum, torch.ones_like(wsum))[None, :, None]
+        out /= torch.where(wsum > 0, wsum, 1.0)[None, :, None]
         model_port = out[0]             # the next template stays in HBM
         niter -= 1
         count += 1
